@@ -1,0 +1,287 @@
+// C ABI implementation (include/fsdkr/fsdkr.h): context, device buffers,
+// kernel launch sequencing and per-kernel HIP-event timing.
+#include "fsdkr/fsdkr.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ctx.hpp"
+#include "kernels.h"
+
+using namespace fsdkr;
+
+// ------------------------------------------------------------------ context ---
+namespace fsdkr {
+
+void Ctx::fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  err = buf;
+}
+
+int Ctx::hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return FSDKR_OK;
+  fail("%s: %s", what, hipGetErrorString(e));
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return FSDKR_E_OOM;
+  return FSDKR_E_HIP;
+}
+
+void* Ctx::buf(const char* name, size_t bytes) {
+  DevBuf& b = bufs[name];
+  if (b.bytes >= bytes && b.ptr) return b.ptr;
+  if (b.ptr) (void)hipFree(b.ptr);
+  b.ptr = nullptr;
+  b.bytes = 0;
+  size_t want = bytes < 256 ? 256 : bytes;
+  if (hipMalloc(&b.ptr, want) != hipSuccess) {
+    b.ptr = nullptr;
+    return nullptr;
+  }
+  b.bytes = want;
+  return b.ptr;
+}
+
+void Ctx::mark(const char* name, bool begin) {
+  if (!timing) return;
+  hipEvent_t ev;
+  if (hipEventCreate(&ev) != hipSuccess) return;
+  (void)hipEventRecord(ev, stream);
+  if (begin) {
+    pending.push_back({name, ev, nullptr});
+  } else if (!pending.empty() && pending.back().e1 == nullptr) {
+    pending.back().e1 = ev;
+  } else {
+    (void)hipEventDestroy(ev);
+  }
+}
+
+int Ctx::sync() {
+  int rc = hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+  for (auto& p : pending) {
+    if (p.e1) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, p.e0, p.e1) == hipSuccess) {
+        auto& t = times[p.name];
+        t.ms += ms;
+        t.launches += 1;
+      }
+      (void)hipEventDestroy(p.e1);
+    }
+    (void)hipEventDestroy(p.e0);
+  }
+  pending.clear();
+  return rc;
+}
+
+uint32_t choose_window(uint32_t ebits) {
+  // minimise squarings + window multiplies + table build
+  uint32_t best_w = 1;
+  double best = 1e30;
+  for (uint32_t w = 1; w <= 6; ++w) {
+    double cost = (double)ebits + (double)((ebits + w - 1) / w) + (double)(1u << w);
+    if (cost < best) {
+      best = cost;
+      best_w = w;
+    }
+  }
+  return best_w;
+}
+
+// Runs mod_setup + modexp on device-resident operands.
+int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
+                      uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,
+                      uint32_t n_mod, uint32_t* d_out) {
+  const int KD = shape_digits(k32);
+  if (!KD) {
+    c->fail("unsupported modulus width %u limbs", k32);
+    return FSDKR_E_UNSUPPORTED;
+  }
+  if (count == 0) return FSDKR_OK;
+  if (exp_bits == 0) exp_bits = 1;
+  const uint32_t w = choose_window(exp_bits);
+  const uint32_t nwin = (exp_bits + w - 1) / w;
+  const size_t stride = 3 * (size_t)KD + 4;
+  uint32_t* d_consts = (uint32_t*)c->buf("consts", sizeof(uint32_t) * stride * n_mod);
+  uint32_t* d_table = (uint32_t*)c->buf("table", sizeof(uint32_t) * (size_t)count * ((size_t)1 << w) * KD);
+  if (!d_consts || !d_table) {
+    c->fail("device allocation failed (%u instances, window %u)", count, w);
+    return FSDKR_E_OOM;
+  }
+  c->mark("mod_setup", true);
+  int rc = c->hip_check(mod_setup(k32, d_mods, n_mod, d_consts, c->stream), "mod_setup launch");
+  c->mark("mod_setup", false);
+  if (rc) return rc;
+  ModexpArgs a;
+  a.base = d_base;
+  a.exps = d_exp;
+  a.exp_limbs = exp_limbs;
+  a.nwin = nwin;
+  a.window = w;
+  a.mod_idx = d_mod_idx;
+  a.consts = d_consts;
+  a.out = d_out;
+  a.table = d_table;
+  a.count = count;
+  c->mark("modexp", true);
+  rc = c->hip_check(modexp(k32, a, c->stream), "modexp launch");
+  c->mark("modexp", false);
+  return rc;
+}
+
+}  // namespace fsdkr
+
+// ---------------------------------------------------------------- C ABI -------
+extern "C" {
+
+int fsdkr_device_available(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n > 0 ? 1 : 0;
+}
+
+int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out) {
+  if (!out) return FSDKR_E_ARG;
+  *out = nullptr;
+  Ctx* c = new (std::nothrow) Ctx();
+  if (!c) return FSDKR_E_OOM;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    delete c;
+    return FSDKR_E_HIP;
+  }
+  int dev = cfg ? cfg->device : -1;
+  if (dev >= 0) {
+    if (dev >= n || hipSetDevice(dev) != hipSuccess) {
+      delete c;
+      return FSDKR_E_ARG;
+    }
+  } else {
+    (void)hipGetDevice(&dev);
+  }
+  c->device = dev;
+  c->timing = cfg && (cfg->flags & FSDKR_CFG_TIMING);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return FSDKR_E_HIP;
+  }
+  *out = reinterpret_cast<fsdkr_ctx*>(c);
+  return FSDKR_OK;
+}
+
+void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return;
+  (void)c->sync();
+  for (auto& kv : c->bufs)
+    if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* fsdkr_last_error(const fsdkr_ctx* ctx) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  return c ? c->err.c_str() : "null context";
+}
+
+int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* base,
+                       const uint32_t* exp, uint32_t exp_limbs, const uint32_t* mod_idx, const uint32_t* mods,
+                       uint32_t n_mod, uint32_t* out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!base || !exp || !mod_idx || !mods || !out || n_mod == 0 || exp_limbs == 0) {
+    c->fail("fsdkr_modexp_batch: null pointer or empty table");
+    return FSDKR_E_ARG;
+  }
+  if (!shape_digits(mod_limbs)) {
+    c->fail("fsdkr_modexp_batch: unsupported modulus width %u limbs", mod_limbs);
+    return FSDKR_E_UNSUPPORTED;
+  }
+  for (uint32_t m = 0; m < n_mod; ++m) {
+    if ((mods[(size_t)m * mod_limbs] & 1u) == 0) {
+      c->fail("fsdkr_modexp_batch: modulus %u is even", m);
+      return FSDKR_E_ARG;
+    }
+  }
+  uint32_t exp_bits = 0;
+  for (uint32_t i = 0; i < count; ++i) {
+    if (mod_idx[i] >= n_mod) {
+      c->fail("fsdkr_modexp_batch: mod_idx[%u]=%u out of range", i, mod_idx[i]);
+      return FSDKR_E_ARG;
+    }
+    const uint32_t* e = exp + (size_t)i * exp_limbs;
+    for (int k = (int)exp_limbs - 1; k >= 0; --k) {
+      if (e[k]) {
+        uint32_t b = 32u * (uint32_t)k + 32u - (uint32_t)__builtin_clz(e[k]);
+        if (b > exp_bits) exp_bits = b;
+        break;
+      }
+    }
+  }
+  const size_t nb = sizeof(uint32_t) * (size_t)count * mod_limbs;
+  const size_t ne = sizeof(uint32_t) * (size_t)count * exp_limbs;
+  uint32_t* d_base = (uint32_t*)c->buf("mx_base", nb);
+  uint32_t* d_exp = (uint32_t*)c->buf("mx_exp", ne);
+  uint32_t* d_idx = (uint32_t*)c->buf("mx_idx", sizeof(uint32_t) * count);
+  uint32_t* d_mods = (uint32_t*)c->buf("mx_mods", sizeof(uint32_t) * (size_t)n_mod * mod_limbs);
+  uint32_t* d_out = (uint32_t*)c->buf("mx_out", nb);
+  if (!d_base || !d_exp || !d_idx || !d_mods || !d_out) {
+    c->fail("fsdkr_modexp_batch: device allocation failed");
+    return FSDKR_E_OOM;
+  }
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_base, base, nb, hipMemcpyHostToDevice, c->stream), "H2D base"))) return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_exp, exp, ne, hipMemcpyHostToDevice, c->stream), "H2D exp"))) return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_idx, mod_idx, sizeof(uint32_t) * count, hipMemcpyHostToDevice, c->stream),
+                         "H2D idx")))
+    return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_mods, mods, sizeof(uint32_t) * (size_t)n_mod * mod_limbs,
+                                        hipMemcpyHostToDevice, c->stream),
+                         "H2D mods")))
+    return rc;
+  rc = run_modexp_device(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_idx, d_mods, n_mod, d_out);
+  if (rc) return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(out, d_out, nb, hipMemcpyDeviceToHost, c->stream), "D2H out"))) return rc;
+  return c->sync();
+}
+
+int fsdkr_modexp_batch_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* d_base,
+                              const uint32_t* d_exp, uint32_t exp_limbs, uint32_t exp_bits,
+                              const uint32_t* d_mod_idx, const uint32_t* d_mods, uint32_t n_mod, uint32_t* d_out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!d_base || !d_exp || !d_mod_idx || !d_mods || !d_out || n_mod == 0 || exp_limbs == 0 ||
+      exp_bits > 32u * exp_limbs) {
+    c->fail("fsdkr_modexp_batch_device: bad argument");
+    return FSDKR_E_ARG;
+  }
+  int rc = run_modexp_device(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_mod_idx, d_mods, n_mod, d_out);
+  if (rc) return rc;
+  return c->sync();
+}
+
+int fsdkr_kernel_time(const fsdkr_ctx* ctx, const char* name, double* ms, uint32_t* launches) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  if (!c || !name) return FSDKR_E_ARG;
+  auto it = c->times.find(name);
+  if (ms) *ms = (it == c->times.end()) ? 0.0 : it->second.ms;
+  if (launches) *launches = (it == c->times.end()) ? 0u : it->second.launches;
+  return FSDKR_OK;
+}
+
+void fsdkr_kernel_time_reset(fsdkr_ctx* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c) c->times.clear();
+}
+
+}  // extern "C"

@@ -1,0 +1,225 @@
+// Batched modular exponentiation on gfx950:  out[i] = base[i]^exp[i] mod N[mod_idx[i]].
+//
+// Replaces the GMP mpz_powm behind curv BigInt::mod_pow on the collect() hot
+// path (zk_pdl_with_slack.rs:129-157 via commitment_unknown_order :170-188;
+// range_proofs.rs:129-148; ring_pedersen_proof.rs:144-148; zk-paillier
+// NiCorrectKeyProof/CompositeDLogProof verify called at refresh_message.rs:376-378,
+// 401-425) and r^N mod N^2 of Paillier encryption (refresh_message.rs:72-84).
+//
+// One instance = G lanes (mont29.hpp); 256-thread blocks of 256/G instances.
+// Fixed-window left-to-right exponentiation (window w chosen by the host), the
+// window table lives in a per-instance global scratch slab, the streamed row
+// operand of every Montgomery product in LDS.
+#include "mont29.hpp"
+#include "kernels.h"
+
+namespace fsdkr {
+
+template <int KD, int G>
+__device__ __forceinline__ void lds_put(uint32_t* stream, const uint32_t* d, int g) {
+  constexpr int L = KD / G;
+#pragma unroll
+  for (int j = 0; j < L; ++j) stream[g * L + j] = d[j];
+}
+
+// consts[m] = {N digits | R mod N | R^2 mod N | ninv}   (STRIDE = 3*KD + 4 words)
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __restrict__ mods, uint32_t n_mod,
+                                                          uint32_t* __restrict__ consts) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t m = blockIdx.x * IPB + li;
+  if (m >= n_mod) return;
+  uint32_t* stream = lds + li * KD;
+  const uint32_t* N = mods + (size_t)m * K32;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = digit_of(N, K32, g * L + j);
+  const uint32_t n0 = N[0];
+  uint32_t inv = n0;
+#pragma unroll
+  for (int it = 0; it < 5; ++it) inv *= 2u - n0 * inv;
+  M.ninv = (0u - inv) & M29;
+  int hb = -1;
+#pragma unroll
+  for (int j = 0; j < L; ++j)
+    if (M.n[j]) hb = (g * L + j) * 29 + 31 - __builtin_clz(M.n[j]);
+  hb = group_max<G>(hb);
+  uint32_t y[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) y[j] = ((g * L + j) == hb / 29) ? (1u << (hb % 29)) : 0u;  // 2^(bitlen-1) < N
+  const int nd1 = 29 * KD - hb;                 // -> 2^(29 KD) = R mod N
+  for (int k = 0; k < nd1; ++k) M.dbl(y);
+  uint32_t* out = consts + (size_t)m * (3 * KD + 4);
+#pragma unroll
+  for (int j = 0; j < L; ++j) out[KD + g * L + j] = y[j];
+  // R^2 mod N: 2^c * R (Montgomery form of 2^c) squared s times, c * 2^s = 29 KD
+  constexpr int TWO_S = ((29 * KD) % 16 == 0) ? 16 : ((29 * KD) % 8 == 0) ? 8 : ((29 * KD) % 4 == 0) ? 4 : ((29 * KD) % 2 == 0) ? 2 : 1;
+  constexpr int S = (TWO_S == 16) ? 4 : (TWO_S == 8) ? 3 : (TWO_S == 4) ? 2 : (TWO_S == 2) ? 1 : 0;
+  constexpr int C = 29 * KD / TWO_S;
+  for (int k = 0; k < C; ++k) M.dbl(y);
+  for (int s = 0; s < S; ++s) {
+    lds_put<KD, G>(stream, y, g);
+    __builtin_amdgcn_wave_barrier();
+    M.mul(y, y, stream);
+    __builtin_amdgcn_wave_barrier();
+  }
+  M.carry_exact(y);
+  M.sub_if_ge(y);
+  M.sub_if_ge(y);
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    out[g * L + j] = M.n[j];
+    out[2 * KD + g * L + j] = y[j];
+  }
+  if (g == 0) out[3 * KD] = M.ninv;
+}
+
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = 3 * KD + 4;
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * IPB + li;
+  if (inst >= a.count) return;
+  uint32_t* stream = lds + li * KD;
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
+  M.ninv = C[3 * KD];
+  const uint32_t w = a.window;
+  const uint32_t tsize = 1u << w;
+  uint32_t* T = a.table + (size_t)inst * tsize * KD;
+  const uint32_t* E = a.exps + (size_t)inst * a.exp_limbs;
+
+  uint32_t acc[L];
+  const uint32_t* B = a.base + (size_t)inst * K32;
+#pragma unroll
+  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, K32, g * L + j);
+#pragma unroll
+  for (int j = 0; j < L; ++j) T[g * L + j] = C[KD + g * L + j];             // T[0] = R mod N
+  const uint32_t nwin = a.nwin;
+  auto digit = [&](uint32_t k) -> uint32_t {
+    const uint32_t p = (nwin - 1 - k) * w;
+    const uint32_t lo = p >> 5, sh = p & 31;
+    const uint32_t v0 = (lo < a.exp_limbs) ? E[lo] : 0u;
+    const uint32_t v1 = (lo + 1 < a.exp_limbs) ? E[lo + 1] : 0u;
+    return (uint32_t)(mk64(v0, v1) >> sh) & (tsize - 1);
+  };
+  // Every Montgomery product of the exponentiation is acc <- acc * stream, issued
+  // from this ONE site so the unrolled product body exists once in the I-cache.
+  //   step 0                      : stream = R^2            -> acc = xm, T[1] = xm
+  //   step 1 .. tsize-2           : stream = T[1]           -> T[step+1]
+  //   then per window k=1..nwin-1 : w x (stream = acc), then stream = T[d_k]
+  //   last                        : stream = 1 (leave Montgomery form)
+  const uint32_t n_build = tsize - 1;
+  const uint32_t n_steps = n_build + (nwin - 1) * (w + 1) + 1;
+  uint32_t k = 1, sub = 0;
+  for (uint32_t st = 0; st < n_steps; ++st) {
+    const uint32_t* src = nullptr;
+    bool from_acc = false, one = false;
+    if (st == n_build) {                                                    // start of the ladder
+      const uint32_t d0 = digit(0);
+#pragma unroll
+      for (int j = 0; j < L; ++j) acc[j] = T[(size_t)d0 * KD + g * L + j];
+    }
+    if (st == 0) {
+      src = C + 2 * KD;
+    } else if (st < n_build) {
+      src = T + KD;
+    } else if (st == n_steps - 1) {
+      one = true;
+    } else {
+      if (sub < w) from_acc = true;
+      else src = T + (size_t)digit(k) * KD;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (from_acc) {
+      lds_put<KD, G>(stream, acc, g);
+    } else if (one) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
+    } else {
+#pragma unroll
+      for (int j = 0; j < L; ++j) stream[g * L + j] = src[g * L + j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    M.mul(acc, acc, stream);
+    if (st < n_build) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) T[(size_t)(st + 1) * KD + g * L + j] = acc[j];
+    } else if (st < n_steps - 1) {
+      if (++sub == w + 1) { sub = 0; ++k; }
+    }
+  }
+  M.carry_exact(acc);
+  M.sub_if_ge(acc);
+  __builtin_amdgcn_wave_barrier();
+  lds_put<KD, G>(stream, acc, g);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* O = a.out + (size_t)inst * K32;
+  constexpr int LO = K32 / G;
+#pragma unroll
+  for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
+}
+
+// ---- host-side launchers -------------------------------------------------------
+template <int KD, int G, int K32>
+static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
+  constexpr int IPB = BLOCK / G;
+  const uint32_t blocks = (n_mod + IPB - 1) / IPB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((mod_setup_kernel<KD, G, K32>), dim3(blocks), dim3(BLOCK), 0, st, mods, n_mod, consts);
+  return hipGetLastError();
+}
+template <int KD, int G, int K32>
+static hipError_t launch_modexp(const ModexpArgs& a, hipStream_t st) {
+  constexpr int IPB = BLOCK / G;
+  const uint32_t blocks = (a.count + IPB - 1) / IPB;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((modexp_kernel<KD, G, K32>), dim3(blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+int shape_digits(uint32_t k32) {
+  switch (k32) {
+    case 64: return 72;
+    case 96: return 108;
+    case 128: return 144;
+    case 192: return 216;
+    default: return 0;
+  }
+}
+
+hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
+  switch (k32) {
+    case 64: return launch_setup<72, 2, 64>(mods, n_mod, consts, st);
+    case 96: return launch_setup<108, 4, 96>(mods, n_mod, consts, st);
+    case 128: return launch_setup<144, 4, 128>(mods, n_mod, consts, st);
+    case 192: return launch_setup<216, 4, 192>(mods, n_mod, consts, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
+  switch (k32) {
+    case 64: return launch_modexp<72, 2, 64>(a, st);
+    case 96: return launch_modexp<108, 4, 96>(a, st);
+    case 128: return launch_modexp<144, 4, 128>(a, st);
+    case 192: return launch_modexp<216, 4, 192>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace fsdkr

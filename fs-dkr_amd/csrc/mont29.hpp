@@ -1,0 +1,210 @@
+// Lane-distributed radix-2^29 Montgomery arithmetic for gfx950 (CDNA4, wave64).
+//
+// Why radix 2^29: on gfx950 v_mad_u64_u32 and every carry-writing add issue at
+// half rate (tools/microbench, profiles/r01_intrates.jsonl), so a radix-2^32
+// CIOS costs two half-rate instructions per MAC.  With 29-bit digits a product
+// is < 2^58 and a 64-bit column accumulator absorbs 31 rows of products, so the
+// inner loop is ONE v_mad_u64_u32 per MAC with no carry chain; carries are
+// resolved by a cheap parallel normalisation every 18 rows.
+//
+// Layout: a KD-digit integer is owned by G consecutive lanes (G in {2,4}, one
+// DPP quad); lane g holds digits [g*L, g*L+L), L = KD/G.  Row-oriented CIOS:
+// row i broadcasts digit a_i of the streamed operand (LDS) to the group, every
+// lane adds a_i*b and m_i*n into its L column accumulators, lane 0 folds the
+// retired column's carry and the accumulator shifts one digit down (register
+// slot rotation inside an L-row unrolled cycle plus one 64-bit DPP move).
+//
+// Values are kept "almost Montgomery": R = 2^(29*KD) > 4N, operands < 2N with
+// digits <= 2^29+127, outputs < 2N; exact reduction happens once per modexp.
+//
+// This replaces GMP mpz_powm/mpz_mul/mpz_mod behind curv BigInt::mod_pow and
+// BigInt::mod_mul (curv-kzen 0.10, /root/reference/Cargo.toml:33,41-44) on the
+// collect() hot path (/root/reference/src/refresh_message.rs:321-467).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <utility>
+
+namespace fsdkr {
+
+constexpr uint32_t M29 = (1u << 29) - 1;
+
+// ---- intra-quad DPP helpers (quad_perm) --------------------------------------
+template <int G>
+__device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
+  if constexpr (G == 1) return v;
+  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
+  else return __builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);                       // [0,0,0,0]
+}
+template <int G>
+__device__ __forceinline__ uint32_t bcast_top(uint32_t v) {
+  if constexpr (G == 1) return v;
+  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
+  else return __builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, false);                       // [3,3,3,3]
+}
+// raw value of lane g+1 (top lane reads itself: caller masks)
+template <int G>
+__device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
+  if constexpr (G == 1) return v;
+  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
+  else return __builtin_amdgcn_mov_dpp((int)v, 0xF9, 0xF, 0xF, false);                       // [1,2,3,3]
+}
+// raw value of lane g-1 (lane 0 reads itself: caller masks)
+template <int G>
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {
+  if constexpr (G == 1) return v;
+  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
+  else return __builtin_amdgcn_mov_dpp((int)v, 0x90, 0xF, 0xF, false);                       // [0,0,1,2]
+}
+// group-wide max over the G lanes
+template <int G>
+__device__ __forceinline__ int group_max(int v) {
+  if constexpr (G >= 2) v = max(v, (int)__builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  if constexpr (G == 4) v = max(v, (int)__builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  return v;
+}
+
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+template <int KD, int G>
+struct Mont29 {
+  static constexpr int L = KD / G;
+  static_assert(KD % G == 0, "KD must split evenly over the group");
+  // normalisation points inside one L-row cycle: at most 18 rows apart (bound: 31)
+  static constexpr int NSTEP = (L + 1) / 2 <= 18 ? (L + 1) / 2 : (L + 2) / 3;
+
+  uint32_t n[L];
+  uint32_t ninv;      // -N^-1 mod 2^29
+  int g;
+  uint32_t m_lane0;   // ~0 in group lane 0
+  uint32_t m_first;   // ~0 unless lane 0   (masks dpp_prev)
+  uint32_t m_top;     // ~0 unless top lane (masks dpp_next)
+
+  __device__ __forceinline__ void init_lane(int g_) {
+    g = g_;
+    m_lane0 = (g == 0) ? 0xFFFFFFFFu : 0u;
+    m_first = (g == 0) ? 0u : 0xFFFFFFFFu;
+    m_top = (g == G - 1) ? 0u : 0xFFFFFFFFu;
+  }
+
+  __device__ __forceinline__ uint64_t prev64(uint64_t v) const {
+    return mk64(dpp_prev<G>((uint32_t)v) & m_first, dpp_prev<G>((uint32_t)(v >> 32)) & m_first);
+  }
+  __device__ __forceinline__ uint64_t next64(uint64_t v) const {
+    return mk64(dpp_next<G>((uint32_t)v) & m_top, dpp_next<G>((uint32_t)(v >> 32)) & m_top);
+  }
+
+  // one parallel carry step over the logical columns (slot of logical j = (j+RHO)%L)
+  template <int RHO>
+  __device__ __forceinline__ void norm_step(uint64_t* acc) const {
+    const uint64_t cin = prev64(acc[(L - 1 + RHO) % L] >> 29);
+#pragma unroll
+    for (int j = L - 1; j > 0; --j) {
+      const int s = (j + RHO) % L, sp = (j - 1 + RHO) % L;
+      acc[s] = (uint64_t)((uint32_t)acc[s] & M29) + (acc[sp] >> 29);
+    }
+    acc[RHO % L] = (uint64_t)((uint32_t)acc[RHO % L] & M29) + cin;
+  }
+
+  // one CIOS row at rotation R (logical column j lives in slot (j+R)%L)
+  template <int R>
+  __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, uint32_t ai) const {
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[(j + R) % L] += (uint64_t)ai * b[j];
+    constexpr int s0 = R % L, s1 = (R + 1) % L;
+    const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[(j + R) % L] += (uint64_t)m * n[j];
+    const uint64_t c = acc[s0] >> 29;
+    acc[s1] += mk64((uint32_t)c & m_lane0, (uint32_t)(c >> 32) & m_lane0);
+    acc[s0] = next64(acc[s0]);
+    if constexpr (((R + 1) % NSTEP == 0) || (R + 1 == L)) norm_step<(R + 1) % L>(acc);
+  }
+
+  template <int... Rs>
+  __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* arow,
+                                        std::integer_sequence<int, Rs...>) const {
+    (row<Rs>(acc, b, arow[Rs]), ...);
+  }
+
+  // out = a * b / R  (almost Montgomery, < 2N), b = this lane's L digits (regs),
+  // a = full KD-digit operand in LDS.  out may alias b.
+  __device__ __forceinline__ void mul(uint32_t* out, const uint32_t* b, const uint32_t* a_lds) const {
+    uint64_t acc[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[j] = 0;
+#pragma unroll 1
+    for (int cyc = 0; cyc < G; ++cyc) cycle(acc, b, a_lds + cyc * L, std::make_integer_sequence<int, L>{});
+    // rotation is back to identity; two more carry steps give digits <= 2^29+127
+    norm_step<0>(acc);
+    const uint32_t cin = dpp_prev<G>((uint32_t)(acc[L - 1] >> 29)) & m_first;
+#pragma unroll
+    for (int j = L - 1; j > 0; --j) out[j] = ((uint32_t)acc[j] & M29) + (uint32_t)(acc[j - 1] >> 29);
+    out[0] = ((uint32_t)acc[0] & M29) + cin;
+  }
+
+  // Exact normalisation of lazy digits (value < 2^(29*KD)) to digits < 2^29.
+  __device__ __forceinline__ void carry_exact(uint32_t* d) const {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) { uint32_t v = d[j] + c; d[j] = v & M29; c = v >> 29; }
+#pragma unroll 1
+    for (int round = 0; round < G - 1; ++round) {
+      uint32_t in = dpp_prev<G>(c) & m_first;
+      c = 0;
+#pragma unroll
+      for (int j = 0; j < L; ++j) { uint32_t v = d[j] + in; d[j] = v & M29; in = v >> 29; }
+      c = in;
+    }
+  }
+
+  // d (exact digits, value < 2N) -> d mod N
+  __device__ __forceinline__ void sub_if_ge(uint32_t* d) const {
+    uint32_t t[L];
+    uint32_t bin = 0;
+#pragma unroll 1
+    for (int round = 0; round < G; ++round) {
+      uint32_t bw = (round == 0) ? 0u : (dpp_prev<G>(bin) & m_first);
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        uint32_t v = d[j] - n[j] - bw;
+        t[j] = v & M29;
+        bw = v >> 31;
+      }
+      bin = bw;
+    }
+    const uint32_t ge = bcast_top<G>(bin == 0u ? 1u : 0u);
+#pragma unroll
+    for (int j = 0; j < L; ++j) d[j] = ge ? t[j] : d[j];
+  }
+
+  // d (exact, < N) -> 2d mod N, exact
+  __device__ __forceinline__ void dbl(uint32_t* d) const {
+    const uint32_t in = dpp_prev<G>(d[L - 1] >> 28) & m_first;
+#pragma unroll
+    for (int j = L - 1; j > 0; --j) d[j] = ((d[j] << 1) & M29) | (d[j - 1] >> 28);
+    d[0] = ((d[0] << 1) & M29) | in;
+    sub_if_ge(d);
+  }
+};
+
+// ---- radix conversion helpers (global u32 limbs <-> 29-bit digits) -----------
+// digit j of a K32-limb little-endian integer
+__device__ __forceinline__ uint32_t digit_of(const uint32_t* __restrict__ x, int K32, int j) {
+  const int bit = 29 * j;
+  const int w = bit >> 5, sh = bit & 31;
+  const uint32_t lo = (w < K32) ? x[w] : 0u;
+  const uint32_t hi = (w + 1 < K32) ? x[w + 1] : 0u;
+  return (uint32_t)(mk64(lo, hi) >> sh) & M29;
+}
+// limb k (32-bit) of an exact-digit integer stored in LDS
+__device__ __forceinline__ uint32_t limb_of(const uint32_t* d, int KD, int k) {
+  const int bit = 32 * k;
+  const int j = bit / 29, sh = bit % 29;
+  uint64_t v = (j < KD) ? d[j] : 0u;
+  if (j + 1 < KD) v |= (uint64_t)d[j + 1] << 29;
+  if (j + 2 < KD) v |= (uint64_t)d[j + 2] << 58;
+  return (uint32_t)(v >> sh);
+}
+
+}  // namespace fsdkr
