@@ -66,6 +66,24 @@ __device__ __forceinline__ int group_max(int v) {
 
 __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
+// acc += a * b  -> one v_mad_u64_u32 (callers guarantee acc never exceeds 2^64).
+__device__ __forceinline__ void mac(uint64_t& acc, uint32_t a, uint32_t b) {
+  acc += (uint64_t)a * b;
+}
+
+// Make N register values opaque to the optimiser at this point (no code).  Used
+// at the top of each product cycle so LLVM cannot hoist zext(digit) out of the
+// cycle loop: a hoisted i64 zext is a cross-block value that ISel materialises
+// as a VGPR pair per digit (+2L VGPRs for b and n), instead of folding it into
+// each v_mad_u64_u32's 32-bit source operand.
+template <int N>
+__device__ __forceinline__ void opaque(uint32_t* v) {
+#pragma unroll
+  for (int j = 0; j + 3 < N; j += 4) asm volatile("" : "+v"(v[j]), "+v"(v[j + 1]), "+v"(v[j + 2]), "+v"(v[j + 3]));
+#pragma unroll
+  for (int j = N - N % 4; j < N; ++j) asm volatile("" : "+v"(v[j]));
+}
+
 template <int KD, int G>
 struct Mont29 {
   static constexpr int L = KD / G;
@@ -85,6 +103,9 @@ struct Mont29 {
     m_lane0 = (g == 0) ? 0xFFFFFFFFu : 0u;
     m_first = (g == 0) ? 0u : 0xFFFFFFFFu;
     m_top = (g == G - 1) ? 0u : 0xFFFFFFFFu;
+    // keep the masks as plain values so `x & mask` stays one full-rate v_and
+    // (the optimiser otherwise rewrites it into v_cndmask on a lane predicate)
+    asm volatile("" : "+v"(m_lane0), "+v"(m_first), "+v"(m_top));
   }
 
   __device__ __forceinline__ uint64_t prev64(uint64_t v) const {
@@ -98,43 +119,55 @@ struct Mont29 {
   template <int RHO>
   __device__ __forceinline__ void norm_step(uint64_t* acc) const {
     const uint64_t cin = prev64(acc[(L - 1 + RHO) % L] >> 29);
+    // descending so each column reads its lower neighbour before that one is
+    // rewritten; sched barriers every 6 columns stop the scheduler from
+    // hoisting all L shifts at once (that alone costs 2L VGPRs)
 #pragma unroll
     for (int j = L - 1; j > 0; --j) {
       const int s = (j + RHO) % L, sp = (j - 1 + RHO) % L;
       acc[s] = (uint64_t)((uint32_t)acc[s] & M29) + (acc[sp] >> 29);
+      if (j % 6 == 0) __builtin_amdgcn_sched_barrier(0);
     }
     acc[RHO % L] = (uint64_t)((uint32_t)acc[RHO % L] & M29) + cin;
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // one CIOS row at rotation R (logical column j lives in slot (j+R)%L)
   template <int R>
-  __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, uint32_t ai) const {
+  __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, const uint32_t* n, uint32_t ai) const {
 #pragma unroll
-    for (int j = 0; j < L; ++j) acc[(j + R) % L] += (uint64_t)ai * b[j];
+    for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], ai, b[j]);
     constexpr int s0 = R % L, s1 = (R + 1) % L;
     const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
 #pragma unroll
-    for (int j = 0; j < L; ++j) acc[(j + R) % L] += (uint64_t)m * n[j];
+    for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
     const uint64_t c = acc[s0] >> 29;
     acc[s1] += mk64((uint32_t)c & m_lane0, (uint32_t)(c >> 32) & m_lane0);
     acc[s0] = next64(acc[s0]);
     if constexpr (((R + 1) % NSTEP == 0) || (R + 1 == L)) norm_step<(R + 1) % L>(acc);
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   template <int... Rs>
-  __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* arow,
+  __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* arow,
                                         std::integer_sequence<int, Rs...>) const {
-    (row<Rs>(acc, b, arow[Rs]), ...);
+    (row<Rs>(acc, b, n, arow[Rs]), ...);
   }
 
   // out = a * b / R  (almost Montgomery, < 2N), b = this lane's L digits (regs),
-  // a = full KD-digit operand in LDS.  out may alias b.
-  __device__ __forceinline__ void mul(uint32_t* out, const uint32_t* b, const uint32_t* a_lds) const {
+  // a = full KD-digit operand in LDS.  out may alias b.  (Non-const: b and n
+  // pass through opaque(), which leaves their values unchanged.)
+  __device__ __forceinline__ void mul(uint32_t* out, uint32_t* b, const uint32_t* a_lds) {
     uint64_t acc[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) acc[j] = 0;
 #pragma unroll 1
-    for (int cyc = 0; cyc < G; ++cyc) cycle(acc, b, a_lds + cyc * L, std::make_integer_sequence<int, L>{});
+    for (int cyc = 0; cyc < G; ++cyc) {
+      // values unchanged; only the optimiser's view of them is reset (see opaque)
+      opaque<L>(b);
+      opaque<L>(n);
+      cycle(acc, b, n, a_lds + cyc * L, std::make_integer_sequence<int, L>{});
+    }
     // rotation is back to identity; two more carry steps give digits <= 2^29+127
     norm_step<0>(acc);
     const uint32_t cin = dpp_prev<G>((uint32_t)(acc[L - 1] >> 29)) & m_first;
