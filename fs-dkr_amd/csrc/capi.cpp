@@ -96,45 +96,119 @@ uint32_t choose_window(uint32_t ebits) {
   return best_w;
 }
 
-// Runs mod_setup + modexp on device-resident operands.
-int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
-                      uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,
-                      uint32_t n_mod, uint32_t* d_out) {
+// Launch one modexp job whose descriptors are already in device memory.
+int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
+                       const uint32_t* d_consts, uint32_t* d_out) {
+  if (count == 0) return FSDKR_OK;
   const int KD = shape_digits(k32);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
     return FSDKR_E_UNSUPPORTED;
   }
-  if (count == 0) return FSDKR_OK;
-  if (exp_bits == 0) exp_bits = 1;
-  const uint32_t w = choose_window(exp_bits);
-  const uint32_t nwin = (exp_bits + w - 1) / w;
-  const size_t stride = 3 * (size_t)KD + 4;
-  uint32_t* d_consts = (uint32_t*)c->buf("consts", sizeof(uint32_t) * stride * n_mod);
-  uint32_t* d_table = (uint32_t*)c->buf("table", sizeof(uint32_t) * (size_t)count * ((size_t)1 << w) * KD);
-  if (!d_consts || !d_table) {
+  const uint32_t ebits = exp_bits ? exp_bits : 1;
+  const uint32_t w = choose_window(ebits);
+  const uint32_t nwin = (ebits + w - 1) / w;
+  uint32_t* d_table = (uint32_t*)c->buf("mxtable", sizeof(uint32_t) * (size_t)count * ((size_t)1 << w) * KD);
+  if (!d_table) {
     c->fail("device allocation failed (%u instances, window %u)", count, w);
     return FSDKR_E_OOM;
   }
-  c->mark("mod_setup", true);
-  int rc = c->hip_check(mod_setup(k32, d_mods, n_mod, d_consts, c->stream), "mod_setup launch");
-  c->mark("mod_setup", false);
-  if (rc) return rc;
+  const size_t n8 = (size_t)count * 8, n4 = (size_t)count * 4;
   ModexpArgs a;
-  a.base = d_base;
-  a.exps = d_exp;
-  a.exp_limbs = exp_limbs;
+  a.base_ptr = reinterpret_cast<const uint64_t*>(d_desc);
+  a.exp_ptr = reinterpret_cast<const uint64_t*>(d_desc + n8);
+  a.base_len = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8);
+  a.exp_len = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + n4);
+  a.mod_idx = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 2 * n4);
   a.nwin = nwin;
   a.window = w;
-  a.mod_idx = d_mod_idx;
   a.consts = d_consts;
   a.out = d_out;
   a.table = d_table;
   a.count = count;
   c->mark("modexp", true);
-  rc = c->hip_check(modexp(k32, a, c->stream), "modexp launch");
+  int rc = c->hip_check(modexp(k32, a, c->stream), "modexp launch");
   c->mark("modexp", false);
   return rc;
+}
+
+void ModexpJob::pack(std::vector<uint8_t>& dst) const {
+  const size_t n8 = size() * 8, n4 = size() * 4;
+  const size_t o = dst.size();
+  dst.resize(o + desc_bytes());
+  memcpy(dst.data() + o, base_ptr.data(), n8);
+  memcpy(dst.data() + o + n8, exp_ptr.data(), n8);
+  memcpy(dst.data() + o + 2 * n8, base_len.data(), n4);
+  memcpy(dst.data() + o + 2 * n8 + n4, exp_len.data(), n4);
+  memcpy(dst.data() + o + 2 * n8 + 2 * n4, mod_idx.data(), n4);
+}
+
+// Upload a modexp descriptor set and launch it against prepared constants.
+int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag) {
+  const uint32_t count = (uint32_t)job.size();
+  if (count == 0) return FSDKR_OK;
+  std::string dname = std::string("mxdesc_") + tag;
+  uint8_t* d_desc = (uint8_t*)c->buf(dname.c_str(), job.desc_bytes());
+  if (!d_desc) {
+    c->fail("device allocation failed (descriptors)");
+    return FSDKR_E_OOM;
+  }
+  std::vector<uint8_t>& h = c->staging;
+  h.clear();
+  job.pack(h);
+  int rc = c->hip_check(hipMemcpyAsync(d_desc, h.data(), h.size(), hipMemcpyHostToDevice, c->stream), "H2D modexp desc");
+  if (rc) return rc;
+  // the staging buffer is reused by the next call: make this copy complete first
+  rc = c->hip_check(hipStreamSynchronize(c->stream), "sync desc");
+  if (rc) return rc;
+  return launch_modexp_desc(c, job.k32, count, job.exp_bits, d_desc, d_consts, d_out);
+}
+
+int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag) {
+  const int KD = shape_digits(k32);
+  if (!KD) {
+    c->fail("unsupported modulus width %u limbs", k32);
+    return FSDKR_E_UNSUPPORTED;
+  }
+  std::string name = std::string("consts_") + tag;
+  *d_consts = (uint32_t*)c->buf(name.c_str(), sizeof(uint32_t) * (3 * (size_t)KD + 4) * (n_mod ? n_mod : 1));
+  if (!*d_consts) {
+    c->fail("device allocation failed (mod consts)");
+    return FSDKR_E_OOM;
+  }
+  c->mark("mod_setup", true);
+  int rc = c->hip_check(mod_setup(k32, d_mods, n_mod, *d_consts, c->stream), "mod_setup launch");
+  c->mark("mod_setup", false);
+  return rc;
+}
+
+// Runs mod_setup + modexp on device-resident contiguous operands.
+int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
+                      uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,
+                      uint32_t n_mod, uint32_t* d_out) {
+  if (count == 0) return FSDKR_OK;
+  uint32_t* d_consts = nullptr;
+  int rc = setup_moduli(c, k32, d_mods, n_mod, &d_consts, "generic");
+  if (rc) return rc;
+  ModexpJob job;
+  job.k32 = k32;
+  job.exp_bits = exp_bits;
+  job.base_ptr.resize(count);
+  job.exp_ptr.resize(count);
+  job.base_len.assign(count, k32);
+  job.exp_len.assign(count, exp_limbs);
+  job.mod_idx.resize(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    job.base_ptr[i] = (uint64_t)(uintptr_t)(d_base + (size_t)i * k32);
+    job.exp_ptr[i] = (uint64_t)(uintptr_t)(d_exp + (size_t)i * exp_limbs);
+  }
+  rc = c->hip_check(hipMemcpyAsync(job.mod_idx.data(), d_mod_idx, sizeof(uint32_t) * count, hipMemcpyDeviceToHost,
+                                   c->stream),
+                    "D2H mod_idx");
+  if (rc) return rc;
+  rc = c->hip_check(hipStreamSynchronize(c->stream), "sync");
+  if (rc) return rc;
+  return launch_modexp_job(c, job, d_consts, d_out, "generic");
 }
 
 }  // namespace fsdkr

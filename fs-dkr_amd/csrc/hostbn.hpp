@@ -1,0 +1,180 @@
+// Minimal host big-integer helpers (little-endian u32 limbs) for the O(1)- or
+// O(n)-per-collect host logic around the GPU batch: N^2, bit lengths,
+// comparisons, the correct-key rho reduction, small-prime trial division,
+// gcd tests of DLog statements and the Paillier L-function.  Not on the
+// O(n^2) verification path (that is all GPU).
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace fsdkr {
+namespace hbn {
+
+using Limbs = std::vector<uint32_t>;
+
+inline void trim(Limbs& a) {
+  while (!a.empty() && a.back() == 0) a.pop_back();
+}
+inline Limbs from(const uint32_t* p, size_t n) {
+  Limbs a(p, p + n);
+  trim(a);
+  return a;
+}
+inline uint32_t bitlen(const Limbs& a) {
+  if (a.empty()) return 0;
+  return (uint32_t)(a.size() - 1) * 32 + 32 - __builtin_clz(a.back());
+}
+inline uint32_t bitlen(const uint32_t* p, size_t n) {
+  for (size_t k = n; k-- > 0;)
+    if (p[k]) return (uint32_t)k * 32 + 32 - __builtin_clz(p[k]);
+  return 0;
+}
+inline int cmp(const Limbs& a, const Limbs& b) {
+  if (a.size() != b.size()) return a.size() < b.size() ? -1 : 1;
+  for (size_t k = a.size(); k-- > 0;)
+    if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1;
+  return 0;
+}
+inline Limbs add(const Limbs& a, const Limbs& b) {
+  Limbs r(std::max(a.size(), b.size()) + 1, 0);
+  uint64_t c = 0;
+  for (size_t k = 0; k < r.size(); ++k) {
+    c += (uint64_t)(k < a.size() ? a[k] : 0) + (k < b.size() ? b[k] : 0);
+    r[k] = (uint32_t)c;
+    c >>= 32;
+  }
+  trim(r);
+  return r;
+}
+inline Limbs add_small(const Limbs& a, uint32_t v) { return add(a, Limbs{v}); }
+// a - b, requires a >= b
+inline Limbs sub(const Limbs& a, const Limbs& b) {
+  Limbs r(a.size(), 0);
+  int64_t br = 0;
+  for (size_t k = 0; k < a.size(); ++k) {
+    int64_t d = (int64_t)a[k] - (k < b.size() ? b[k] : 0) + br;
+    r[k] = (uint32_t)d;
+    br = d >> 32;
+  }
+  trim(r);
+  return r;
+}
+inline Limbs mul(const Limbs& a, const Limbs& b) {
+  if (a.empty() || b.empty()) return {};
+  Limbs r(a.size() + b.size(), 0);
+  for (size_t i = 0; i < a.size(); ++i) {
+    uint64_t c = 0;
+    for (size_t j = 0; j < b.size(); ++j) {
+      c += (uint64_t)a[i] * b[j] + r[i + j];
+      r[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    r[i + b.size()] = (uint32_t)c;
+  }
+  trim(r);
+  return r;
+}
+inline Limbs shl(const Limbs& a, uint32_t s) {
+  if (a.empty()) return {};
+  const uint32_t w = s / 32, b = s % 32;
+  Limbs r(a.size() + w + 1, 0);
+  for (size_t k = 0; k < a.size(); ++k) {
+    r[k + w] |= a[k] << b;
+    if (b) r[k + w + 1] |= a[k] >> (32 - b);
+  }
+  trim(r);
+  return r;
+}
+inline Limbs shr1(const Limbs& a) {
+  Limbs r(a.size(), 0);
+  for (size_t k = 0; k < a.size(); ++k) r[k] = (a[k] >> 1) | (k + 1 < a.size() ? a[k + 1] << 31 : 0);
+  trim(r);
+  return r;
+}
+// remainder modulo a small word
+inline uint32_t mod_small(const Limbs& a, uint32_t m) {
+  uint64_t r = 0;
+  for (size_t k = a.size(); k-- > 0;) r = ((r << 32) | a[k]) % m;
+  return (uint32_t)r;
+}
+// (q, r) = a / b, bit-serial long division (inputs are a few thousand bits)
+inline void divmod(const Limbs& a, const Limbs& b, Limbs* q, Limbs* r) {
+  Limbs rem;
+  Limbs quo(a.size(), 0);
+  const uint32_t nb = bitlen(a);
+  for (uint32_t i = nb; i-- > 0;) {
+    rem = shl(rem, 1);
+    if ((a[i / 32] >> (i % 32)) & 1u) {
+      if (rem.empty()) rem.push_back(1);
+      else rem[0] |= 1u;
+    }
+    if (cmp(rem, b) >= 0) {
+      rem = sub(rem, b);
+      quo[i / 32] |= 1u << (i % 32);
+    }
+  }
+  trim(quo);
+  if (q) *q = quo;
+  if (r) *r = rem;
+}
+inline Limbs mod(const Limbs& a, const Limbs& m) {
+  Limbs r;
+  divmod(a, m, nullptr, &r);
+  return r;
+}
+inline Limbs mulmod(const Limbs& a, const Limbs& b, const Limbs& m) { return mod(mul(a, b), m); }
+inline bool is_even(const Limbs& a) { return a.empty() || (a[0] & 1u) == 0; }
+// binary gcd
+inline Limbs gcd(Limbs a, Limbs b) {
+  if (a.empty()) return b;
+  if (b.empty()) return a;
+  uint32_t shift = 0;
+  while (is_even(a) && is_even(b)) {
+    a = shr1(a);
+    b = shr1(b);
+    ++shift;
+  }
+  while (is_even(a)) a = shr1(a);
+  while (!b.empty()) {
+    while (is_even(b)) b = shr1(b);
+    if (cmp(a, b) > 0) std::swap(a, b);
+    b = sub(b, a);
+  }
+  return shl(a, shift);
+}
+inline bool is_one(const Limbs& a) { return a.size() == 1 && a[0] == 1; }
+// modular inverse by the extended binary method (m odd), false if none
+inline bool modinv(const Limbs& y, const Limbs& m, Limbs* out) {
+  Limbs a = mod(y, m), b = m, u{1}, v{};
+  auto half = [&](Limbs& x) {  // x/2 mod m
+    if (is_even(x)) x = shr1(x);
+    else x = shr1(add(x, m));
+  };
+  while (!a.empty()) {
+    if (is_even(a)) {
+      a = shr1(a);
+      half(u);
+    } else {
+      if (cmp(a, b) < 0) {
+        std::swap(a, b);
+        std::swap(u, v);
+      }
+      a = shr1(sub(a, b));
+      Limbs d = cmp(u, v) >= 0 ? sub(u, v) : sub(add(u, m), v);
+      half(d);
+      u = d;
+    }
+  }
+  if (!is_one(b)) return false;
+  *out = v;
+  return true;
+}
+inline void store(const Limbs& a, uint32_t* out, size_t n) {
+  for (size_t k = 0; k < n; ++k) out[k] = k < a.size() ? a[k] : 0u;
+}
+
+}  // namespace hbn
+}  // namespace fsdkr

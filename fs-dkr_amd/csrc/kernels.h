@@ -7,16 +7,19 @@ namespace fsdkr {
 
 constexpr int BLOCK = 256;
 
+// One batched-modexp launch.  Operands are addressed per instance so a launch
+// can mix proof fields, device-computed challenges and other kernels' outputs.
 struct ModexpArgs {
-  const uint32_t* base;     // [count][K32]
-  const uint32_t* exps;     // [count][exp_limbs]
-  uint32_t exp_limbs;
-  uint32_t nwin;            // windows of `window` bits, taken from bit nwin*window-1 down
+  const uint64_t* base_ptr;  // [count] device addresses of little-endian u32 limbs
+  const uint32_t* base_len;  // [count] limbs (<= K32)
+  const uint64_t* exp_ptr;   // [count]
+  const uint32_t* exp_len;   // [count] limbs
+  uint32_t nwin;             // windows of `window` bits, taken from bit nwin*window-1 down
   uint32_t window;
-  const uint32_t* mod_idx;  // [count]
-  const uint32_t* consts;   // [n_mod][3*KD+4]  from mod_setup
-  uint32_t* out;            // [count][K32]
-  uint32_t* table;          // [count][2^window][KD] scratch
+  const uint32_t* mod_idx;   // [count] row of `consts`
+  const uint32_t* consts;    // [n_mod][3*KD+4]  from mod_setup
+  uint32_t* out;             // [count][K32]
+  uint32_t* table;           // [count][2^window][KD] scratch
   uint32_t count;
 };
 

@@ -101,20 +101,22 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   const uint32_t w = a.window;
   const uint32_t tsize = 1u << w;
   uint32_t* T = a.table + (size_t)inst * tsize * KD;
-  const uint32_t* E = a.exps + (size_t)inst * a.exp_limbs;
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[inst]);
+  const uint32_t exp_limbs = a.exp_len[inst];
 
   uint32_t acc[L];
-  const uint32_t* B = a.base + (size_t)inst * K32;
+  const uint32_t* B = reinterpret_cast<const uint32_t*>(a.base_ptr[inst]);
+  const int blen = (int)min(a.base_len[inst], (uint32_t)K32);
 #pragma unroll
-  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, K32, g * L + j);
+  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);
 #pragma unroll
   for (int j = 0; j < L; ++j) T[g * L + j] = C[KD + g * L + j];             // T[0] = R mod N
   const uint32_t nwin = a.nwin;
   auto digit = [&](uint32_t k) -> uint32_t {
     const uint32_t p = (nwin - 1 - k) * w;
     const uint32_t lo = p >> 5, sh = p & 31;
-    const uint32_t v0 = (lo < a.exp_limbs) ? E[lo] : 0u;
-    const uint32_t v1 = (lo + 1 < a.exp_limbs) ? E[lo + 1] : 0u;
+    const uint32_t v0 = (lo < exp_limbs) ? E[lo] : 0u;
+    const uint32_t v1 = (lo + 1 < exp_limbs) ? E[lo + 1] : 0u;
     return (uint32_t)(mk64(v0, v1) >> sh) & (tsize - 1);
   };
   // Every Montgomery product of the exponentiation is acc <- acc * stream, issued

@@ -1,0 +1,117 @@
+// Argument blocks of the verification kernels (verify.hip).  Device
+// addresses are carried as uint64_t so descriptor arrays can be built on the
+// host and uploaded in one copy.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace fsdkr {
+
+struct BinomArgs {          // out = 1 + s * n
+  const uint64_t* s_ptr;
+  const uint64_t* n_ptr;
+  uint32_t s_len, n_len, out_limbs;
+  uint32_t* out;
+  uint32_t count;
+};
+
+struct PdlHashArgs {        // e = H(G, Q, c, z, u1, u2, u3)
+  const uint32_t *Q, *c, *z, *u1, *u2, *u3;
+  uint32_t c_len, z_len;
+  uint32_t* e_out;          // [count][8]
+  uint32_t count;
+};
+
+struct PedHashArgs {        // ring-Pedersen challenge bits
+  const uint32_t* A;        // [count][M][a_len]
+  uint32_t M, a_len;
+  uint32_t* bits;           // [count][ceil(M/32)]
+  uint32_t* panic;          // [count]
+  uint32_t count;
+};
+
+struct AliceHashArgs {      // H(N, N+1, c, z, u, w) == e
+  const uint64_t* n_ptr;    // receiver N
+  const uint64_t* c_ptr;    // ciphertext
+  const uint32_t *z, *u, *w, *e;
+  uint32_t n_len, c_len, z_len, e_len;
+  uint8_t* verdict;         // in: host pre-checks, out: AND hash equality
+  uint32_t count;
+};
+
+struct InverseArgs {
+  const uint64_t* y_ptr;    // value to invert (reduced, K32 limbs)
+  const uint64_t* m_ptr;    // odd modulus (K32 limbs)
+  uint32_t* out;            // [count][K32] inverse (may be null)
+  uint32_t* unit;           // [count] 1 if gcd(y, m) == 1
+  uint32_t* scratch;        // 6 * (K32+2) * count words
+  uint32_t count;
+};
+
+struct EqOperand {
+  uint64_t a, b, c, d;      // device addresses
+  uint32_t a_len, b_len, c_len, d_len;
+  uint32_t sel;             // bit index into sel_bits choosing d (set) or 1 (clear); ~0 = always d
+  uint32_t flags;           // bit0: require c < N
+};
+
+struct EqCheckArgs {        // a*b == c*d (mod N)
+  const EqOperand* ops;
+  const uint32_t* mod_idx;
+  const uint32_t* consts;
+  const uint32_t* sel_bits;
+  uint64_t one;             // address of the constant 1 (K32 limbs)
+  uint32_t* out;            // [count] 1/0
+  uint32_t count;
+};
+
+struct Prod3Operand {
+  uint64_t a, b, c;
+  uint32_t a_len, b_len, c_len, pad;
+};
+
+struct Prod3Args {          // out = a*b*c mod N
+  const Prod3Operand* ops;
+  const uint32_t* mod_idx;
+  const uint32_t* consts;
+  uint32_t* out;            // [count][K32]
+  uint32_t count;
+};
+
+struct PdlU1Args {          // G*(s1 mod q) + Q*(q - e) == u1
+  const uint32_t *s1, *e, *Q, *u1;
+  uint32_t s1_len;
+  uint8_t* verdict;         // bit0 written
+  uint32_t count;
+};
+
+struct FeldmanArgs {
+  const uint32_t* vss;      // [R][t+1][16]
+  const uint32_t* S;        // [R*n][16]
+  uint32_t n, t;
+  uint8_t* verdict;         // [R*n]
+  uint32_t count;
+};
+
+struct EcMsmArgs {          // out[o] = sum_j scalars[o][j] * P[o][j]
+  const uint64_t* pt_ptr;   // [count][terms] affine points (16 limbs)
+  const uint32_t* scalars;  // [count][terms][8]
+  uint32_t terms;
+  uint32_t* out;            // [count][16] affine
+  uint32_t count;
+};
+
+hipError_t launch_binom(const BinomArgs& a, hipStream_t st);
+hipError_t launch_pdl_hash(const PdlHashArgs& a, hipStream_t st);
+hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st);
+hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st);
+hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);
+hipError_t launch_eq_check(uint32_t k32, const EqCheckArgs& a, hipStream_t st);
+hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st);
+hipError_t launch_pdl_u1(const PdlU1Args& a, hipStream_t st);
+hipError_t launch_feldman(const FeldmanArgs& a, hipStream_t st);
+hipError_t launch_ec_msm(const EcMsmArgs& a, hipStream_t st);
+
+}  // namespace fsdkr

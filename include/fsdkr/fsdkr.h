@@ -73,6 +73,105 @@ int fsdkr_modexp_batch_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count
                               const uint32_t* d_mod_idx, const uint32_t* d_mods, uint32_t n_mod,
                               uint32_t* d_out);
 
+
+/* ---- Job 2: batched verification of RefreshMessage::collect ----------------
+ * One call verifies every proof collect() checks (refresh_message.rs:321-437):
+ * n^2 Feldman share checks (:177-188), R*n PDL-with-slack + Alice range proofs
+ * (:330-350), R+J ring-Pedersen proofs (:353-365), R+J Paillier correct-key
+ * proofs + modulus sizes (:375-396), J pairs of composite-DLog proofs
+ * (:398-437).  The caller's batching layer gathers the messages into the SoA
+ * arrays below (pairs p = k*n + i, k < R sender slice order, i < n receiver);
+ * big integers use fixed per-field limb widths chosen by the caller.
+ * Points are affine x||y (8+8 limbs), (0,0) encodes the point at infinity. */
+typedef struct fsdkr_collect_batch {
+  uint32_t n_refresh;    /* R */
+  uint32_t n_join;       /* J;  n = R + J receivers (new_n, :327)                 */
+  uint32_t t;            /* local_key.t                                           */
+  uint32_t m_security;   /* M of RingPedersenProof (256)                          */
+  uint32_t key_bits;     /* PAILLIER_KEY_SIZE (lib.rs:26)                         */
+  uint32_t nl;           /* limbs of N, N~, h1, h2, ring-Pedersen N (64 = 2048 bit) */
+  uint32_t s1l, s3l, el, zl, yl; /* limb widths of PDL/Alice s1, s3|s2, Alice e, RP Z, DLog y */
+  const uint32_t* party_index;   /* [R+J] message party indices (joins: 0 = unassigned) */
+  const uint32_t* msg_lens;      /* [R][3] pdl_proof_vec / points_committed / points_encrypted lengths */
+  /* receivers: local_key.paillier_key_vec[i].n and h1_h2_n_tilde_vec[i] */
+  const uint32_t *recv_n, *recv_ntilde, *recv_h1, *recv_h2;          /* [n][nl]   */
+  /* pairs */
+  const uint32_t* enc;      /* [P][2nl] points_encrypted_vec[i]       */
+  const uint32_t* commit;   /* [P][16]  points_committed_vec[i]       */
+  const uint32_t *pdl_z, *pdl_u3, *pdl_s2;                            /* [P][nl]   */
+  const uint32_t* pdl_u1;   /* [P][16]  */
+  const uint32_t* pdl_u2;   /* [P][2nl] */
+  const uint32_t* pdl_s1;   /* [P][s1l] */
+  const uint32_t* pdl_s3;   /* [P][s3l] */
+  const uint32_t *rp_z, *rp_s;                                        /* [P][nl]   */
+  const uint32_t* rp_e;     /* [P][el]  */
+  const uint32_t* rp_s1;    /* [P][s1l] */
+  const uint32_t* rp_s2;    /* [P][s3l] */
+  const uint32_t* vss;      /* [R][t+1][16] coefficients_committed_vec commitments */
+  /* ring-Pedersen statement + proof of the R refresh then J join messages */
+  const uint32_t *ped_S, *ped_T, *ped_N;                              /* [R+J][nl] */
+  const uint32_t* ped_A;    /* [R+J][M][nl] */
+  const uint32_t* ped_Z;    /* [R+J][M][zl] */
+  /* NiCorrectKeyProof: ek.n and sigma_vec of the R then J messages */
+  const uint32_t* ck_n;     /* [R+J][nl]     */
+  const uint32_t* ck_sigma; /* [R+J][11][nl] */
+  /* join messages: dlog_statement {N, g, ni} and the two CompositeDLogProofs */
+  const uint32_t *dlog_N, *dlog_g, *dlog_ni, *dlog_x1, *dlog_x2;      /* [J][nl]  */
+  const uint32_t *dlog_y1, *dlog_y2;                                  /* [J][yl]  */
+} fsdkr_collect_batch;
+
+/* Verdicts (caller-allocated). 1 bits mean "check passed". */
+typedef struct fsdkr_verdicts {
+  uint8_t* feldman;  /* [R*n]  validate_share_public                                  */
+  uint8_t* pdl;      /* [R*n]  bit0 u1, bit1 u2, bit2 u3 equal; bit3: reference panics */
+  uint8_t* range;    /* [R*n]  AliceProof::verify                                      */
+  uint8_t* ped;      /* [R+J]  bit0 RingPedersenProof::verify ok; bit1: panics         */
+  uint8_t* ck;       /* [R+J]  NiCorrectKeyProof::verify ok                            */
+  uint8_t* dlog;     /* [J]    bit0 base-h1 proof ok, bit1 base-h2 proof ok           */
+} fsdkr_verdicts;
+
+int fsdkr_verify_collect(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch, fsdkr_verdicts* out);
+
+/* FsDkrError variants, in error.rs declaration order (error.rs:6-60). */
+#define FSDKR_ERR_NONE 0
+#define FSDKR_ERR_PARTIES_THRESHOLD_VIOLATION 1
+#define FSDKR_ERR_PUBLIC_SHARE_VALIDATION 2
+#define FSDKR_ERR_SIZE_MISMATCH 3
+#define FSDKR_ERR_PDL_W_SLACK_PROOF 4
+#define FSDKR_ERR_RING_PEDERSEN_PROOF 5
+#define FSDKR_ERR_RANGE_PROOF 6
+#define FSDKR_ERR_MODULI_TOO_SMALL 7
+#define FSDKR_ERR_PAILLIER_VERIFICATION 8
+#define FSDKR_ERR_NEW_PARTY_UNASSIGNED_INDEX 9
+#define FSDKR_ERR_BROADCASTED_PUBLIC_KEY 10
+#define FSDKR_ERR_DLOG_PROOF_VALIDATION 11
+#define FSDKR_ERR_RING_PEDERSEN_PROOF_VALIDATION 12
+
+typedef struct fsdkr_error {
+  int32_t variant;        /* FSDKR_ERR_*                                                 */
+  int32_t panic;          /* 1: the reference panics at this point instead of returning */
+  uint32_t f[4];          /* payload fields in declaration order                         */
+  uint32_t keys_applied;  /* messages (R first, then J) whose ek was written into
+                             local_key.paillier_key_vec before the error (:394, :436)   */
+} fsdkr_error;
+
+/* Map verdicts to the FIRST failing check in collect() order:
+ * threshold, sizes, Feldman (k, i), [PDL then range] (k, i), ring-Pedersen
+ * (refresh, then join), per refresh message correct-key then modulus size,
+ * per join message index, correct-key, DLog, modulus size.  `verdicts` may be
+ * NULL when the threshold or size check already fails.  Pure host logic. */
+int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out);
+
+/* ---- share recovery building blocks (refresh_message.rs:367-373, 439-464) ---
+ * Paillier decryption m = L(c^lambda mod N^2) * mu mod N with dk = (p, q)
+ * (kzen-paillier decrypt; the exponentiation runs on the GPU). */
+int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, const uint32_t* c, const uint32_t* p, const uint32_t* q,
+                           uint32_t* m_out);
+/* out[o] = sum_j scalars[o][j] * points[o][j] on secp256k1 (affine 16-limb
+ * points, 8-limb scalars reduced mod q on device): pk_vec entries and G*x. */
+int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t* points, const uint32_t* scalars,
+                 uint32_t* out);
+
 /* Kernel timing (needs FSDKR_CFG_TIMING): accumulated milliseconds and launch
  * count of kernel `name` since the last reset ("modexp", "mod_setup", ...). */
 int fsdkr_kernel_time(const fsdkr_ctx* ctx, const char* name, double* ms, uint32_t* launches);
