@@ -120,12 +120,87 @@ inline void divmod(const Limbs& a, const Limbs& b, Limbs* q, Limbs* r) {
   if (q) *q = quo;
   if (r) *r = rem;
 }
+// Knuth algorithm D (TAOCP 4.3.1) for larger operands
+inline void divmod_knuth(const Limbs& a, const Limbs& b, Limbs* q, Limbs* r) {
+  if (cmp(a, b) < 0) {
+    if (q) q->clear();
+    if (r) *r = a;
+    return;
+  }
+  if (b.size() == 1) {
+    Limbs quo(a.size(), 0);
+    uint64_t rem = 0;
+    for (size_t k = a.size(); k-- > 0;) {
+      const uint64_t cur = (rem << 32) | a[k];
+      quo[k] = (uint32_t)(cur / b[0]);
+      rem = cur % b[0];
+    }
+    trim(quo);
+    if (q) *q = quo;
+    if (r) *r = rem ? Limbs{(uint32_t)rem} : Limbs{};
+    return;
+  }
+  const uint32_t s = __builtin_clz(b.back());
+  Limbs v = shl(b, s), u = shl(a, s);
+  const size_t n = v.size();
+  if (u.size() == a.size() + (s ? 0 : 0)) u.push_back(0);
+  while (u.size() < a.size() + 1) u.push_back(0);
+  const size_t m = u.size() - n - 1 + 1;
+  Limbs quo(m, 0);
+  for (size_t j = m; j-- > 0;) {
+    const uint64_t num = ((uint64_t)u[j + n] << 32) | u[j + n - 1];
+    uint64_t qhat = num / v[n - 1], rhat = num % v[n - 1];
+    while (qhat > 0xFFFFFFFFull || qhat * v[n - 2] > ((rhat << 32) | u[j + n - 2])) {
+      --qhat;
+      rhat += v[n - 1];
+      if (rhat > 0xFFFFFFFFull) break;
+    }
+    int64_t borrow = 0;
+    uint64_t carry = 0;
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t p = qhat * v[i] + carry;
+      carry = p >> 32;
+      const int64_t t = (int64_t)u[i + j] - (int64_t)(uint32_t)p + borrow;
+      u[i + j] = (uint32_t)t;
+      borrow = t >> 32;
+    }
+    const int64_t t = (int64_t)u[j + n] - (int64_t)carry + borrow;
+    u[j + n] = (uint32_t)t;
+    if (t < 0) {  // add back
+      --qhat;
+      uint64_t c = 0;
+      for (size_t i = 0; i < n; ++i) {
+        c += (uint64_t)u[i + j] + v[i];
+        u[i + j] = (uint32_t)c;
+        c >>= 32;
+      }
+      u[j + n] += (uint32_t)c;
+    }
+    quo[j] = (uint32_t)qhat;
+  }
+  trim(quo);
+  if (q) *q = quo;
+  if (r) {
+    u.resize(n);
+    trim(u);
+    // unnormalise
+    Limbs rr(u.size(), 0);
+    for (size_t k = 0; k < u.size(); ++k) rr[k] = (s ? (u[k] >> s) | (k + 1 < u.size() ? u[k + 1] << (32 - s) : 0) : u[k]);
+    trim(rr);
+    *r = rr;
+  }
+}
 inline Limbs mod(const Limbs& a, const Limbs& m) {
   Limbs r;
-  divmod(a, m, nullptr, &r);
+  divmod_knuth(a, m, nullptr, &r);
   return r;
 }
 inline Limbs mulmod(const Limbs& a, const Limbs& b, const Limbs& m) { return mod(mul(a, b), m); }
+inline Limbs div_exact(const Limbs& a, const Limbs& b) {
+  Limbs q;
+  divmod_knuth(a, b, &q, nullptr);
+  return q;
+}
 inline bool is_even(const Limbs& a) { return a.empty() || (a[0] & 1u) == 0; }
 // binary gcd
 inline Limbs gcd(Limbs a, Limbs b) {

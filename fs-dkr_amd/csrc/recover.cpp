@@ -18,40 +18,142 @@ using namespace fsdkr;
 
 extern "C" {
 
-int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, const uint32_t* c, const uint32_t* p, const uint32_t* q,
-                           uint32_t* m_out) {
+int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c, const uint32_t* p,
+                           const uint32_t* q, uint32_t* m_out) {
   Ctx* cx = reinterpret_cast<Ctx*>(ctx);
   if (!cx || !c || !p || !q || !m_out) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
   const uint32_t nn = 2 * nl;
-  if (!shape_digits(nn)) {
+  if (!shape_digits(nl)) {
     cx->fail("fsdkr_paillier_decrypt: unsupported width %u", nl);
     return FSDKR_E_UNSUPPORTED;
   }
   const hbn::Limbs P = hbn::from(p, nl), Q = hbn::from(q, nl);
-  const hbn::Limbs N = hbn::mul(P, Q), NN = hbn::mul(N, N);
-  const hbn::Limbs lam = hbn::mul(hbn::sub(P, hbn::Limbs{1}), hbn::sub(Q, hbn::Limbs{1}));
-  if (hbn::bitlen(NN) > 32 * nn || hbn::is_even(N)) {
+  const hbn::Limbs N = hbn::mul(P, Q);
+  const hbn::Limbs PP = hbn::mul(P, P), QQ = hbn::mul(Q, Q);
+  if (hbn::is_even(P) || hbn::is_even(Q) || hbn::bitlen(PP) > 32 * nl || hbn::bitlen(QQ) > 32 * nl ||
+      hbn::bitlen(N) > 32 * nl) {
     cx->fail("fsdkr_paillier_decrypt: bad key");
     return FSDKR_E_ARG;
   }
-  // u = c^lambda mod N^2 on the GPU
-  std::vector<uint32_t> cb(nn), eb(nl), mb(nn), ub(nn);
-  hbn::store(hbn::mod(hbn::from(c, nn), NN), cb.data(), nn);
-  hbn::store(lam, eb.data(), nl);
-  hbn::store(NN, mb.data(), nn);
-  const uint32_t idx = 0;
-  int rc = fsdkr_modexp_batch(ctx, nn, 1, cb.data(), eb.data(), nl, &idx, mb.data(), 1, ub.data());
-  if (rc) return rc;
-  // m = L(u) * lambda^-1 mod N,  L(u) = (u - 1) / N
-  hbn::Limbs Lq, r;
-  hbn::divmod(hbn::sub(hbn::from(ub.data(), nn), hbn::Limbs{1}), N, &Lq, &r);
-  hbn::Limbs mu;
-  if (!hbn::modinv(lam, N, &mu)) {
-    cx->fail("fsdkr_paillier_decrypt: lambda not invertible mod N");
+  const hbn::Limbs one{1};
+  const hbn::Limbs pm1 = hbn::sub(P, one), qm1 = hbn::sub(Q, one);
+  // kzen-paillier CRT decryption: m_p = L_p(c^(p-1) mod p^2) h_p mod p, h_p = L_p(g^(p-1) mod p^2)^-1, g = N+1
+  auto hconst = [&](const hbn::Limbs& X, const hbn::Limbs& XX, const hbn::Limbs& xm1, hbn::Limbs* h) {
+    const hbn::Limbs gx = hbn::mod(hbn::add(one, hbn::mul(xm1, N)), XX);  // (1+N)^(x-1) = 1 + (x-1)N mod x^2
+    const hbn::Limbs L = hbn::div_exact(hbn::sub(gx, one), X);
+    return hbn::modinv(L, X, h);
+  };
+  hbn::Limbs hp, hq, qinv;
+  if (!hconst(P, PP, pm1, &hp) || !hconst(Q, QQ, qm1, &hq) || !hbn::modinv(Q, P, &qinv)) {
+    cx->fail("fsdkr_paillier_decrypt: degenerate key");
     return FSDKR_E_ARG;
   }
-  hbn::store(hbn::mulmod(Lq, mu, N), m_out, nl);
+  // 2*count GPU exponentiations: (c mod p^2)^(p-1) mod p^2, (c mod q^2)^(q-1) mod q^2
+  std::vector<uint32_t> base((size_t)2 * count * nl), ex((size_t)2 * count * nl), idx(2 * count), mods(2 * nl),
+      outv((size_t)2 * count * nl);
+  hbn::store(PP, mods.data(), nl);
+  hbn::store(QQ, mods.data() + nl, nl);
+  for (uint32_t k = 0; k < count; ++k) {
+    const hbn::Limbs ck = hbn::from(c + (size_t)k * nn, nn);
+    hbn::store(hbn::mod(ck, PP), base.data() + (size_t)(2 * k) * nl, nl);
+    hbn::store(hbn::mod(ck, QQ), base.data() + (size_t)(2 * k + 1) * nl, nl);
+    hbn::store(pm1, ex.data() + (size_t)(2 * k) * nl, nl);
+    hbn::store(qm1, ex.data() + (size_t)(2 * k + 1) * nl, nl);
+    idx[2 * k] = 0;
+    idx[2 * k + 1] = 1;
+  }
+  int rc = fsdkr_modexp_batch(ctx, nl, 2 * count, base.data(), ex.data(), nl, idx.data(), mods.data(), 2, outv.data());
+  if (rc) return rc;
+  for (uint32_t k = 0; k < count; ++k) {
+    const hbn::Limbs up = hbn::from(outv.data() + (size_t)(2 * k) * nl, nl);
+    const hbn::Limbs uq = hbn::from(outv.data() + (size_t)(2 * k + 1) * nl, nl);
+    const hbn::Limbs mp = hbn::mulmod(hbn::div_exact(hbn::sub(up.empty() ? one : up, one), P), hp, P);
+    const hbn::Limbs mq = hbn::mulmod(hbn::div_exact(hbn::sub(uq.empty() ? one : uq, one), Q), hq, Q);
+    // m = mq + q * ((mp - mq) q^-1 mod p)
+    const hbn::Limbs mqp = hbn::mod(mq, P);
+    const hbn::Limbs d = hbn::cmp(mp, mqp) >= 0 ? hbn::sub(mp, mqp) : hbn::sub(hbn::add(mp, P), mqp);
+    const hbn::Limbs m = hbn::add(mq, hbn::mul(Q, hbn::mulmod(d, qinv, P)));
+    hbn::store(m, m_out + (size_t)k * nl, nl);
+  }
   return FSDKR_OK;
+}
+
+// Job 1 (refresh_message.rs:72-84): c_k = (1 + m_k N) * r_k^N mod N^2 for the
+// n shares of distribute(), each under its receiver's key ns[n_idx[k]].
+int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* m, uint32_t ml,
+                           const uint32_t* r, const uint32_t* n_idx, const uint32_t* ns, uint32_t n_keys,
+                           uint32_t* out) {
+  Ctx* cx = reinterpret_cast<Ctx*>(ctx);
+  if (!cx || !m || !r || !n_idx || !ns || !out || ml == 0 || n_keys == 0) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  const uint32_t nn = 2 * nl;
+  if (!shape_digits(nn)) return FSDKR_E_UNSUPPORTED;
+  std::vector<uint32_t> NNs((size_t)n_keys * nn);
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    const hbn::Limbs N = hbn::from(ns + (size_t)k * nl, nl);
+    if (hbn::is_even(N)) {
+      cx->fail("fsdkr_paillier_encrypt: even modulus");
+      return FSDKR_E_ARG;
+    }
+    hbn::store(hbn::mul(N, N), NNs.data() + (size_t)k * nn, nn);
+  }
+  for (uint32_t k = 0; k < count; ++k)
+    if (n_idx[k] >= n_keys) return FSDKR_E_ARG;
+  // device image: ns | NNs | m | r | one | outputs
+  const size_t b_ns = 0, b_nns = b_ns + (size_t)n_keys * nl * 4, b_m = b_nns + NNs.size() * 4;
+  const size_t b_r = b_m + (size_t)count * ml * 4, b_one = b_r + (size_t)count * nl * 4;
+  const size_t b_gm = b_one + (size_t)nn * 4, b_rn = b_gm + (size_t)count * nn * 4;
+  const size_t b_out = b_rn + (size_t)count * nn * 4, b_desc = b_out + (size_t)count * nn * 4;
+  const size_t total = b_desc + (size_t)count * (16 + 16 + sizeof(Prod3Operand) + 8) + 4096;
+  uint8_t* d = (uint8_t*)cx->buf("enc", total);
+  if (!d) return FSDKR_E_OOM;
+  std::vector<uint8_t> img(b_desc, 0);
+  memcpy(img.data() + b_ns, ns, (size_t)n_keys * nl * 4);
+  memcpy(img.data() + b_nns, NNs.data(), NNs.size() * 4);
+  memcpy(img.data() + b_m, m, (size_t)count * ml * 4);
+  memcpy(img.data() + b_r, r, (size_t)count * nl * 4);
+  ((uint32_t*)(img.data() + b_one))[0] = 1;
+  auto A = [&](size_t off) { return (uint64_t)(uintptr_t)(d + off); };
+  // binom: gm = 1 + m*N  (m < N for a share; reduced mod N^2 by prod3 anyway)
+  std::vector<uint64_t> s_ptr(count), n_ptr(count);
+  ModexpJob job;
+  job.k32 = nn;
+  std::vector<Prod3Operand> ops(count);
+  std::vector<uint32_t> midx(count);
+  for (uint32_t k = 0; k < count; ++k) {
+    s_ptr[k] = A(b_m + (size_t)k * ml * 4);
+    n_ptr[k] = A(b_ns + (size_t)n_idx[k] * nl * 4);
+    job.add(A(b_r + (size_t)k * nl * 4), nl, A(b_ns + (size_t)n_idx[k] * nl * 4), nl, 32 * nl, n_idx[k]);
+    ops[k] = {A(b_gm + (size_t)k * nn * 4), A(b_rn + (size_t)k * nn * 4), A(b_one), nn, nn, nn, 0};
+    midx[k] = n_idx[k];
+  }
+  auto app = [&](const void* src, size_t bytes) {
+    const size_t o = (img.size() + 255) & ~(size_t)255;
+    img.resize(o + bytes);
+    memcpy(img.data() + o, src, bytes);
+    return o;
+  };
+  const size_t o_s = app(s_ptr.data(), count * 8), o_n = app(n_ptr.data(), count * 8);
+  const size_t o_ops = app(ops.data(), count * sizeof(Prod3Operand)), o_midx = app(midx.data(), count * 4);
+  std::vector<uint8_t> jd;
+  job.pack(jd);
+  const size_t o_job = app(jd.data(), jd.size());
+  if (img.size() > total) return FSDKR_E_ARG;
+  int rc = cx->hip_check(hipMemcpyAsync(d, img.data(), img.size(), hipMemcpyHostToDevice, cx->stream), "H2D enc");
+  if (rc) return rc;
+  uint32_t* consts = nullptr;
+  if ((rc = setup_moduli(cx, nn, (const uint32_t*)(d + b_nns), n_keys, &consts, "enc"))) return rc;
+  BinomArgs ba{(const uint64_t*)(d + o_s), (const uint64_t*)(d + o_n), ml, nl, nn, (uint32_t*)(d + b_gm), count};
+  if ((rc = cx->hip_check(launch_binom(ba, cx->stream), "binom"))) return rc;
+  if ((rc = launch_modexp_desc(cx, nn, count, 32 * nl, d + o_job, consts, (uint32_t*)(d + b_rn)))) return rc;
+  Prod3Args pa{(const Prod3Operand*)(d + o_ops), (const uint32_t*)(d + o_midx), consts, (uint32_t*)(d + b_out), count};
+  // prod3 computes a*b*c mod N^2 exactly: (1+mN) * r^N * 1
+  if ((rc = cx->hip_check(launch_prod3(nn, pa, cx->stream), "prod3"))) return rc;
+  if ((rc = cx->hip_check(hipMemcpyAsync(out, d + b_out, (size_t)count * nn * 4, hipMemcpyDeviceToHost, cx->stream),
+                          "D2H enc")))
+    return rc;
+  return cx->sync();
 }
 
 int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t* points, const uint32_t* scalars,

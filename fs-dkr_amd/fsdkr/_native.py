@@ -30,6 +30,29 @@ class _Cfg(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("flags", ctypes.c_uint32)]
 
 
+class CollectBatchC(ctypes.Structure):
+    """struct fsdkr_collect_batch (include/fsdkr/fsdkr.h)."""
+    _fields_ = [(f, ctypes.c_uint32) for f in ("n_refresh", "n_join", "t", "m_security", "key_bits", "nl",
+                                               "s1l", "s3l", "el", "zl", "yl")] + \
+               [(f, u32p) for f in ("party_index", "msg_lens", "recv_n", "recv_ntilde", "recv_h1", "recv_h2",
+                                    "enc", "commit", "pdl_z", "pdl_u3", "pdl_s2", "pdl_u1", "pdl_u2", "pdl_s1",
+                                    "pdl_s3", "rp_z", "rp_s", "rp_e", "rp_s1", "rp_s2", "vss", "ped_S", "ped_T",
+                                    "ped_N", "ped_A", "ped_Z", "ck_n", "ck_sigma", "dlog_N", "dlog_g", "dlog_ni",
+                                    "dlog_x1", "dlog_x2", "dlog_y1", "dlog_y2")]
+
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class VerdictsC(ctypes.Structure):
+    _fields_ = [(f, u8p) for f in ("feldman", "pdl", "range", "ped", "ck", "dlog")]
+
+
+class ErrorC(ctypes.Structure):
+    _fields_ = [("variant", ctypes.c_int32), ("panic", ctypes.c_int32), ("f", ctypes.c_uint32 * 4),
+                ("keys_applied", ctypes.c_uint32)]
+
+
 _lib = None
 
 
@@ -61,6 +84,18 @@ def lib():
     L.fsdkr_kernel_time.restype = ctypes.c_int
     L.fsdkr_kernel_time_reset.argtypes = [vp]
     L.fsdkr_kernel_time_reset.restype = None
+    L.fsdkr_verify_collect.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.POINTER(VerdictsC)]
+    L.fsdkr_verify_collect.restype = ctypes.c_int
+    L.fsdkr_collect_first_error.argtypes = [ctypes.POINTER(CollectBatchC), ctypes.POINTER(VerdictsC),
+                                            ctypes.POINTER(ErrorC)]
+    L.fsdkr_collect_first_error.restype = ctypes.c_int
+    L.fsdkr_paillier_decrypt.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p]
+    L.fsdkr_paillier_decrypt.restype = ctypes.c_int
+    L.fsdkr_paillier_encrypt.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p, u32p,
+                                         u32p, ctypes.c_uint32, u32p]
+    L.fsdkr_paillier_encrypt.restype = ctypes.c_int
+    L.fsdkr_ec_msm.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
+    L.fsdkr_ec_msm.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -145,3 +180,50 @@ class Context:
         self.check(self._lib.fsdkr_modexp_batch(self._h, mod_limbs, count, _ptr(B), _ptr(E), exp_limbs, _ptr(I),
                                                 _ptr(Mo), len(mods), _ptr(O)))
         return limbs_to_ints(O)
+
+    # ---- collect() verification -------------------------------------------
+    def verify_collect(self, batch):
+        """Run fsdkr_verify_collect on a fsdkr.batch.CollectBatch; returns a Verdicts."""
+        from .batch import Verdicts
+        v = Verdicts(batch.R, batch.J, batch.n)
+        self.check(self._lib.fsdkr_verify_collect(self._h, ctypes.byref(batch.c), ctypes.byref(v.c)))
+        return v
+
+    def paillier_decrypt(self, cts, p, q, nl):
+        """Decrypt ciphertexts under dk = (p, q) on the GPU (CRT form)."""
+        C = ints_to_limbs(cts, 2 * nl)
+        Pp = ints_to_limbs([p], nl)
+        Qq = ints_to_limbs([q], nl)
+        O = np.zeros((len(cts), nl), dtype=np.uint32)
+        self.check(self._lib.fsdkr_paillier_decrypt(self._h, nl, len(cts), _ptr(C), _ptr(Pp), _ptr(Qq), _ptr(O)))
+        return limbs_to_ints(O)
+
+    def paillier_encrypt(self, ms, rs, ns, n_idx, nl):
+        """Job 1: [(1 + m N) r^N mod N^2] for N = ns[n_idx[k]]."""
+        ml = max(1, (max(m.bit_length() for m in ms) + 31) // 32)
+        Mm = ints_to_limbs(ms, ml)
+        Rr = ints_to_limbs(rs, nl)
+        Nn = ints_to_limbs(ns, nl)
+        I = np.ascontiguousarray(np.asarray(n_idx, dtype=np.uint32))
+        O = np.zeros((len(ms), 2 * nl), dtype=np.uint32)
+        self.check(self._lib.fsdkr_paillier_encrypt(self._h, nl, len(ms), _ptr(Mm), ml, _ptr(Rr), _ptr(I), _ptr(Nn),
+                                                    len(ns), _ptr(O)))
+        return limbs_to_ints(O)
+
+    def ec_msm(self, points, scalars):
+        """points/scalars: lists (count) of equal-length lists; points are (x, y) or None."""
+        count, terms = len(points), len(points[0])
+        Pt = np.zeros((count, terms, 16), dtype=np.uint32)
+        for o in range(count):
+            for j in range(terms):
+                pt = points[o][j]
+                if pt is not None:
+                    Pt[o, j] = ints_to_limbs([pt[0] | (pt[1] << 256)], 16)[0]
+        Sc = ints_to_limbs([s for row in scalars for s in row], 8).reshape(count, terms, 8)
+        O = np.zeros((count, 16), dtype=np.uint32)
+        self.check(self._lib.fsdkr_ec_msm(self._h, count, terms, _ptr(Pt), _ptr(Sc), _ptr(O)))
+        out = []
+        for v in limbs_to_ints(O):
+            x, y = v & ((1 << 256) - 1), v >> 256
+            out.append(None if (x == 0 and y == 0) else (x, y))
+        return out

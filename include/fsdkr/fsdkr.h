@@ -162,11 +162,20 @@ typedef struct fsdkr_error {
  * NULL when the threshold or size check already fails.  Pure host logic. */
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out);
 
+/* ---- Job 1: Paillier encryption of the shares (refresh_message.rs:72-84) ----
+ * out[k] = (1 + m[k] N) * r[k]^N mod N^2, N = ns[n_idx[k]]  (kzen-paillier
+ * encrypt_with_chosen_randomness).  m: [count][ml], r: [count][nl] (< N),
+ * ns: [n_keys][nl], out: [count][2nl]. */
+int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* m, uint32_t ml,
+                           const uint32_t* r, const uint32_t* n_idx, const uint32_t* ns, uint32_t n_keys,
+                           uint32_t* out);
+
 /* ---- share recovery building blocks (refresh_message.rs:367-373, 439-464) ---
- * Paillier decryption m = L(c^lambda mod N^2) * mu mod N with dk = (p, q)
- * (kzen-paillier decrypt; the exponentiation runs on the GPU). */
-int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, const uint32_t* c, const uint32_t* p, const uint32_t* q,
-                           uint32_t* m_out);
+ * Paillier decryption of `count` ciphertexts [count][2nl] under one key
+ * dk = (p, q) (each [nl], zero-padded), kzen-paillier CRT form; the
+ * exponentiations run on the GPU.  m_out: [count][nl]. */
+int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c, const uint32_t* p,
+                           const uint32_t* q, uint32_t* m_out);
 /* out[o] = sum_j scalars[o][j] * points[o][j] on secp256k1 (affine 16-limb
  * points, 8-limb scalars reduced mod q on device): pk_vec entries and G*x. */
 int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t* points, const uint32_t* scalars,

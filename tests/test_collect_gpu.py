@@ -1,0 +1,201 @@
+"""GPU parity of RefreshMessage::collect (fs-dkr_amd, HIP via the C ABI)
+against the oracle (CPU restatement of refresh_message.rs:321-467).
+
+For every scenario both sides run on the same seeded messages; the outcome
+(Ok, or the FsDkrError variant + payload), the side effects on
+paillier_key_vec and, on success, the whole updated LocalKey must be equal."""
+import copy
+
+import pytest
+
+from oracle import paillier, protocol
+from oracle import secp256k1 as ec
+from oracle import zk_pdl_with_slack as pdl
+from oracle import range_proofs
+from oracle.rng import Rng
+
+pytestmark = pytest.mark.gpu
+
+KB = 1024          # flows are size-independent; one test below runs 2048-bit keys
+
+
+def _dkr(t, n, seed, key_bits=KB):
+    rng = Rng(seed)
+    keys = protocol.simulate_keygen(t, n, rng, key_bits)
+    msgs, dks = [], []
+    for key in keys:
+        m, dk = protocol.distribute(key.i, key, n, rng, key_bits)
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks, rng
+
+
+def _both(msgs, key, dk, joins, key_bits=KB, ctx=None):
+    """Run oracle and GPU collect on copies; return (oracle_result, gpu_result, oracle_key, gpu_key)."""
+    from fsdkr import refresh
+    ko, kg = key.clone(), key.clone()
+    ro = rg = None
+    try:
+        protocol.collect(copy.deepcopy(msgs), ko, dk, copy.deepcopy(joins), Rng("a8"), key_bits)
+    except protocol.FsDkrError as e:
+        ro = (e.variant, e.fields)
+    except Exception as e:  # PanicError
+        ro = ("panic", type(e).__name__)
+    try:
+        refresh.collect(copy.deepcopy(msgs), kg, dk, copy.deepcopy(joins), ctx=ctx, key_bits=key_bits)
+    except refresh.FsDkrError as e:
+        rg = (e.variant, e.fields)
+    except refresh.FsDkrPanic:
+        rg = ("panic", "PanicError")
+    return ro, rg, ko, kg
+
+
+def _same_key(a, b):
+    assert a.x_i == b.x_i
+    assert a.y == b.y
+    assert a.pk_vec == b.pk_vec
+    assert [k.n for k in a.paillier_key_vec] == [k.n for k in b.paillier_key_vec]
+    assert (a.paillier_dk.p, a.paillier_dk.q) == (b.paillier_dk.p, b.paillier_dk.q)
+
+
+@pytest.fixture(scope="module")
+def dkr5():
+    return _dkr(2, 5, "collect-gpu-t2n5")
+
+
+def test_collect_valid_t2_n5(gpu_ctx, dkr5):
+    keys, msgs, dks, _ = dkr5
+    for party in (0, 3):
+        ro, rg, ko, kg = _both(msgs, keys[party], dks[party], [], ctx=gpu_ctx)
+        assert ro is None and rg is None
+        _same_key(ko, kg)
+
+
+def test_collect_valid_2048(gpu_ctx):
+    keys, msgs, dks, _ = _dkr(1, 3, "collect-gpu-2048", key_bits=2048)
+    ro, rg, ko, kg = _both(msgs, keys[1], dks[1], [], key_bits=2048, ctx=gpu_ctx)
+    assert ro is None and rg is None
+    _same_key(ko, kg)
+
+
+def _tampered(msgs, fn):
+    m2 = copy.deepcopy(msgs)
+    fn(m2)
+    return m2
+
+
+def _bump_pdl(m, k, i, **kw):
+    p = m[k].pdl_proof_vec[i]
+    m[k].pdl_proof_vec[i] = pdl.PDLwSlackProof(**{**p.__dict__, **kw})
+
+
+def _bump_range(m, k, i, **kw):
+    a = m[k].range_proofs[i]
+    m[k].range_proofs[i] = range_proofs.AliceProof(**{**a.__dict__, **kw})
+
+
+TAMPERS = {
+    "feldman": lambda m: m[1].points_committed_vec.__setitem__(2, ec.mul(ec.G, 12345)),
+    "pdl_u2": lambda m: _bump_pdl(m, 2, 1, u2=m[2].pdl_proof_vec[1].u2 + 1),
+    "pdl_u3": lambda m: _bump_pdl(m, 0, 4, s3=m[0].pdl_proof_vec[4].s3 + 1),
+    "pdl_u1": lambda m: _bump_pdl(m, 3, 0, s1=m[3].pdl_proof_vec[0].s1 + 1),
+    "range_s2": lambda m: _bump_range(m, 1, 3, s2=m[1].range_proofs[3].s2 + 1),
+    "range_s1_bound": lambda m: _bump_range(m, 4, 2, s1=ec.Q ** 3 + 1),
+    "range_e": lambda m: _bump_range(m, 2, 2, e=m[2].range_proofs[2].e ^ 1),
+    "ped_Z": lambda m: setattr(m[3], "ring_pedersen_proof", type(m[3].ring_pedersen_proof)(
+        m[3].ring_pedersen_proof.A, tuple(z + (j == 7) for j, z in enumerate(m[3].ring_pedersen_proof.Z)))),
+    "ck_sigma": lambda m: setattr(m[2], "dk_correctness_proof", type(m[2].dk_correctness_proof)(
+        (m[2].dk_correctness_proof.sigma_vec[0] + 1,) + tuple(m[2].dk_correctness_proof.sigma_vec[1:]))),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TAMPERS))
+def test_collect_tampered(gpu_ctx, dkr5, name):
+    keys, msgs, dks, _ = dkr5
+    m2 = _tampered(msgs, TAMPERS[name])
+    ro, rg, ko, kg = _both(m2, keys[0], dks[0], [], ctx=gpu_ctx)
+    assert ro is not None, "tamper did not break the oracle"
+    assert rg == ro
+    # side effects before the failure (paillier_key_vec written per passing message)
+    assert [k.n for k in ko.paillier_key_vec] == [k.n for k in kg.paillier_key_vec]
+
+
+def test_pdl_soundness_vector(gpu_ctx, dkr5):
+    """zk_pdl_with_slack.rs:268-331: encrypting x+1 with an honest-looking proof."""
+    keys, msgs, dks, rng = dkr5
+    m2 = copy.deepcopy(msgs)
+    k, i = 1, 2
+    ek = keys[0].paillier_key_vec[i]
+    st0 = keys[0].h1_h2_n_tilde_vec[i]
+    x = paillier.decrypt(keys[i].paillier_dk, msgs[k].points_encrypted_vec[i])   # the honest share
+    r = rng.sample_below(ek.n)
+    c = paillier.encrypt_with_chosen_randomness(ek, x + 1, r)                      # here we encrypt x + 1
+    st = pdl.PDLwSlackStatement(c, ek, msgs[k].points_committed_vec[i], ec.G, st0.g, st0.ni, st0.N)
+    m2[k].points_encrypted_vec[i] = c
+    m2[k].pdl_proof_vec[i] = pdl.prove(x, r, st, rng)
+    ro, rg, _, _ = _both(m2, keys[0], dks[0], [], ctx=gpu_ctx)
+    assert ro == ("PDLwSlackProof", {"is_u1_eq": True, "is_u2_eq": False, "is_u3_eq": True})
+    assert rg == ro
+
+
+def test_threshold_and_size(gpu_ctx, dkr5):
+    keys, msgs, dks, _ = dkr5
+    ro, rg, _, _ = _both(msgs[:2], keys[0], dks[0], [], ctx=gpu_ctx)
+    assert ro == ("PartiesThresholdViolation", {"threshold": 2, "refreshed_keys": 2}) and rg == ro
+    m2 = copy.deepcopy(msgs)
+    m2[3].pdl_proof_vec.pop()
+    ro, rg, _, _ = _both(m2, keys[0], dks[0], [], ctx=gpu_ctx)
+    assert ro[0] == "SizeMismatchError" and rg == ro
+
+
+def test_moduli_too_small(gpu_ctx, dkr5):
+    keys, msgs, dks, rng = dkr5
+    m2 = copy.deepcopy(msgs)
+    ek, dk = paillier.keypair_with_modulus_size(KB - 128, rng)
+    m2[3].ek = ek
+    m2[3].dk_correctness_proof = protocol.NiCorrectKeyProof.proof(dk.p, dk.q)
+    ro, rg, ko, kg = _both(m2, keys[2], dks[2], [], ctx=gpu_ctx)
+    assert ro[0] == "ModuliTooSmall" and rg == ro
+    assert [k.n for k in ko.paillier_key_vec] == [k.n for k in kg.paillier_key_vec]
+
+
+def test_collect_with_joins(gpu_ctx):
+    """replace + JoinMessage path (test.rs:95-224 shape, t=1, n=4: 3 refresh + 1 join)."""
+    rng = Rng("joins")
+    t, n = 1, 4
+    all_keys = protocol.simulate_keygen(t, n, rng, KB)
+    keys = [k.clone() for k in all_keys[:3]]
+    jm, kk = protocol.join_distribute(rng, KB)
+    jm.set_party_index(4)
+    old_to_new = {1: 1, 2: 2, 3: 3}
+    msgs, dks = [], []
+    for key in keys:
+        m, dk = protocol.replace([jm], key, old_to_new, 4, rng, KB)
+        msgs.append(m)
+        dks.append(dk)
+    ro, rg, ko, kg = _both(msgs, keys[1], dks[1], [jm], ctx=gpu_ctx)
+    assert ro is None and rg is None
+    _same_key(ko, kg)
+    # tampered DLog proof of the joiner
+    j2 = copy.deepcopy(jm)
+    j2.composite_dlog_proof_base_h2 = type(jm.composite_dlog_proof_base_h2)(jm.composite_dlog_proof_base_h2.x + 1,
+                                                                            jm.composite_dlog_proof_base_h2.y)
+    ro, rg, _, _ = _both(msgs, keys[1], dks[1], [j2], ctx=gpu_ctx)
+    assert ro == ("DLogProofValidation", {"party_index": 4}) and rg == ro
+    # unassigned joiner index
+    j3 = copy.deepcopy(jm)
+    j3.party_index = None
+    ro, rg, _, _ = _both(msgs, keys[1], dks[1], [j3], ctx=gpu_ctx)
+    assert rg == ro
+
+
+def test_paillier_encrypt_job1(gpu_ctx):
+    """Job 1: encrypt_with_chosen_randomness (refresh_message.rs:72-84) on the GPU."""
+    rng = Rng("job1")
+    keys = [paillier.keypair_with_modulus_size(2048, rng)[0] for _ in range(3)]
+    ms = [rng.sample_below(ec.Q) for _ in range(24)]
+    idx = [k % 3 for k in range(24)]
+    rs = [rng.sample_below(keys[i].n) for i in idx]
+    got = gpu_ctx.paillier_encrypt(ms, rs, [k.n for k in keys], idx, 64)
+    want = [paillier.encrypt_with_chosen_randomness(keys[i], m, r) for m, r, i in zip(ms, rs, idx)]
+    assert got == want
