@@ -50,18 +50,29 @@ void* Ctx::buf(const char* name, size_t bytes) {
   return b.ptr;
 }
 
-void Ctx::mark(const char* name, bool begin) {
-  if (!timing) return;
+size_t Ctx::tbeg(const char* name, hipStream_t st) {
+  last_mark = (size_t)-1;
+  if (!timing) return last_mark;
+  hipEvent_t ev;
+  if (hipEventCreate(&ev) != hipSuccess) return last_mark;
+  (void)hipEventRecord(ev, st ? st : stream);
+  pending.push_back({name, ev, nullptr});
+  last_mark = pending.size() - 1;
+  return last_mark;
+}
+
+void Ctx::tend(size_t idx, hipStream_t st) {
+  if (!timing || idx >= pending.size() || pending[idx].e1) return;
   hipEvent_t ev;
   if (hipEventCreate(&ev) != hipSuccess) return;
-  (void)hipEventRecord(ev, stream);
-  if (begin) {
-    pending.push_back({name, ev, nullptr});
-  } else if (!pending.empty() && pending.back().e1 == nullptr) {
-    pending.back().e1 = ev;
-  } else {
-    (void)hipEventDestroy(ev);
-  }
+  (void)hipEventRecord(ev, st ? st : stream);
+  pending[idx].e1 = ev;
+}
+
+hipStream_t Ctx::side_stream(int k) {
+  k %= NSIDE;
+  if (!side[k] && hipStreamCreateWithFlags(&side[k], hipStreamNonBlocking) != hipSuccess) side[k] = nullptr;
+  return side[k] ? side[k] : stream;
 }
 
 int Ctx::sync() {
@@ -98,7 +109,8 @@ uint32_t choose_window(uint32_t ebits) {
 
 // Launch one modexp job whose descriptors are already in device memory.
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
-                       const uint32_t* d_consts, uint32_t* d_out) {
+                       const uint32_t* d_consts, uint32_t* d_out, hipStream_t st, const char* table_tag) {
+  if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
   const int KD = shape_digits(k32);
   if (!KD) {
@@ -108,7 +120,7 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   const uint32_t ebits = exp_bits ? exp_bits : 1;
   const uint32_t w = choose_window(ebits);
   const uint32_t nwin = (ebits + w - 1) / w;
-  uint32_t* d_table = (uint32_t*)c->buf("mxtable", sizeof(uint32_t) * (size_t)count * ((size_t)1 << w) * KD);
+  uint32_t* d_table = (uint32_t*)c->buf(table_tag, sizeof(uint32_t) * (size_t)count * ((size_t)1 << w) * KD);
   if (!d_table) {
     c->fail("device allocation failed (%u instances, window %u)", count, w);
     return FSDKR_E_OOM;
@@ -126,9 +138,9 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.out = d_out;
   a.table = d_table;
   a.count = count;
-  c->mark("modexp", true);
-  int rc = c->hip_check(modexp(k32, a, c->stream), "modexp launch");
-  c->mark("modexp", false);
+  const size_t tm = c->tbeg("modexp", st);
+  int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
+  c->tend(tm, st);
   return rc;
 }
 
@@ -257,7 +269,10 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
   (void)c->sync();
   for (auto& kv : c->bufs)
     if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+  for (auto& sd : c->side)
+    if (sd) (void)hipStreamDestroy(sd);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  fsdkr::free_collect_plan(c);
   delete c;
 }
 

@@ -84,17 +84,47 @@ inline void absorb_u32(Sha256& h, uint32_t v) { h.bigint(&v, 1); }
 }  // namespace
 
 // ------------------------------------------------------------------------------
-int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v) {
-  Sizes s;
+// Everything the run phase needs after the host pre-pass and the upload.
+struct CollectPlan {
+  Sizes s{};
+  uint32_t el = 0, t = 0;
+  size_t in_bytes = 0, out_off = 0, total = 0;
+  uint8_t* dev = nullptr;
+  // input offsets used by launches
+  size_t o_Q, o_enc, o_pz, o_pu1, o_pu2, o_pu3, o_ps1, o_pA, o_az, o_ae, o_vss, o_NN, o_mods, o_one, o_rn;
+  uint32_t s1l = 0, n_mods_nl = 0;
+  // output offsets
+  size_t x_epdl, x_pbits, x_ppanic, x_Bpdl, x_gs1, x_J[10], x_invc, x_invz, x_unn, x_uzA, x_uzp, x_eq2, x_eq3, x_u,
+      x_w, x_fel, x_pdlv, x_rng, x_scr128, x_scr64;
+  // descriptor offsets + counts
+  size_t d_J[10], d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_p3nn, d_p3nl, d_p3m,
+      d_ahn, d_ahc, d_alpre;
+  uint32_t jk32[10], jcount[10], jbits[10];
+  uint32_t n_inv_nn = 0, n_eq_nn = 0, n_eq_nl = 0;
+  std::vector<uint32_t> cpdl_extra, ae_bits;
+  std::vector<uint8_t> ck_pre, dlog_pre;
+};
+
+void free_collect_plan(Ctx* c) {
+  delete reinterpret_cast<CollectPlan*>(c->plan);
+  c->plan = nullptr;
+}
+
+int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
+  free_collect_plan(c);
+  CollectPlan* plan = new CollectPlan();
+  c->plan = plan;
+  CollectPlan& pl = *plan;
+  Sizes& s = pl.s;
   s.R = b->n_refresh;
   s.J = b->n_join;
-  s.n = s.R + s.J;
+  s.n = b->n_recv ? b->n_recv : s.R + s.J;
   s.P = s.R * s.n;
   s.Mt = s.R + s.J;
   s.M = b->m_security;
   s.nl = b->nl;
   s.nn = 2 * b->nl;
-  if (s.R == 0 || s.M == 0 || !(s.nl == 64 || s.nl == 96) || b->s1l == 0 || b->s3l == 0 || b->el == 0 ||
+  if (s.n < s.R || s.M == 0 || !(s.nl == 64 || s.nl == 96) || b->s1l == 0 || b->s3l == 0 || b->el == 0 ||
       b->zl == 0 || (s.J && b->yl == 0)) {
     c->fail("fsdkr_verify_collect: unsupported shape (R=%u nl=%u)", s.R, s.nl);
     return FSDKR_E_UNSUPPORTED;
@@ -129,7 +159,9 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
   const hbn::Limbs q = hbn::from(Q_LIMBS_H, 8);
   const hbn::Limbs q3 = hbn::mul(hbn::mul(q, q), q);
   std::vector<uint8_t> alice_pre(P), pdl_small(P);
-  std::vector<uint32_t> s1_bits(P), s3_bits(P), a1_bits(P), a2_bits(P), ae_bits(P);
+  std::vector<uint32_t> s1_bits(P), s3_bits(P), a1_bits(P), a2_bits(P);
+  std::vector<uint32_t>& ae_bits = pl.ae_bits;
+  ae_bits.assign(P, 0);
   uint32_t pdl_s1_max = 1, pdl_s3_max = 1, a_s1_max = 1, a_s2_max = 1, a_e_max = 1;
   bool any_big_s1 = false;
   for (uint32_t p = 0; p < P; ++p) {
@@ -159,7 +191,8 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
   }
   // correct-key: rho_j = mask_generation(len(n), H(n, salt, j)) mod n; primorial gcd
   std::vector<uint32_t> RHO((size_t)Mt * CK_M2 * nl);
-  std::vector<uint8_t> ck_pre(Mt);
+  std::vector<uint8_t>& ck_pre = pl.ck_pre;
+  ck_pre.assign(Mt, 0);
   for (uint32_t m = 0; m < Mt; ++m) {
     const uint32_t* ckn = b->ck_n + (size_t)m * nl;
     const hbn::Limbs N = hbn::from(ckn, nl);
@@ -191,7 +224,8 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
     }
   }
   // DLog statements: N > 2^128, gcd(g, N) = gcd(ni, N) = 1; challenges e = H(x, g, N, ni)
-  std::vector<uint8_t> dlog_pre(J);
+  std::vector<uint8_t>& dlog_pre = pl.dlog_pre;
+  dlog_pre.assign(J, 0);
   std::vector<uint32_t> DE((size_t)J * 2 * 8);
   uint32_t y_max = 1;
   for (uint32_t j = 0; j < J; ++j) {
@@ -389,7 +423,8 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
   const size_t d_bs = L.in_vecT(bs_ptr), d_bn = L.in_vecT(bn_ptr);
   // inverse descriptors: nn: c^eA (Alice; also the PDL unit test of c when eA != 0) + c^e_pdl (eA == 0)
   std::vector<uint64_t> inv_y_nn, inv_m_nn, inv_y_nl, inv_m_nl;
-  std::vector<uint32_t> cpdl_extra;  // pairs whose PDL c unit test needs its own inverse
+  std::vector<uint32_t>& cpdl_extra = pl.cpdl_extra;  // pairs whose PDL c unit test needs its own inverse
+  cpdl_extra.clear();
   for (uint32_t p = 0; p < P; ++p) {
     inv_y_nn.push_back(DX(x_J2 + ((size_t)P + p) * nn * 4));
     inv_m_nn.push_back(DI(o_NN + (size_t)(p % n) * nn * 4));
@@ -507,11 +542,79 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
     return FSDKR_E_ARG;
   }
 
+  // ---------------- record the plan and upload the image (the only host->device copy)
+  pl.el = b->el;
+  pl.t = b->t;
+  pl.s1l = b->s1l;
+  pl.n_mods_nl = n_mods_nl;
+  pl.in_bytes = L.host.size();
+  pl.out_off = Layout::al(in_bytes_pre + desc_bound);
+  pl.total = total;
+  pl.dev = dev;
+  pl.o_Q = o_Q; pl.o_enc = o_enc; pl.o_pz = o_pz; pl.o_pu1 = o_pu1; pl.o_pu2 = o_pu2; pl.o_pu3 = o_pu3;
+  pl.o_ps1 = o_ps1; pl.o_pA = o_pA; pl.o_az = o_az; pl.o_ae = o_ae; pl.o_vss = o_vss; pl.o_NN = o_NN;
+  pl.o_mods = o_mods; pl.o_one = o_one; pl.o_rn = o_rn;
+  pl.x_epdl = x_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
+  const size_t xs[10] = {x_J1, x_J2, x_J9, x_J3, x_J4, x_J5, x_J6, x_J7, x_J8, 0};
+  const size_t ds[10] = {d_J1, d_J2, d_J9, d_J3, d_J4, d_J5, d_J6, d_J7, d_J8, 0};
+  const ModexpJob* js[9] = {&J1, &J2, &J9, &J3, &J4, &J5, &J6, &J7, &J8};
+  for (int k = 0; k < 9; ++k) {
+    pl.x_J[k] = xs[k];
+    pl.d_J[k] = ds[k];
+    pl.jk32[k] = js[k]->k32;
+    pl.jcount[k] = (uint32_t)js[k]->size();
+    pl.jbits[k] = js[k]->exp_bits;
+  }
+  pl.x_invc = x_invc; pl.x_invz = x_invz; pl.x_unn = x_unn; pl.x_uzA = x_uzA; pl.x_uzp = x_uzp;
+  pl.x_eq2 = x_eq2; pl.x_eq3 = x_eq3; pl.x_u = x_u; pl.x_w = x_w; pl.x_fel = x_fel; pl.x_pdlv = x_pdlv;
+  pl.x_rng = x_rng; pl.x_scr128 = x_scr128; pl.x_scr64 = x_scr64;
+  pl.d_bs = d_bs; pl.d_bn = d_bn; pl.d_iynn = d_iynn; pl.d_imnn = d_imnn; pl.d_iynl = d_iynl; pl.d_imnl = d_imnl;
+  pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_p3nn = d_p3nn;
+  pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc; pl.d_alpre = d_alpre;
+  pl.n_inv_nn = (uint32_t)inv_y_nn.size();
+  pl.n_eq_nn = (uint32_t)eq_nn.size();
+  pl.n_eq_nl = (uint32_t)eq_nl.size();
+  int rc = c->hip_check(hipMemcpyAsync(dev, L.host.data(), L.host.size(), hipMemcpyHostToDevice, c->stream),
+                        "H2D batch");
+  if (rc) return rc;
+  return c->hip_check(hipStreamSynchronize(c->stream), "sync H2D");
+}
+
+// Kernel pipeline on the prepared (device-resident) batch; writes verdicts.
+int collect_run(Ctx* c, fsdkr_verdicts* v) {
+  CollectPlan* plan = reinterpret_cast<CollectPlan*>(c->plan);
+  if (!plan) {
+    c->fail("fsdkr_collect_run: no prepared batch");
+    return FSDKR_E_ARG;
+  }
+  CollectPlan& pl = *plan;
+  const Sizes& s = pl.s;
+  const uint32_t nl = s.nl, nn = s.nn, P = s.P, n = s.n, Mt = s.Mt, M = s.M, J = s.J;
+  uint8_t* dev = pl.dev;
+  uint8_t* const out_base = dev + pl.out_off;
+  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
+  auto PX = [&](size_t o) { return (uint32_t*)(out_base + o); };
+  auto PI = [&](size_t o) { return (const uint32_t*)(dev + o); };
+  const size_t o_Q = pl.o_Q, o_enc = pl.o_enc, o_pz = pl.o_pz, o_pu1 = pl.o_pu1, o_pu2 = pl.o_pu2, o_pu3 = pl.o_pu3;
+  const size_t o_ps1 = pl.o_ps1, o_pA = pl.o_pA, o_az = pl.o_az, o_ae = pl.o_ae, o_vss = pl.o_vss, o_NN = pl.o_NN;
+  const size_t o_mods = pl.o_mods, o_one = pl.o_one;
+  const size_t x_epdl = pl.x_epdl, x_pbits = pl.x_pbits, x_ppanic = pl.x_ppanic, x_Bpdl = pl.x_Bpdl, x_gs1 = pl.x_gs1;
+  const size_t x_invc = pl.x_invc, x_invz = pl.x_invz, x_unn = pl.x_unn, x_uzA = pl.x_uzA, x_uzp = pl.x_uzp;
+  const size_t x_eq2 = pl.x_eq2, x_eq3 = pl.x_eq3, x_u = pl.x_u, x_w = pl.x_w, x_fel = pl.x_fel, x_pdlv = pl.x_pdlv;
+  const size_t x_rng = pl.x_rng, x_scr128 = pl.x_scr128, x_scr64 = pl.x_scr64;
+  const size_t d_bs = pl.d_bs, d_bn = pl.d_bn, d_iynn = pl.d_iynn, d_imnn = pl.d_imnn, d_iynl = pl.d_iynl;
+  const size_t d_imnl = pl.d_imnl, d_eqnn = pl.d_eqnn, d_eqnnm = pl.d_eqnnm, d_eqnl = pl.d_eqnl, d_eqnlm = pl.d_eqnlm;
+  const size_t d_p3nn = pl.d_p3nn, d_p3nl = pl.d_p3nl, d_p3m = pl.d_p3m, d_ahn = pl.d_ahn, d_ahc = pl.d_ahc;
+  const size_t d_alpre = pl.d_alpre;
+  const uint32_t n_mods_nl = pl.n_mods_nl;
+  const std::vector<uint32_t>& ae_bits = pl.ae_bits;
+  const std::vector<uint32_t>& cpdl_extra = pl.cpdl_extra;
+  const std::vector<uint8_t>& ck_pre = pl.ck_pre;
+  const std::vector<uint8_t>& dlog_pre = pl.dlog_pre;
+  (void)ae_bits;
   // ---------------- launch
   int rc;
   hipStream_t st = c->stream;
-  if ((rc = c->hip_check(hipMemcpyAsync(dev, L.host.data(), L.host.size(), hipMemcpyHostToDevice, st), "H2D batch")))
-    return rc;
   // the alice pre-verdicts become the initial range verdicts
   if ((rc = c->hip_check(hipMemcpyAsync(out_base + x_rng, dev + d_alpre, P, hipMemcpyDeviceToDevice, st), "D2D")))
     return rc;
@@ -533,26 +636,42 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
     if (rc) return rc;
   }
   {
-    BinomArgs a{(const uint64_t*)(dev + d_bs), (const uint64_t*)(dev + d_bn), b->s1l, nl, nn, PX(x_Bpdl), P};
+    BinomArgs a{(const uint64_t*)(dev + d_bs), (const uint64_t*)(dev + d_bn), pl.s1l, nl, nn, PX(x_Bpdl), P};
     if ((rc = c->hip_check(launch_binom(a, st), "binom"))) return rc;
-    BinomArgs a2{(const uint64_t*)(dev + d_bs) + P, (const uint64_t*)(dev + d_bn) + P, b->s1l, nl, nn, PX(x_gs1), P};
+    BinomArgs a2{(const uint64_t*)(dev + d_bs) + P, (const uint64_t*)(dev + d_bn) + P, pl.s1l, nl, nn, PX(x_gs1), P};
     if ((rc = c->hip_check(launch_binom(a2, st), "binom"))) return rc;
   }
-  struct JobRun {
-    const ModexpJob* j;
-    size_t d;
-    const uint32_t* cons;
-    size_t x;
-  } runs[] = {{&J1, d_J1, cons_nn, x_J1}, {&J2, d_J2, cons_nn, x_J2}, {&J9, d_J9, cons_nn, x_J9},
-              {&J3, d_J3, cons_nl, x_J3}, {&J4, d_J4, cons_nl, x_J4}, {&J5, d_J5, cons_nl, x_J5},
-              {&J6, d_J6, cons_nl, x_J6}, {&J7, d_J7, cons_nl, x_J7}, {&J8, d_J8, cons_nl, x_J8}};
-  for (const auto& r : runs)
-    if ((rc = launch_modexp_desc(c, r.j->k32, (uint32_t)r.j->size(), r.j->exp_bits, dev + r.d, r.cons, PX(r.x))))
-      return rc;
+  // the nine modexp jobs are independent: run them concurrently on side streams
+  {
+    hipEvent_t ready;
+    if ((rc = c->hip_check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event"))) return rc;
+    (void)hipEventRecord(ready, st);
+    static const char* tags[9] = {"mxt_J1", "mxt_J2", "mxt_J9", "mxt_J3", "mxt_J4", "mxt_J5", "mxt_J6", "mxt_J7",
+                                  "mxt_J8"};
+    std::vector<hipEvent_t> done;
+    for (int k = 0; k < 9; ++k) {
+      if (!pl.jcount[k]) continue;
+      hipStream_t ss = c->side_stream(k);
+      (void)hipStreamWaitEvent(ss, ready, 0);
+      const uint32_t* cons = (pl.jk32[k] == nn) ? cons_nn : cons_nl;
+      if ((rc = launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
+                                   tags[k])))
+        return rc;
+      hipEvent_t ev;
+      if ((rc = c->hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return rc;
+      (void)hipEventRecord(ev, ss);
+      done.push_back(ev);
+    }
+    for (hipEvent_t ev : done) {
+      (void)hipStreamWaitEvent(st, ev, 0);
+      (void)hipEventDestroy(ev);
+    }
+    (void)hipEventDestroy(ready);
+  }
   // inverses
   {
     InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
-                  PX(x_scr128), (uint32_t)inv_y_nn.size()};
+                  PX(x_scr128), pl.n_inv_nn};
     c->mark("inverse", true);
     rc = c->hip_check(launch_inverse(nn, a, st), "inverse nn");
     c->mark("inverse", false);
@@ -570,14 +689,14 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
   // equality checks and exact products
   {
     EqCheckArgs a{(const EqOperand*)(dev + d_eqnn), PI(d_eqnnm), cons_nn, PX(x_pbits), DI(o_one), PX(x_eq2),
-                  (uint32_t)eq_nn.size()};
+                  pl.n_eq_nn};
     c->mark("eq_check", true);
     rc = c->hip_check(launch_eq_check(nn, a, st), "eq_check nn");
     c->mark("eq_check", false);
     if (rc) return rc;
     // eq_nl outputs: [u3 P | RP Mt*M | CK Mt*11 | DLog 2J] contiguous from x_eq3
     EqCheckArgs b1{(const EqOperand*)(dev + d_eqnl), PI(d_eqnlm), cons_nl, PX(x_pbits), DI(o_one), PX(x_eq3),
-                   (uint32_t)eq_nl.size()};
+                   pl.n_eq_nl};
     c->mark("eq_check", true);
     rc = c->hip_check(launch_eq_check(nl, b1, st), "eq_check nl");
     c->mark("eq_check", false);
@@ -589,17 +708,17 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
   }
   {
     AliceHashArgs a{(const uint64_t*)(dev + d_ahn), (const uint64_t*)(dev + d_ahc), PI(o_az), PX(x_u), PX(x_w),
-                    PI(o_ae), nl, nn, nl, b->el, (uint8_t*)(out_base + x_rng), P};
+                    PI(o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + x_rng), P};
     c->mark("alice_hash", true);
     rc = c->hip_check(launch_alice_hash(a, st), "alice_hash");
     c->mark("alice_hash", false);
     if (rc) return rc;
-    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), b->s1l, (uint8_t*)(out_base + x_pdlv), P};
+    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
     c->mark("ec", true);
     rc = c->hip_check(launch_pdl_u1(u, st), "pdl_u1");
     c->mark("ec", false);
     if (rc) return rc;
-    FeldmanArgs f{PI(o_vss), PI(o_Q), n, b->t, (uint8_t*)(out_base + x_fel), P};
+    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
     c->mark("ec", true);
     rc = c->hip_check(launch_feldman(f, st), "feldman");
     c->mark("ec", false);
@@ -607,13 +726,13 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
   }
   // ---------------- results
   std::vector<uint32_t> e_pdl((size_t)P * 8), ppanic(Mt), unn(2 * (size_t)P), uzA(P), uzp(P), eq2(P),
-      eq_nl_res(eq_nl.size());
+      eq_nl_res(pl.n_eq_nl);
   std::vector<uint8_t> fel(P), pdlv(P), rng(P);
   auto D2H = [&](void* dst, size_t off, size_t bytes) {
     return c->hip_check(hipMemcpyAsync(dst, out_base + off, bytes, hipMemcpyDeviceToHost, st), "D2H verdicts");
   };
   if ((rc = D2H(e_pdl.data(), x_epdl, e_pdl.size() * 4)) || (rc = D2H(ppanic.data(), x_ppanic, Mt * 4)) ||
-      (rc = D2H(unn.data(), x_unn, inv_y_nn.size() * 4)) || (rc = D2H(uzA.data(), x_uzA, P * 4)) ||
+      (rc = D2H(unn.data(), x_unn, (size_t)pl.n_inv_nn * 4)) || (rc = D2H(uzA.data(), x_uzA, P * 4)) ||
       (rc = D2H(uzp.data(), x_uzp, P * 4)) || (rc = D2H(eq2.data(), x_eq2, P * 4)) ||
       (rc = D2H(eq_nl_res.data(), x_eq3, eq_nl_res.size() * 4)) || (rc = D2H(fel.data(), x_fel, P)) ||
       (rc = D2H(pdlv.data(), x_pdlv, P)) || (rc = D2H(rng.data(), x_rng, P)))
@@ -656,6 +775,13 @@ int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v)
     v->dlog[j] = d;
   }
   return FSDKR_OK;
+}
+
+
+int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v) {
+  int rc = collect_prepare(c, b);
+  if (rc) return rc;
+  return collect_run(c, v);
 }
 
 int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdkr_error* e) {
@@ -785,6 +911,18 @@ int fsdkr_verify_collect(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch, fsdkr
       (batch->n_join && !out->dlog))
     return FSDKR_E_ARG;
   return fsdkr::verify_collect_impl(c, batch, out);
+}
+
+int fsdkr_collect_prepare(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
+  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
+  if (!c || !batch) return FSDKR_E_ARG;
+  return fsdkr::collect_prepare(c, batch);
+}
+
+int fsdkr_collect_run(fsdkr_ctx* ctx, fsdkr_verdicts* out) {
+  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
+  if (!c || !out || !out->feldman || !out->pdl || !out->range || !out->ped || !out->ck) return FSDKR_E_ARG;
+  return fsdkr::collect_run(c, out);
 }
 
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out) {

@@ -34,13 +34,20 @@ struct Ctx {
   std::map<std::string, TimeAcc> times;
   std::vector<PendingEvent> pending;
   std::vector<uint8_t> staging;   // host staging for descriptor uploads
+  static constexpr int NSIDE = 8;
+  hipStream_t side[NSIDE] = {};   // concurrent streams for independent jobs (lazily created)
+  void* plan = nullptr;           // prepared collect() batch (collect.cpp)
 
   void fail(const char* fmt, ...);
   int hip_check(hipError_t e, const char* what);
   // grow-only named device buffer (contents undefined after growth)
   void* buf(const char* name, size_t bytes);
-  // HIP-event brackets around a kernel launch on `stream` (timing mode only)
-  void mark(const char* name, bool begin);
+  // HIP-event brackets around a kernel launch (timing mode only); st = nullptr: main stream
+  void mark(const char* name, bool begin) { if (begin) tbeg(name, stream); else tend(last_mark, stream); }
+  size_t tbeg(const char* name, hipStream_t st);
+  void tend(size_t idx, hipStream_t st);
+  size_t last_mark = (size_t)-1;
+  hipStream_t side_stream(int k);
   // synchronise the stream and fold pending events into `times`
   int sync();
 };
@@ -68,9 +75,11 @@ struct ModexpJob {
 };
 
 uint32_t choose_window(uint32_t ebits);
+void free_collect_plan(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag);
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
-                       const uint32_t* d_consts, uint32_t* d_out);
+                       const uint32_t* d_consts, uint32_t* d_out, hipStream_t st = nullptr,
+                       const char* table_tag = "mxtable");
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag);
 int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
                       uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,

@@ -38,7 +38,7 @@ class CollectBatchC(ctypes.Structure):
                                     "enc", "commit", "pdl_z", "pdl_u3", "pdl_s2", "pdl_u1", "pdl_u2", "pdl_s1",
                                     "pdl_s3", "rp_z", "rp_s", "rp_e", "rp_s1", "rp_s2", "vss", "ped_S", "ped_T",
                                     "ped_N", "ped_A", "ped_Z", "ck_n", "ck_sigma", "dlog_N", "dlog_g", "dlog_ni",
-                                    "dlog_x1", "dlog_x2", "dlog_y1", "dlog_y2")]
+                                    "dlog_x1", "dlog_x2", "dlog_y1", "dlog_y2")] + [("n_recv", ctypes.c_uint32)]
 
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -86,6 +86,10 @@ def lib():
     L.fsdkr_kernel_time_reset.restype = None
     L.fsdkr_verify_collect.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.POINTER(VerdictsC)]
     L.fsdkr_verify_collect.restype = ctypes.c_int
+    L.fsdkr_collect_prepare.argtypes = [vp, ctypes.POINTER(CollectBatchC)]
+    L.fsdkr_collect_prepare.restype = ctypes.c_int
+    L.fsdkr_collect_run.argtypes = [vp, ctypes.POINTER(VerdictsC)]
+    L.fsdkr_collect_run.restype = ctypes.c_int
     L.fsdkr_collect_first_error.argtypes = [ctypes.POINTER(CollectBatchC), ctypes.POINTER(VerdictsC),
                                             ctypes.POINTER(ErrorC)]
     L.fsdkr_collect_first_error.restype = ctypes.c_int
@@ -187,6 +191,17 @@ class Context:
         from .batch import Verdicts
         v = Verdicts(batch.R, batch.J, batch.n)
         self.check(self._lib.fsdkr_verify_collect(self._h, ctypes.byref(batch.c), ctypes.byref(v.c)))
+        return v
+
+    def collect_prepare(self, batch):
+        """Host pre-pass + one upload of the batch image (device-resident afterwards)."""
+        self.check(self._lib.fsdkr_collect_prepare(self._h, ctypes.byref(batch.c)))
+
+    def collect_run(self, batch):
+        """Kernel pipeline on the prepared batch; returns Verdicts."""
+        from .batch import Verdicts
+        v = Verdicts(batch.R, batch.J, batch.n)
+        self.check(self._lib.fsdkr_collect_run(self._h, ctypes.byref(v.c)))
         return v
 
     def paillier_decrypt(self, cts, p, q, nl):

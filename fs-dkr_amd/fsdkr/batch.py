@@ -73,10 +73,12 @@ class CollectBatch:
     (refresh_message.rs:149-175): then only the counts are filled and the
     first error is decided without the GPU."""
 
-    def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048):
+    def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048, n_recv=None):
+        """n_recv: receivers (default R + J); a multi-GPU shard passes its slice of
+        the messages together with the full receiver count."""
         msgs, joins = list(refresh_messages), list(join_messages)
         R, J = len(msgs), len(joins)
-        n = R + J
+        n = n_recv if n_recv else R + J
         self.R, self.J, self.n = R, J, n
         self._keep = []
         c = CollectBatchC()
@@ -85,6 +87,7 @@ class CollectBatch:
         lens = np.array([[len(m.pdl_proof_vec), len(m.points_committed_vec), len(m.points_encrypted_vec)]
                          for m in msgs] or [[0, 0, 0]], dtype=np.uint32)
         c.party_index, c.msg_lens = self._k(pidx), self._k(lens)
+        c.n_recv = n if n_recv else 0
         self.c = c
         ref = lens[0][0] if R else 0
         self.header_only = (R <= local_key.t or R == 0 or any(tuple(l) != (ref, ref, ref) for l in lens[:R])

@@ -118,6 +118,9 @@ typedef struct fsdkr_collect_batch {
   /* join messages: dlog_statement {N, g, ni} and the two CompositeDLogProofs */
   const uint32_t *dlog_N, *dlog_g, *dlog_ni, *dlog_x1, *dlog_x2;      /* [J][nl]  */
   const uint32_t *dlog_y1, *dlog_y2;                                  /* [J][yl]  */
+  /* receivers; 0 means R + J.  A multi-GPU shard passes a slice of the refresh
+   * messages (and of the joins' proofs) with the full receiver set n. */
+  uint32_t n_recv;
 } fsdkr_collect_batch;
 
 /* Verdicts (caller-allocated). 1 bits mean "check passed". */
@@ -131,6 +134,12 @@ typedef struct fsdkr_verdicts {
 } fsdkr_verdicts;
 
 int fsdkr_verify_collect(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch, fsdkr_verdicts* out);
+
+/* The same as two phases: prepare = host pre-pass + ONE host->device copy of
+ * the batch image (kept in the context); run = the kernel pipeline on the
+ * device-resident batch + verdict readback.  run may be repeated. */
+int fsdkr_collect_prepare(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
+int fsdkr_collect_run(fsdkr_ctx* ctx, fsdkr_verdicts* out);
 
 /* FsDkrError variants, in error.rs declaration order (error.rs:6-60). */
 #define FSDKR_ERR_NONE 0
