@@ -232,7 +232,7 @@ def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256):
     for k in range(R):
         pts_sc += [[a] for a in coeffs[k]]
     for k in range(R):
-        pts_sc += [[pr[k, i]["alpha"]] for i in range(n)]
+        pts_sc += [[pr[k, i]["alpha"] % Q] for i in range(n)]   # Scalar::from(alpha) reduces mod q
     ecres = ctx.ec_msm([[G]] * len(pts_sc), pts_sc)
     committed = [ecres[k * n:(k + 1) * n] for k in range(R)]
     off = R * n
