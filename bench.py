@@ -178,45 +178,27 @@ def main():
     tg = time.perf_counter()
     msgs, joins, lk = synth.synth_collect(ctx, R, J, t, a.seed, key_bits=a.key_bits)
     gen_s = time.perf_counter() - tg
-    # shard: contiguous slices of the refresh messages and of the joins
-    r0, r1 = rank * R // world, (rank + 1) * R // world
-    j0, j1 = rank * J // world, (rank + 1) * J // world
+    # shard: contiguous slices of the refresh messages and of the joins (fsdkr.shard)
+    from fsdkr import shard
+    r0, r1 = shard.shard_range(R, world, rank)
+    j0, j1 = shard.shard_range(J, world, rank)
     batch = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], 256, a.key_bits, n_recv=n)
     ctx.collect_prepare(batch)
     P = R * n
-    allv = None
-    if dist is not None:
-        allv = torch.zeros(3 * P + 2 * (R + J) + max(J, 1), dtype=torch.uint8, device="cuda")
+    dev = torch.device("cuda", local)
 
     def step():
         v = ctx.collect_run(batch)
         if dist is not None:
-            allv.zero_()
-            host = np.zeros(allv.numel(), np.uint8)
-            pr = (r1 - r0) * n
-            host[r0 * n:r0 * n + pr] = v.feldman
-            host[P + r0 * n:P + r0 * n + pr] = v.pdl
-            host[2 * P + r0 * n:2 * P + r0 * n + pr] = v.range
-            mr = list(range(r1 - r0)) + [r1 - r0 + q for q in range(j1 - j0)]
-            gm = list(range(r0, r1)) + [R + q for q in range(j0, j1)]
-            for lm, g in zip(mr, gm):
-                host[3 * P + g] = v.ped[lm]
-                host[3 * P + (R + J) + g] = v.ck[lm]
-            allv.copy_(torch.from_numpy(host))
-            dist.all_reduce(allv, op=dist.ReduceOp.MAX)
-            host = allv.cpu().numpy()
-            return host
+            return shard.MergedVerdicts(shard.merge(dist, shard.scatter(v, R, J, n, world, rank), dev), R, J, n)
         return v
 
     for _ in range(a.warmup):
         res = step()
     # correctness gate: every synthetic proof verifies
-    if dist is None:
-        from fsdkr.batch import CollectBatch as _CB  # noqa: F401
-        assert res.feldman.all() and (res.pdl == 7).all() and res.range.all() and (res.ped == 1).all() and \
-            res.ck.all() and (res.dlog[:J] == 3).all(), "synthetic workload failed verification"
-    else:
-        assert (res[:P] == 1).all() and (res[P:2 * P] == 7).all() and (res[2 * P:3 * P] == 1).all()
+    assert res.feldman[:P].all() and (res.pdl[:P] == 7).all() and res.range[:P].all() and \
+        (res.ped[:R + J] == 1).all() and res.ck[:R + J].all() and (res.dlog[:J] == 3).all(), \
+        "synthetic workload failed verification"
     ctx.kernel_time_reset()
     if dist is not None:
         dist.barrier()
