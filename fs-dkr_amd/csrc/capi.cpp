@@ -13,6 +13,8 @@
 
 #include "ctx.hpp"
 #include "kernels.h"
+#include "verify.h"
+#include "verify.h"
 
 using namespace fsdkr;
 
@@ -109,7 +111,8 @@ uint32_t choose_window(uint32_t ebits) {
 
 // Launch one modexp job whose descriptors are already in device memory.
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
-                       const uint32_t* d_consts, uint32_t* d_out, hipStream_t st, const char* table_tag) {
+                       const uint32_t* d_consts, uint32_t* d_out, hipStream_t st, const char* table_tag,
+                       uint32_t prio) {
   if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
   const int KD = shape_digits(k32);
@@ -132,12 +135,15 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.base_len = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8);
   a.exp_len = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + n4);
   a.mod_idx = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 2 * n4);
+  a.nwin_i = reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 3 * n4);
   a.nwin = nwin;
   a.window = w;
   a.consts = d_consts;
   a.out = d_out;
   a.table = d_table;
   a.count = count;
+  a.prio = prio;
+  a.group = c->modexp_group;
   const size_t tm = c->tbeg("modexp", st);
   int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
   c->tend(tm, st);
@@ -153,6 +159,9 @@ void ModexpJob::pack(std::vector<uint8_t>& dst) const {
   memcpy(dst.data() + o + 2 * n8, base_len.data(), n4);
   memcpy(dst.data() + o + 2 * n8 + n4, exp_len.data(), n4);
   memcpy(dst.data() + o + 2 * n8 + 2 * n4, mod_idx.data(), n4);
+  const uint32_t w = choose_window(exp_bits ? exp_bits : 1);
+  uint32_t* nw = reinterpret_cast<uint32_t*>(dst.data() + o + 2 * n8 + 3 * n4);
+  for (size_t k = 0; k < size(); ++k) nw[k] = ebits[k] ? (ebits[k] + w - 1) / w : 1u;
 }
 
 // Upload a modexp descriptor set and launch it against prepared constants.
@@ -209,6 +218,7 @@ int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_ba
   job.exp_ptr.resize(count);
   job.base_len.assign(count, k32);
   job.exp_len.assign(count, exp_limbs);
+  job.ebits.assign(count, exp_bits);
   job.mod_idx.resize(count);
   for (uint32_t i = 0; i < count; ++i) {
     job.base_ptr[i] = (uint64_t)(uintptr_t)(d_base + (size_t)i * k32);
@@ -279,6 +289,66 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
 const char* fsdkr_last_error(const fsdkr_ctx* ctx) {
   const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
   return c ? c->err.c_str() : "null context";
+}
+
+int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16)) return FSDKR_E_ARG;
+  c->modexp_group = lanes;
+  return FSDKR_OK;
+}
+
+int fsdkr_mod_inverse(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* y, const uint32_t* m,
+                      uint32_t* out, uint32_t* unit) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!y || !m || !unit) {
+    c->fail("fsdkr_mod_inverse: null pointer");
+    return FSDKR_E_ARG;
+  }
+  if (!shape_digits(mod_limbs)) {
+    c->fail("fsdkr_mod_inverse: unsupported modulus width %u limbs", mod_limbs);
+    return FSDKR_E_UNSUPPORTED;
+  }
+  for (uint32_t i = 0; i < count; ++i)
+    if ((m[(size_t)i * mod_limbs] & 1u) == 0) {
+      c->fail("fsdkr_mod_inverse: modulus %u is even", i);
+      return FSDKR_E_ARG;
+    }
+  const size_t nb = sizeof(uint32_t) * (size_t)count * mod_limbs;
+  uint8_t* d = (uint8_t*)c->buf("inv_io", 3 * nb + 2 * 8 * (size_t)count + 4 * (size_t)count + 1024);
+  if (!d) {
+    c->fail("fsdkr_mod_inverse: device allocation failed");
+    return FSDKR_E_OOM;
+  }
+  uint32_t* d_y = (uint32_t*)d;
+  uint32_t* d_m = (uint32_t*)(d + nb);
+  uint32_t* d_o = (uint32_t*)(d + 2 * nb);
+  uint64_t* d_yp = (uint64_t*)(d + 3 * nb);
+  uint64_t* d_mp = d_yp + count;
+  uint32_t* d_u = (uint32_t*)(d_mp + count);
+  std::vector<uint64_t> ptrs(2 * (size_t)count);
+  for (uint32_t i = 0; i < count; ++i) {
+    ptrs[i] = (uint64_t)(uintptr_t)(d_y + (size_t)i * mod_limbs);
+    ptrs[count + i] = (uint64_t)(uintptr_t)(d_m + (size_t)i * mod_limbs);
+  }
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_y, y, nb, hipMemcpyHostToDevice, c->stream), "H2D y")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_m, m, nb, hipMemcpyHostToDevice, c->stream), "H2D m")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_yp, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice, c->stream),
+                         "H2D ptrs")))
+    return rc;
+  InverseArgs a{d_yp, d_mp, d_o, d_u, nullptr, count};
+  c->mark("inverse", true);
+  rc = c->hip_check(launch_inverse(mod_limbs, a, c->stream), "inverse launch");
+  c->mark("inverse", false);
+  if (rc) return rc;
+  if (out && (rc = c->hip_check(hipMemcpyAsync(out, d_o, nb, hipMemcpyDeviceToHost, c->stream), "D2H inv")))
+    return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(unit, d_u, 4 * (size_t)count, hipMemcpyDeviceToHost, c->stream), "D2H unit")))
+    return rc;
+  return c->sync();
 }
 
 int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* base,

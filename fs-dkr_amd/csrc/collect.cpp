@@ -311,15 +311,19 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   const size_t x_epdl = L.out((size_t)P * 8 * 4);
   const size_t x_pbits = L.out((size_t)Mt * ((M + 31) / 32) * 4), x_ppanic = L.out((size_t)Mt * 4);
   const size_t x_Bpdl = L.out((size_t)P * nn * 4), x_gs1 = L.out((size_t)P * nn * 4);
-  const size_t x_J1 = L.out((size_t)2 * P * nn * 4);   // s2^N | s^N
-  const size_t x_J2 = L.out((size_t)2 * P * nn * 4);   // c^e_pdl | c^e_A
-  const size_t x_J3 = L.out((size_t)2 * P * nl * 4);   // h1^s1 | h1^s1A
-  const size_t x_J4 = L.out((size_t)2 * P * nl * 4);   // h2^s3 | h2^s2A
-  const size_t x_J5 = L.out((size_t)2 * P * nl * 4);   // z^e_pdl | zA^e_A
-  const size_t x_J6 = L.out((size_t)(Mt * M + Mt * CK_M2) * nl * 4);  // T^Z | sigma^n
-  const size_t x_J7 = L.out((size_t)(2 * J + 1) * nl * 4);           // g^y1 | ni^y2
-  const size_t x_J8 = L.out((size_t)(2 * J + 1) * nl * 4);           // ni^e1 | g^e2
-  const size_t x_J9 = L.out((size_t)P * nn * 4);                     // (N+1)^s1 (s1 >= N only)
+  // modexp outputs, laid out per merged launch (instance k of a launch writes slot k):
+  //   GA (nn, long)  = J1 s2^N | s^N  [2P]  ++  J9 (N+1)^s1 for s1 >= N  [<= P]
+  //   J2 (nn, short) = c^e_pdl | c^e_A  [2P]
+  //   J5 (nl, short) = z^e_pdl | zA^e_A [2P]
+  //   GD (nl, long)  = J4 h2^s3 | h2^s2A [2P] ++ J7 g^y1 | ni^y2 [2J] ++ J6 T^Z | sigma^n [Mt(M+11)]
+  //                    ++ J3 h1^s1 | h1^s1A [2P] ++ J8 ni^e1 | g^e2 [2J]      (longest exponents first)
+  const size_t x_GA = L.out((size_t)3 * P * nn * 4 + 4);
+  const size_t x_J1 = x_GA, x_J9 = x_GA + (size_t)2 * P * nn * 4;
+  const size_t x_J2 = L.out((size_t)2 * P * nn * 4);
+  const size_t x_J5 = L.out((size_t)2 * P * nl * 4);
+  const size_t x_GD = L.out(((size_t)4 * P + 4 * J + (size_t)Mt * (M + CK_M2) + 1) * nl * 4);
+  const size_t x_J4 = x_GD, x_J7 = x_J4 + (size_t)2 * P * nl * 4, x_J6 = x_J7 + (size_t)2 * J * nl * 4;
+  const size_t x_J3 = x_J6 + (size_t)Mt * (M + CK_M2) * nl * 4, x_J8 = x_J3 + (size_t)2 * P * nl * 4;
   const size_t x_invc = L.out((size_t)2 * P * nn * 4), x_invz = L.out((size_t)P * nl * 4);
   const size_t x_unn = L.out((size_t)2 * P * 4);    // unit flags of the nn inverses (c^eA, then extra c^e_pdl)
   const size_t x_uzA = L.out((size_t)P * 4), x_uzp = L.out((size_t)P * 4);
@@ -337,7 +341,7 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   // upper bound of descriptor bytes
   const size_t n_inst_nn = 2 * P + 2 * P + (any_big_s1 ? P : 0);
   const size_t n_inst_nl = 2 * P * 3 + (size_t)Mt * (M + CK_M2) + 4 * J;
-  const size_t desc_bound = (n_inst_nn + n_inst_nl) * 28 + 16 * 256 +
+  const size_t desc_bound = (n_inst_nn + n_inst_nl) * 32 + 16 * 256 +
                             ((size_t)P + (size_t)Mt * M + (size_t)Mt * CK_M2 + 2 * J + P) * sizeof(EqOperand) +
                             2 * (size_t)P * sizeof(Prod3Operand) + (size_t)(2 * P + 2 * P) * 16 + (size_t)4 * P * 8 +
                             (size_t)(2 * P + 2 * P) * 4 + 64 * 1024;
@@ -408,9 +412,13 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     j.pack(L.host);
     return o;
   };
-  const size_t d_J1 = pack_job(J1), d_J2 = pack_job(J2), d_J3 = pack_job(J3), d_J4 = pack_job(J4);
-  const size_t d_J5 = pack_job(J5), d_J6 = pack_job(J6), d_J7 = pack_job(J7), d_J8 = pack_job(J8);
-  const size_t d_J9 = pack_job(J9);
+  ModexpJob GA = J1, GD = J4;
+  GA.append(J9);
+  GD.append(J7);
+  GD.append(J6);
+  GD.append(J3);
+  GD.append(J8);
+  const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD);
 
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N
   std::vector<uint64_t> bs_ptr(2 * (size_t)P), bn_ptr(2 * (size_t)P);
@@ -555,10 +563,11 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   pl.o_ps1 = o_ps1; pl.o_pA = o_pA; pl.o_az = o_az; pl.o_ae = o_ae; pl.o_vss = o_vss; pl.o_NN = o_NN;
   pl.o_mods = o_mods; pl.o_one = o_one; pl.o_rn = o_rn;
   pl.x_epdl = x_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
-  const size_t xs[10] = {x_J1, x_J2, x_J9, x_J3, x_J4, x_J5, x_J6, x_J7, x_J8, 0};
-  const size_t ds[10] = {d_J1, d_J2, d_J9, d_J3, d_J4, d_J5, d_J6, d_J7, d_J8, 0};
-  const ModexpJob* js[9] = {&J1, &J2, &J9, &J3, &J4, &J5, &J6, &J7, &J8};
-  for (int k = 0; k < 9; ++k) {
+  // launch order = stream assignment in collect_run: GA, GD (long), J2, J5 (short, feed the inverses)
+  const size_t xs[4] = {x_GA, x_GD, x_J2, x_J5};
+  const size_t ds[4] = {d_GA, d_GD, d_J2, d_J5};
+  const ModexpJob* js[4] = {&GA, &GD, &J2, &J5};
+  for (int k = 0; k < 4; ++k) {
     pl.x_J[k] = xs[k];
     pl.d_J[k] = ds[k];
     pl.jk32[k] = js[k]->k32;
@@ -622,17 +631,16 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   uint32_t *cons_nn = nullptr, *cons_nl = nullptr;
   if ((rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn, "collect_nn"))) return rc;
   if ((rc = setup_moduli(c, nl, PI(o_mods), n_mods_nl, &cons_nl, "collect_nl"))) return rc;
-  // challenges
+  // ---- stream plan (HIP maps streams onto 4 hardware queues, so at most 4 lanes of work):
+  //   st      : pdl_hash, binom x2 | fork | ped_hash, J5, nl inverses, pdl_u1, Feldman | join | eq, prod3, alice
+  //   side 0  : GA  (nn, long exponents)
+  //   side 1  : GD  (nl, long exponents)
+  //   side 2  : J2 (nn, 256-bit challenges) -> nn inverses
   {
     PdlHashArgs a{PI(o_Q), PI(o_enc), PI(o_pz), PI(o_pu1), PI(o_pu2), PI(o_pu3), nn, nl, PX(x_epdl), P};
     c->mark("pdl_hash", true);
     rc = c->hip_check(launch_pdl_hash(a, st), "pdl_hash");
     c->mark("pdl_hash", false);
-    if (rc) return rc;
-    PedHashArgs h{PI(o_pA), M, nl, PX(x_pbits), PX(x_ppanic), Mt};
-    c->mark("ped_hash", true);
-    rc = c->hip_check(launch_ped_hash(h, st), "ped_hash");
-    c->mark("ped_hash", false);
     if (rc) return rc;
   }
   {
@@ -641,41 +649,44 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     BinomArgs a2{(const uint64_t*)(dev + d_bs) + P, (const uint64_t*)(dev + d_bn) + P, pl.s1l, nl, nn, PX(x_gs1), P};
     if ((rc = c->hip_check(launch_binom(a2, st), "binom"))) return rc;
   }
-  // the nine modexp jobs are independent: run them concurrently on side streams
-  {
-    hipEvent_t ready;
-    if ((rc = c->hip_check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event"))) return rc;
-    (void)hipEventRecord(ready, st);
-    static const char* tags[9] = {"mxt_J1", "mxt_J2", "mxt_J9", "mxt_J3", "mxt_J4", "mxt_J5", "mxt_J6", "mxt_J7",
-                                  "mxt_J8"};
-    std::vector<hipEvent_t> done;
-    for (int k = 0; k < 9; ++k) {
-      if (!pl.jcount[k]) continue;
-      hipStream_t ss = c->side_stream(k);
-      (void)hipStreamWaitEvent(ss, ready, 0);
-      const uint32_t* cons = (pl.jk32[k] == nn) ? cons_nn : cons_nl;
-      if ((rc = launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
-                                   tags[k])))
-        return rc;
-      hipEvent_t ev;
-      if ((rc = c->hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return rc;
-      (void)hipEventRecord(ev, ss);
-      done.push_back(ev);
+  hipEvent_t ready;
+  if ((rc = c->hip_check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event"))) return rc;
+  (void)hipEventRecord(ready, st);
+  std::vector<hipEvent_t> done;
+  static const char* tags[4] = {"mxt_GA", "mxt_GD", "mxt_J2", "mxt_J5"};
+  auto launch_group = [&](int k, hipStream_t ss) -> int {
+    if (!pl.jcount[k]) return FSDKR_OK;
+    const uint32_t* cons = (pl.jk32[k] == nn) ? cons_nn : cons_nl;
+    // GA (4096-bit moduli, 2048-bit exponents) is the longest chain: its waves get issue priority
+    return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
+                              tags[k], k == 0 ? 1u : 0u);
+  };
+  for (int k = 0; k < 3; ++k) {
+    hipStream_t ss = c->side_stream(k);
+    (void)hipStreamWaitEvent(ss, ready, 0);
+    if ((rc = launch_group(k, ss))) return rc;
+    if (k == 2) {  // nn inverses right behind the challenges' modexps
+      InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
+                    PX(x_scr128), pl.n_inv_nn};
+      c->mark("inverse", true, ss);
+      rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
+      c->mark("inverse", false, ss);
+      if (rc) return rc;
     }
-    for (hipEvent_t ev : done) {
-      (void)hipStreamWaitEvent(st, ev, 0);
-      (void)hipEventDestroy(ev);
-    }
-    (void)hipEventDestroy(ready);
+    hipEvent_t ev;
+    if ((rc = c->hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return rc;
+    (void)hipEventRecord(ev, ss);
+    done.push_back(ev);
   }
-  // inverses
   {
-    InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
-                  PX(x_scr128), pl.n_inv_nn};
-    c->mark("inverse", true);
-    rc = c->hip_check(launch_inverse(nn, a, st), "inverse nn");
-    c->mark("inverse", false);
+    PedHashArgs h{PI(o_pA), M, nl, PX(x_pbits), PX(x_ppanic), Mt};
+    c->mark("ped_hash", true);
+    rc = c->hip_check(launch_ped_hash(h, st), "ped_hash");
+    c->mark("ped_hash", false);
     if (rc) return rc;
+  }
+  if ((rc = launch_group(3, st))) return rc;
+  {
     InverseArgs b1{(const uint64_t*)(dev + d_iynl), (const uint64_t*)(dev + d_imnl), PX(x_invz), PX(x_uzA),
                    PX(x_scr64), P};
     c->mark("inverse", true);
@@ -686,6 +697,23 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
                    PX(x_scr64), P};
     if ((rc = c->hip_check(launch_inverse(nl, b2, st), "inverse nl 2"))) return rc;
   }
+  {
+    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
+    c->mark("ec", true);
+    rc = c->hip_check(launch_pdl_u1(u, st), "pdl_u1");
+    c->mark("ec", false);
+    if (rc) return rc;
+    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
+    c->mark("ec", true);
+    rc = c->hip_check(launch_feldman(f, st), "feldman");
+    c->mark("ec", false);
+    if (rc) return rc;
+  }
+  for (hipEvent_t ev : done) {
+    (void)hipStreamWaitEvent(st, ev, 0);
+    (void)hipEventDestroy(ev);
+  }
+  (void)hipEventDestroy(ready);
   // equality checks and exact products
   {
     EqCheckArgs a{(const EqOperand*)(dev + d_eqnn), PI(d_eqnnm), cons_nn, PX(x_pbits), DI(o_one), PX(x_eq2),
@@ -712,16 +740,6 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     c->mark("alice_hash", true);
     rc = c->hip_check(launch_alice_hash(a, st), "alice_hash");
     c->mark("alice_hash", false);
-    if (rc) return rc;
-    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
-    c->mark("ec", true);
-    rc = c->hip_check(launch_pdl_u1(u, st), "pdl_u1");
-    c->mark("ec", false);
-    if (rc) return rc;
-    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
-    c->mark("ec", true);
-    rc = c->hip_check(launch_feldman(f, st), "feldman");
-    c->mark("ec", false);
     if (rc) return rc;
   }
   // ---------------- results

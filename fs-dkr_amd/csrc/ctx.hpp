@@ -43,10 +43,13 @@ struct Ctx {
   // grow-only named device buffer (contents undefined after growth)
   void* buf(const char* name, size_t bytes);
   // HIP-event brackets around a kernel launch (timing mode only); st = nullptr: main stream
-  void mark(const char* name, bool begin) { if (begin) tbeg(name, stream); else tend(last_mark, stream); }
+  void mark(const char* name, bool begin, hipStream_t st = nullptr) {
+    if (begin) tbeg(name, st ? st : stream); else tend(last_mark, st ? st : stream);
+  }
   size_t tbeg(const char* name, hipStream_t st);
   void tend(size_t idx, hipStream_t st);
   size_t last_mark = (size_t)-1;
+  uint32_t modexp_group = 0;   // lanes per modexp instance (0 = by batch size)
   hipStream_t side_stream(int k);
   // synchronise the stream and fold pending events into `times`
   int sync();
@@ -60,17 +63,29 @@ struct ModexpJob {
   std::vector<uint64_t> base_ptr, exp_ptr;   // device addresses
   std::vector<uint32_t> base_len, exp_len;   // limbs
   std::vector<uint32_t> mod_idx;
-  void add(uint64_t b, uint32_t blen, uint64_t e, uint32_t elen, uint32_t ebits, uint32_t m) {
+  std::vector<uint32_t> ebits;               // per-instance exponent bit bound
+  void add(uint64_t b, uint32_t blen, uint64_t e, uint32_t elen, uint32_t eb, uint32_t m) {
     base_ptr.push_back(b);
     base_len.push_back(blen);
     exp_ptr.push_back(e);
     exp_len.push_back(elen);
     mod_idx.push_back(m);
-    if (ebits > exp_bits) exp_bits = ebits;
+    ebits.push_back(eb);
+    if (eb > exp_bits) exp_bits = eb;
+  }
+  // append another job's instances (same modulus width): one merged launch
+  void append(const ModexpJob& o) {
+    base_ptr.insert(base_ptr.end(), o.base_ptr.begin(), o.base_ptr.end());
+    exp_ptr.insert(exp_ptr.end(), o.exp_ptr.begin(), o.exp_ptr.end());
+    base_len.insert(base_len.end(), o.base_len.begin(), o.base_len.end());
+    exp_len.insert(exp_len.end(), o.exp_len.begin(), o.exp_len.end());
+    mod_idx.insert(mod_idx.end(), o.mod_idx.begin(), o.mod_idx.end());
+    ebits.insert(ebits.end(), o.ebits.begin(), o.ebits.end());
+    if (o.exp_bits > exp_bits) exp_bits = o.exp_bits;
   }
   size_t size() const { return base_ptr.size(); }
-  size_t desc_bytes() const { return size() * (8 + 8 + 4 + 4 + 4); }
-  // append base_ptr | exp_ptr | base_len | exp_len | mod_idx
+  size_t desc_bytes() const { return size() * (8 + 8 + 4 + 4 + 4 + 4); }
+  // append base_ptr | exp_ptr | base_len | exp_len | mod_idx | nwin (window of choose_window(exp_bits))
   void pack(std::vector<uint8_t>& dst) const;
 };
 
@@ -79,7 +94,7 @@ void free_collect_plan(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag);
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st = nullptr,
-                       const char* table_tag = "mxtable");
+                       const char* table_tag = "mxtable", uint32_t prio = 0);
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag);
 int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
                       uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,

@@ -16,11 +16,14 @@ struct ModexpArgs {
   const uint32_t* exp_len;   // [count] limbs
   uint32_t nwin;             // windows of `window` bits, taken from bit nwin*window-1 down
   uint32_t window;
+  const uint32_t* nwin_i;    // [count] per-instance window count (overrides nwin; merged launches)
   const uint32_t* mod_idx;   // [count] row of `consts`
   const uint32_t* consts;    // [n_mod][3*KD+4]  from mod_setup
   uint32_t* out;             // [count][K32]
   uint32_t* table;           // [count][2^window][KD] scratch
   uint32_t count;
+  uint32_t prio;             // 1: latency-critical launch, waves raise their issue priority (s_setprio)
+  uint32_t group;            // lanes per instance (0 = choose by batch size)
 };
 
 int shape_digits(uint32_t k32);   // KD for a K32-limb modulus class (0 if unsupported)

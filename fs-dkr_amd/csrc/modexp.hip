@@ -12,6 +12,8 @@
 // operand of every Montgomery product in LDS.
 #include "mont29.hpp"
 #include "kernels.h"
+#include <cstdlib>
+#include <initializer_list>
 
 namespace fsdkr {
 
@@ -91,6 +93,9 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   const int li = threadIdx.x / G;
   const uint32_t inst = blockIdx.x * IPB + li;
   if (inst >= a.count) return;
+  // a latency-critical launch sharing the chip with throughput launches on other
+  // streams: its waves win the SIMD issue arbitration
+  if (a.prio) __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
   MT M;
@@ -111,7 +116,7 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);
 #pragma unroll
   for (int j = 0; j < L; ++j) T[g * L + j] = C[KD + g * L + j];             // T[0] = R mod N
-  const uint32_t nwin = a.nwin;
+  const uint32_t nwin = a.nwin_i ? max(1u, a.nwin_i[inst]) : a.nwin;
   auto digit = [&](uint32_t k) -> uint32_t {
     const uint32_t p = (nwin - 1 - k) * w;
     const uint32_t lo = p >> 5, sh = p & 31;
@@ -214,12 +219,45 @@ hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_
   }
 }
 
+// Lanes per instance.  G with L = KD/G = 36 digits per lane is the most
+// efficient per MAC once a launch fills the chip; a launch that cannot fill it
+// runs with more lanes per instance (L = 18 or 9) for lower latency: the
+// largest G whose lanes still fit the resident-wave capacity.
+// ModexpArgs.group or FSDKR_MODEXP_G=<G> force a group size (tuning, tests).
+static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int> allowed) {
+  static int forced_env = -1;
+  if (forced_env < 0) {
+    const char* e = getenv("FSDKR_MODEXP_G");
+    forced_env = e ? atoi(e) : 0;
+  }
+  const int forced = forced_arg ? forced_arg : forced_env;
+  for (int g : allowed)
+    if (g == forced) return g;
+  constexpr uint64_t kLaneCapacity = 256ull * 4 * 3 * 64;   // CUs x SIMDs x resident waves x lanes
+  int best = *allowed.begin();
+  for (int g : allowed)
+    if ((uint64_t)count * (uint64_t)g <= kLaneCapacity) best = g;
+  return best;
+}
+
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
   switch (k32) {
-    case 64: return launch_modexp<72, 2, 64>(a, st);
+    case 64:
+      switch (pick_group(a.count, (int)a.group, {2, 4, 8})) {
+        case 8: return launch_modexp<72, 8, 64>(a, st);
+        case 4: return launch_modexp<72, 4, 64>(a, st);
+        default: return launch_modexp<72, 2, 64>(a, st);
+      }
     case 96: return launch_modexp<108, 4, 96>(a, st);
-    case 128: return launch_modexp<144, 4, 128>(a, st);
-    case 192: return launch_modexp<216, 4, 192>(a, st);
+    case 128:
+      switch (pick_group(a.count, (int)a.group, {4, 8, 16})) {
+        case 16: return launch_modexp<144, 16, 128>(a, st);
+        case 8: return launch_modexp<144, 8, 128>(a, st);
+        default: return launch_modexp<144, 4, 128>(a, st);
+      }
+    case 192:
+      return pick_group(a.count, (int)a.group, {4, 8}) == 8 ? launch_modexp<216, 8, 192>(a, st)
+                                                            : launch_modexp<216, 4, 192>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

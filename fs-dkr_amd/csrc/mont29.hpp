@@ -7,8 +7,10 @@
 // inner loop is ONE v_mad_u64_u32 per MAC with no carry chain; carries are
 // resolved by a cheap parallel normalisation every 18 rows.
 //
-// Layout: a KD-digit integer is owned by G consecutive lanes (G in {2,4}, one
-// DPP quad); lane g holds digits [g*L, g*L+L), L = KD/G.  Row-oriented CIOS:
+// Layout: a KD-digit integer is owned by G consecutive lanes (G in {2,4,8,16}:
+// one DPP quad or part of one 16-lane DPP row); lane g holds digits
+// [g*L, g*L+L), L = KD/G.  Larger G = lower latency per instance (small
+// batches), smaller G = fewer cross-lane ops per MAC (full chip).  Row-oriented CIOS:
 // row i broadcasts digit a_i of the streamed operand (LDS) to the group, every
 // lane adds a_i*b and m_i*n into its L column accumulators, lane 0 folds the
 // retired column's carry and the accumulator shifts one digit down (register
@@ -29,38 +31,53 @@ namespace fsdkr {
 
 constexpr uint32_t M29 = (1u << 29) - 1;
 
-// ---- intra-quad DPP helpers (quad_perm) --------------------------------------
+// ---- intra-group DPP helpers --------------------------------------------------
+// G <= 4: quad_perm inside one DPP quad.  G = 8/16: row_shr/row_shl:1 inside a
+// 16-lane row (group boundaries masked by the caller), row_newbcast:n for the
+// broadcasts (two bank-masked moves for the two 8-lane groups of a row).
+#define FSDKR_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_mov_dpp((int)(v), (ctrl), 0xF, 0xF, false))
+#define FSDKR_DPP_BANK(old, v, ctrl, bank) \
+  ((uint32_t)__builtin_amdgcn_update_dpp((int)(old), (int)(v), (ctrl), 0xF, (bank), false))
+
 template <int G>
 __device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
   if constexpr (G == 1) return v;
-  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
-  else return __builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);                       // [0,0,0,0]
+  else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
+  else if constexpr (G == 4) return FSDKR_DPP(v, 0x00);   // [0,0,0,0]
+  else if constexpr (G == 8) return FSDKR_DPP_BANK(FSDKR_DPP_BANK(v, v, 0x150, 0x3), v, 0x158, 0xC);
+  else return FSDKR_DPP(v, 0x150);                        // row_newbcast:0
 }
 template <int G>
 __device__ __forceinline__ uint32_t bcast_top(uint32_t v) {
   if constexpr (G == 1) return v;
-  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
-  else return __builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, false);                       // [3,3,3,3]
+  else if constexpr (G == 2) return FSDKR_DPP(v, 0xF5);   // [1,1,3,3]
+  else if constexpr (G == 4) return FSDKR_DPP(v, 0xFF);   // [3,3,3,3]
+  else if constexpr (G == 8) return FSDKR_DPP_BANK(FSDKR_DPP_BANK(v, v, 0x157, 0x3), v, 0x15F, 0xC);
+  else return FSDKR_DPP(v, 0x15F);                        // row_newbcast:15
 }
-// raw value of lane g+1 (top lane reads itself: caller masks)
+// raw value of lane g+1 (top lane: caller masks)
 template <int G>
 __device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
   if constexpr (G == 1) return v;
-  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xF5, 0xF, 0xF, false);  // [1,1,3,3]
-  else return __builtin_amdgcn_mov_dpp((int)v, 0xF9, 0xF, 0xF, false);                       // [1,2,3,3]
+  else if constexpr (G == 2) return FSDKR_DPP(v, 0xF5);   // [1,1,3,3]
+  else if constexpr (G == 4) return FSDKR_DPP(v, 0xF9);   // [1,2,3,3]
+  else return FSDKR_DPP(v, 0x101);                        // row_shl:1
 }
-// raw value of lane g-1 (lane 0 reads itself: caller masks)
+// raw value of lane g-1 (lane 0: caller masks)
 template <int G>
 __device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {
   if constexpr (G == 1) return v;
-  else if constexpr (G == 2) return __builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // [0,0,2,2]
-  else return __builtin_amdgcn_mov_dpp((int)v, 0x90, 0xF, 0xF, false);                       // [0,0,1,2]
+  else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
+  else if constexpr (G == 4) return FSDKR_DPP(v, 0x90);   // [0,0,1,2]
+  else return FSDKR_DPP(v, 0x111);                        // row_shr:1
 }
 // group-wide max over the G lanes
 template <int G>
 __device__ __forceinline__ int group_max(int v) {
-  if constexpr (G >= 2) v = max(v, (int)__builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
-  if constexpr (G == 4) v = max(v, (int)__builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  if constexpr (G >= 2) v = max(v, (int)FSDKR_DPP(v, 0xB1));   // [1,0,3,2]
+  if constexpr (G >= 4) v = max(v, (int)FSDKR_DPP(v, 0x4E));   // [2,3,0,1]
+  if constexpr (G >= 8) v = max(v, (int)FSDKR_DPP(v, 0x141));  // row_half_mirror
+  if constexpr (G >= 16) v = max(v, (int)FSDKR_DPP(v, 0x140)); // row_mirror
   return v;
 }
 
@@ -89,7 +106,7 @@ struct Mont29 {
   static constexpr int L = KD / G;
   static_assert(KD % G == 0, "KD must split evenly over the group");
   // normalisation points inside one L-row cycle: at most 18 rows apart (bound: 31)
-  static constexpr int NSTEP = (L + 1) / 2 <= 18 ? (L + 1) / 2 : (L + 2) / 3;
+  static constexpr int NSTEP = L <= 18 ? L : (L + 1) / 2 <= 18 ? (L + 1) / 2 : (L + 2) / 3;
 
   uint32_t n[L];
   uint32_t ninv;      // -N^-1 mod 2^29

@@ -105,7 +105,7 @@ int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const ui
   const size_t b_r = b_m + (size_t)count * ml * 4, b_one = b_r + (size_t)count * nl * 4;
   const size_t b_gm = b_one + (size_t)nn * 4, b_rn = b_gm + (size_t)count * nn * 4;
   const size_t b_out = b_rn + (size_t)count * nn * 4, b_desc = b_out + (size_t)count * nn * 4;
-  const size_t total = b_desc + (size_t)count * (16 + 16 + sizeof(Prod3Operand) + 8) + 4096;
+  const size_t total = b_desc + (size_t)count * (16 + 32 + sizeof(Prod3Operand) + 4) + 8 * 256 + 4096;
   uint8_t* d = (uint8_t*)cx->buf("enc", total);
   if (!d) return FSDKR_E_OOM;
   std::vector<uint8_t> img(b_desc, 0);

@@ -13,13 +13,15 @@ namespace fsdkr {
 
 struct Sha256 {
   uint32_t h[8];
-  uint32_t w[16];   // pending block as big-endian words
+  uint32_t* w;      // pending block as big-endian words (device: a per-thread LDS slot, see init)
   uint32_t nbuf;    // bytes in pending block
   uint64_t total;   // bytes absorbed
+  uint32_t own[16]; // host storage (device code passes LDS: a dynamically indexed private array is scratch)
 
   FSDKR_HD static uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
-  FSDKR_HD void init() {
+  FSDKR_HD void init(uint32_t* buf = nullptr) {
+    w = buf ? buf : own;
     h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
     h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
     nbuf = 0;
@@ -77,6 +79,24 @@ struct Sha256 {
     }
   }
 
+  // four bytes x>>24, x>>16, x>>8, x (big-endian word) at any alignment
+  FSDKR_HD void word(uint32_t x) {
+    const uint32_t off = nbuf & 3, idx = nbuf >> 2;
+    if (off == 0) w[idx] = x;
+    else w[idx] |= x >> (8 * off);
+    nbuf += 4;
+    total += 4;
+    if (nbuf >= 64) {
+      compress();
+      nbuf -= 64;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w[i] = 0;
+      if (off) w[0] = x << (32 - 8 * off);
+    } else if (off) {
+      w[idx + 1] = x << (32 - 8 * off);
+    }
+  }
+
   FSDKR_HD void bytes(const uint8_t* p, uint32_t n) {
     for (uint32_t i = 0; i < n; ++i) byte(p[i]);
   }
@@ -94,13 +114,7 @@ struct Sha256 {
     int sh = 24;
     while (sh > 0 && ((v >> sh) & 0xffu) == 0) sh -= 8;
     for (; sh >= 0; sh -= 8) byte((uint8_t)(v >> sh));
-    for (int k = top - 1; k >= 0; --k) {
-      const uint32_t x = limbs[k];
-      byte((uint8_t)(x >> 24));
-      byte((uint8_t)(x >> 16));
-      byte((uint8_t)(x >> 8));
-      byte((uint8_t)x);
-    }
+    for (int k = top - 1; k >= 0; --k) word(limbs[k]);
   }
 
   // finalize; digest as a 256-bit little-endian limb array (= BigInt::from_bytes(digest))

@@ -108,6 +108,8 @@ hipError_t launch_pdl_hash(const PdlHashArgs& a, hipStream_t st);
 hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st);
 hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st);
 hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);
+// lane-cooperative variant (inverse.hip): registers + DPP, no scratch
+hipError_t launch_inverse_coop(uint32_t k32, const InverseArgs& a, hipStream_t st);
 hipError_t launch_eq_check(uint32_t k32, const EqCheckArgs& a, hipStream_t st);
 hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st);
 hipError_t launch_pdl_u1(const PdlU1Args& a, hipStream_t st);

@@ -15,6 +15,7 @@
 #include "secp256k1.hpp"
 #include "sha256.hpp"
 #include "verify.h"
+#include <cstdlib>
 
 namespace fsdkr {
 
@@ -80,8 +81,9 @@ __device__ __forceinline__ void absorb_point(Sha256& h, const uint32_t* p16) {
 __global__ void pdl_hash_kernel(const PdlHashArgs a) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.count) return;
+  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
   Sha256 h;
-  h.init();
+  h.init(sha_w + threadIdx.x * 16);
   for (int i = 0; i < 33; ++i) h.byte(G_COMPRESSED[i]);
   absorb_point(h, a.Q + (size_t)p * 16);
   h.bigint(a.c + (size_t)p * a.c_len, a.c_len);
@@ -97,8 +99,9 @@ __global__ void pdl_hash_kernel(const PdlHashArgs a) {
 __global__ void ped_hash_kernel(const PedHashArgs a) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= a.count) return;
+  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
   Sha256 h;
-  h.init();
+  h.init(sha_w + threadIdx.x * 16);
   const uint32_t* A = a.A + (size_t)m * a.M * a.a_len;
   for (uint32_t i = 0; i < a.M; ++i) h.bigint(A + (size_t)i * a.a_len, a.a_len);
   uint32_t e[8];
@@ -127,8 +130,9 @@ __global__ void alice_hash_kernel(const AliceHashArgs a) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.count) return;
   const uint32_t* N = P32(a.n_ptr[p]);
+  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
   Sha256 h;
-  h.init();
+  h.init(sha_w + threadIdx.x * 16);
   h.bigint(N, a.n_len);
   // N + 1, streamed limb by limb from the top: compute the carry chain first
   {
@@ -636,6 +640,8 @@ hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st) {
 }
 hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
+  static const bool per_thread = getenv("FSDKR_INVERSE_PER_THREAD") != nullptr;   // A/B switch
+  if (!per_thread) return launch_inverse_coop(k32, a, st);
   const dim3 grid(blocks_for(a.count, 64)), blk(64);
   switch (k32) {
     case 64: hipLaunchKernelGGL(inverse_kernel<64>, grid, blk, 0, st, a); break;

@@ -98,6 +98,10 @@ def lib():
     L.fsdkr_paillier_encrypt.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p, u32p,
                                          u32p, ctypes.c_uint32, u32p]
     L.fsdkr_paillier_encrypt.restype = ctypes.c_int
+    L.fsdkr_ctx_set_modexp_group.argtypes = [vp, ctypes.c_uint32]
+    L.fsdkr_ctx_set_modexp_group.restype = ctypes.c_int
+    L.fsdkr_mod_inverse.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p]
+    L.fsdkr_mod_inverse.restype = ctypes.c_int
     L.fsdkr_ec_msm.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
     L.fsdkr_ec_msm.restype = ctypes.c_int
     _lib = L
@@ -184,6 +188,22 @@ class Context:
         self.check(self._lib.fsdkr_modexp_batch(self._h, mod_limbs, count, _ptr(B), _ptr(E), exp_limbs, _ptr(I),
                                                 _ptr(Mo), len(mods), _ptr(O)))
         return limbs_to_ints(O)
+
+    def set_modexp_group(self, lanes):
+        """Force the lanes per modexp instance (0 = automatic)."""
+        self.check(self._lib.fsdkr_ctx_set_modexp_group(self._h, lanes))
+
+    def mod_inverse(self, ys, ms, mod_limbs):
+        """[(y^-1 mod m or None)] on the GPU (None where gcd(y, m) != 1)."""
+        count = len(ys)
+        if count == 0:
+            return []
+        Y = ints_to_limbs(ys, mod_limbs)
+        M = ints_to_limbs(ms, mod_limbs)
+        O = np.zeros((count, mod_limbs), dtype=np.uint32)
+        U = np.zeros(count, dtype=np.uint32)
+        self.check(self._lib.fsdkr_mod_inverse(self._h, mod_limbs, count, _ptr(Y), _ptr(M), _ptr(O), _ptr(U)))
+        return [v if u else None for v, u in zip(limbs_to_ints(O), U.tolist())]
 
     # ---- collect() verification -------------------------------------------
     def verify_collect(self, batch):

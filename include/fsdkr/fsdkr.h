@@ -48,6 +48,9 @@ typedef struct fsdkr_cfg {
 int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out);
 void fsdkr_ctx_destroy(fsdkr_ctx* ctx);
 const char* fsdkr_last_error(const fsdkr_ctx* ctx);
+/* Lanes cooperating on one modexp instance (2, 4, 8, 16; unsupported values
+ * for a width fall back to the automatic choice); 0 = choose by batch size. */
+int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes);
 /* 1 if the shared library was built with gfx950 kernels and a device is present. */
 int fsdkr_device_available(void);
 
@@ -64,6 +67,13 @@ int fsdkr_device_available(void);
 int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* base,
                        const uint32_t* exp, uint32_t exp_limbs, const uint32_t* mod_idx,
                        const uint32_t* mods, uint32_t n_mod, uint32_t* out);
+
+/* out[i] = y[i]^-1 mod m[i] and unit[i] = (gcd(y[i], m[i]) == 1); y[i] < m[i],
+ * every m[i] odd, all [count][mod_limbs].  out may be NULL (unit test only).
+ * Replaces curv BigInt::mod_inv (GMP mpz_invert) at zk_pdl_with_slack.rs:180
+ * (PDL: unwrap, panics on a non-unit) and range_proofs.rs:129,142 (Alice). */
+int fsdkr_mod_inverse(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* y, const uint32_t* m,
+                      uint32_t* out, uint32_t* unit);
 
 /* Device-resident variant for benchmarking/integration: all pointers are
  * device pointers already in HBM; runs on the context stream and returns

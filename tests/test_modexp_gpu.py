@@ -55,3 +55,24 @@ def test_modexp_paillier_shape(gpu_ctx):
     exps = [Ns[i] for i in idx]
     got = gpu_ctx.modexp_batch(bases, exps, mods, idx, 128)
     assert got == [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
+
+
+@pytest.mark.parametrize("limbs,group", [(64, 2), (64, 4), (64, 8), (128, 4), (128, 8), (128, 16), (192, 4), (192, 8)])
+def test_modexp_every_group_size(gpu_ctx, limbs, group):
+    """Each lanes-per-instance variant (mont29.hpp DPP paths for G = 2..16) is exact,
+    including the all-ones modulus and exponent-length spread in one launch."""
+    rnd = random.Random(1000 * limbs + group)
+    bits = 32 * limbs
+    mods = [_odd(rnd, bits) for _ in range(3)] + [(1 << bits) - 1, _odd(rnd, bits - 61)]
+    count = 200
+    idx = [rnd.randrange(len(mods)) for _ in range(count)]
+    bases = [rnd.getrandbits(bits) for _ in range(count)]
+    exps = [rnd.getrandbits(rnd.choice([1, 30, 256, 1000, 2048])) for _ in range(count)]
+    gpu_ctx.set_modexp_group(group)
+    try:
+        got = gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs)
+    finally:
+        gpu_ctx.set_modexp_group(0)
+    want = [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
+    bad = [k for k in range(count) if got[k] != want[k]]
+    assert not bad, f"G={group}: {len(bad)} mismatches, first at {bad[0]}"
