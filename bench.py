@@ -147,6 +147,20 @@ def modexp_roofline(ctx, count, reps, seed=1234):
             "achieved_mac_per_s": W / (ms * 1e-3)}
 
 
+def pmc_traffic(count):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    --pmc passes (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 per the
+    gfx950 correction + WRITE_SIZE, one pass each), scaled to `count`
+    instances.  PMC cannot be collected inside the timed run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_modexp4096.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    inst = d.get("instances", 65536)
+    return d["hbm_traffic_bytes"] * count / inst, os.path.relpath(files[-1], REPO)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +244,7 @@ def main():
     roof = modexp_roofline(ctx, a.modexp_count, 3)
     cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(msgs, joins, lk, a.key_bits, a.cpu_pairs)
     W_collect = collect_work(R, J, n)
+    traffic, traffic_src = pmc_traffic(roof["count"])
     out = {
         "metric": METRIC, "value": value, "unit": "proofs/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
@@ -240,7 +255,9 @@ def main():
                    "proofs_per_step": proofs, "parallelism": f"refresh messages sharded over {world} GPU(s)"},
         "modexp_4096_per_s": roof["modexp_per_s"],
         "roofline": {"bound": "valu-int", "achieved": roof["achieved_mac_per_s"] / 1e12, "peak": PEAK_MAC / 1e12,
-                     "unit": "T u32-MAC/s", "frac": roof["achieved_mac_per_s"] / PEAK_MAC, "traffic": None,
+                     "unit": "T u32-MAC/s", "frac": roof["achieved_mac_per_s"] / PEAK_MAC, "traffic": traffic,
+                     "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
+                     "algorithmic_bytes": roof["count"] * (512 + 256 + 512),
                      "kernel": "modexp_kernel<144,4,128> (4096-bit modulus N^2, 2048-bit exponent N)",
                      "per_launch": f"{roof['count']} instances x {w_modexp(128, 2048) / 1e6:.2f} M MACs in "
                                    f"{roof['kernel_ms']:.2f} ms (HIP events)"},

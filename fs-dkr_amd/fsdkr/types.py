@@ -124,3 +124,11 @@ class LocalKey:
     i: int
     t: int
     n: int
+
+
+@dataclass
+class Keys:
+    """The Paillier pair of multi-party-ecdsa gg_2020 party_i::Keys that
+    JoinMessage::collect consumes (add_party_message.rs:139, :189-193)."""
+    ek: EncryptionKey
+    dk: DecryptionKey

@@ -80,7 +80,13 @@ if __name__ == "__main__":
     ap.add_argument("--count", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--widths", default="128,64")
+    ap.add_argument("--groups", default="0", help="lanes per instance to force (0 = automatic), comma list")
     a = ap.parse_args()
     ctx = Context(timing=True)
     for k in [int(x) for x in a.widths.split(",")]:
-        print(json.dumps(run(ctx, k, a.count, 16, a.reps, 1234 + k)), flush=True)
+        for g in [int(x) for x in a.groups.split(",")]:
+            ctx.set_modexp_group(g)
+            r = run(ctx, k, a.count, 16, a.reps, 1234 + k)
+            r["group"] = g
+            print(json.dumps(r), flush=True)
+    ctx.set_modexp_group(0)
