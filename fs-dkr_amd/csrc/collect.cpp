@@ -778,9 +778,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     v->range[p] = (rng[p] && u_cA[p] && u_zA[p]) ? 1 : 0;
   }
   for (uint32_t m = 0; m < Mt; ++m) {
-    bool ok = true;
-    for (uint32_t k = 0; k < M; ++k) ok = ok && eq_nl_res[P + (size_t)m * M + k];
-    v->ped[m] = (uint8_t)((ppanic[m] ? 2 : 0) | (ok && !ppanic[m] ? 1 : 0));
+    v->ped[m] = ped_verdict(&eq_nl_res[P + (size_t)m * M], M, ppanic[m]);
     bool ck = ck_pre[m];
     for (uint32_t k = 0; k < CK_M2; ++k) ck = ck && eq_nl_res[P + (size_t)Mt * M + (size_t)m * CK_M2 + k];
     v->ck[m] = ck ? 1 : 0;

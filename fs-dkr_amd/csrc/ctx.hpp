@@ -90,6 +90,17 @@ struct ModexpJob {
 };
 
 uint32_t choose_window(uint32_t ebits);
+
+// RingPedersenProof::verify outcome from the per-index equalities and the
+// challenge-length word of ped_hash (ring_pedersen_proof.rs:136-153): checks run
+// in index order, so a failing check before the BitVec index panic is an error,
+// not a panic.  bit0 = ok, bit1 = the reference panics.
+inline uint8_t ped_verdict(const uint32_t* eq, uint32_t M, uint32_t panic_word) {
+  const uint32_t readable = panic_word ? panic_word - 1 : M;
+  for (uint32_t k = 0; k < readable && k < M; ++k)
+    if (!eq[k]) return 0;
+  return panic_word ? 2 : 1;
+}
 void free_collect_plan(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag);
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,

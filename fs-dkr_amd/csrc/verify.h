@@ -28,7 +28,7 @@ struct PedHashArgs {        // ring-Pedersen challenge bits
   const uint32_t* A;        // [count][M][a_len]
   uint32_t M, a_len;
   uint32_t* bits;           // [count][ceil(M/32)]
-  uint32_t* panic;          // [count]
+  uint32_t* panic;          // [count] 0, or 1 + bits readable before the reference's index panic
   uint32_t count;
 };
 

@@ -95,7 +95,8 @@ __global__ void pdl_hash_kernel(const PdlHashArgs a) {
 }
 
 // e = H(A_0 .. A_{M-1}); bits[m][i/32] bit i%32 = Lsb0 bit i of e.to_bytes();
-// panic[m] = 1 if e.to_bytes() is shorter than M bits (BitVec index panic).
+// panic[m] != 0 if e.to_bytes() is shorter than M bits (BitVec index panic at bit
+// panic[m]-1; checks before that index still run and may fail first).
 __global__ void ped_hash_kernel(const PedHashArgs a) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= a.count) return;
@@ -120,7 +121,8 @@ __global__ void ped_hash_kernel(const PedHashArgs a) {
   if (nb == 0) be[nb++] = 0;
   uint32_t* bits = a.bits + (size_t)m * ((a.M + 31) / 32);
   for (uint32_t w = 0; w < (a.M + 31) / 32; ++w) bits[w] = 0;
-  a.panic[m] = (8u * (uint32_t)nb < a.M) ? 1u : 0u;
+  // short challenge: 1 + the number of bits the reference reads before its index panic
+  a.panic[m] = (8u * (uint32_t)nb < a.M) ? 1u + 8u * (uint32_t)nb : 0u;
   for (uint32_t i = 0; i < a.M && (i >> 3) < (uint32_t)nb; ++i)
     if ((be[i >> 3] >> (i & 7)) & 1u) bits[i >> 5] |= 1u << (i & 31);
 }

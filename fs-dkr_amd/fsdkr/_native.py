@@ -104,6 +104,11 @@ def lib():
     L.fsdkr_mod_inverse.restype = ctypes.c_int
     L.fsdkr_ec_msm.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
     L.fsdkr_ec_msm.restype = ctypes.c_int
+    L.fsdkr_feldman_check.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u8p]
+    L.fsdkr_feldman_check.restype = ctypes.c_int
+    L.fsdkr_ring_pedersen_verify.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                             u32p, u32p, u32p, u32p, u32p, u8p]
+    L.fsdkr_ring_pedersen_verify.restype = ctypes.c_int
     _lib = L
     return L
 
@@ -244,6 +249,32 @@ class Context:
         self.check(self._lib.fsdkr_paillier_encrypt(self._h, nl, len(ms), _ptr(Mm), ml, _ptr(Rr), _ptr(I), _ptr(Nn),
                                                     len(ns), _ptr(O)))
         return limbs_to_ints(O)
+
+    def feldman_check(self, vss, commit, n, t):
+        """vss: [n_msgs][t+1] points, commit: [n_msgs*n] points -> uint8 verdicts [n_msgs*n]."""
+        from .batch import pack_points
+        V = pack_points([p for row in vss for p in row])
+        Cm = pack_points(commit)
+        out = np.zeros(len(commit), dtype=np.uint8)
+        self.check(self._lib.fsdkr_feldman_check(self._h, len(vss), n, t, _ptr(V), _ptr(Cm),
+                                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
+
+    def ring_pedersen_verify(self, statements, proofs, m_security, nl):
+        """[(statement, proof)] -> uint8 verdicts (bit0 ok, bit1 the reference panics)."""
+        from .batch import pack
+        M = m_security
+        zl = max(1, (max(z.bit_length() for p in proofs for z in p.Z[:M]) + 31) // 32)
+        S = pack([s.S for s in statements], nl)
+        T = pack([s.T for s in statements], nl)
+        N = pack([s.N for s in statements], nl)
+        A = pack([a for p in proofs for a in p.A[:M]], nl)
+        Z = pack([z for p in proofs for z in p.Z[:M]], zl)
+        out = np.zeros(len(proofs), dtype=np.uint8)
+        self.check(self._lib.fsdkr_ring_pedersen_verify(self._h, nl, len(proofs), M, zl, _ptr(S), _ptr(T), _ptr(N),
+                                                        _ptr(A), _ptr(Z),
+                                                        out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
 
     def ec_msm(self, points, scalars):
         """points/scalars: lists (count) of equal-length lists; points are (x, y) or None."""

@@ -18,7 +18,7 @@ LIB = os.path.join(PKG, "libfsdkr.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["modexp.hip", "verify.hip", "inverse.hip", "capi.cpp", "collect.cpp", "recover.cpp"]
+SOURCES = ["modexp.hip", "verify.hip", "inverse.hip", "capi.cpp", "collect.cpp", "recover.cpp", "standalone.cpp"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
           "-Wno-unused-result"]
 

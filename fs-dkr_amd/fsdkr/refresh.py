@@ -98,17 +98,29 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
         raise err
     # ---- share recovery (:367-373, :439-464)
     t = local_key.vss_scheme.threshold
-    indices = [msgs[j].old_party_index - 1 for j in range(t + 1)]
-    li = [_lagrange(indices[j], indices) for j in range(t + 1)]
-    nl = batch.nl
-    cts = [msgs[j].points_encrypted_vec[local_key.i - 1] for j in range(t + 1)]
-    dk = local_key.paillier_dk
-    sig = ctx.paillier_decrypt(cts, dk.p, dk.q, nl)
-    # Dec(prod c_j^l_j * Enc(0)) = sum l_j Dec(c_j) mod N  (the Enc(0) factor only re-randomises)
-    new_share = sum(l * s for l, s in zip(li, sig)) % (dk.p * dk.q) % Q
+    n_new = len(msgs) + len(joins)
+    new_share, y, pk = recover_share(ctx, msgs, local_key.i, t, local_key.paillier_dk, batch.nl, n_new)
     local_key.paillier_dk = new_dk
     local_key.x_i = new_share
-    n_new = len(msgs) + len(joins)
+    local_key.y = y
+    for i in range(n_new):
+        local_key.pk_vec.insert(i, pk[i])
+
+
+def recover_share(ctx, msgs, party_index, t, dk, nl, n_new):
+    """get_ciphertext_sum + Paillier::decrypt + the pk_vec loop
+    (refresh_message.rs:193-237, :439-464; add_party_message.rs:186-213):
+    (new share, G * share, [pk_vec entry for each of the n_new parties]).
+
+    Lagrange weights use the first t+1 messages in slice order.  The GPU
+    decrypts each c_j and combines sum_j l_j * Dec(c_j) mod N: decryption is a
+    homomorphism on units of Z_{N^2}, so this equals the reference's decryption
+    of prod_j c_j^l_j * Enc(0) (the Enc(0) factor only re-randomises)."""
+    indices = [msgs[j].old_party_index - 1 for j in range(t + 1)]
+    li = [_lagrange(indices[j], indices) for j in range(t + 1)]
+    cts = [msgs[j].points_encrypted_vec[party_index - 1] for j in range(t + 1)]
+    sig = ctx.paillier_decrypt(cts, dk.p, dk.q, nl)
+    new_share = sum(l * s for l, s in zip(li, sig)) % (dk.p * dk.q) % Q
     pts = [[(GX, GY)]] + [[msgs[j].points_committed_vec[i] for j in range(t + 1)] for i in range(n_new)]
     scs = [[new_share]] + [li[:] for _ in range(n_new)]
     # one MSM launch: y = G*x, then pk_vec[i] = sum_j P_j,i * l_j  (rows padded to t+1 terms)
@@ -116,6 +128,4 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     pts = [row + [None] * (width - len(row)) for row in pts]
     scs = [row + [0] * (width - len(row)) for row in scs]
     res = ctx.ec_msm(pts, scs)
-    local_key.y = res[0]
-    for i in range(n_new):
-        local_key.pk_vec.insert(i, res[1 + i])
+    return new_share, res[0], res[1:]

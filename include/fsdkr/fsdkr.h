@@ -181,6 +181,23 @@ typedef struct fsdkr_error {
  * NULL when the threshold or size check already fails.  Pure host logic. */
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out);
 
+/* ---- Stand-alone checks (JoinMessage::collect, per-proof callers) ---------
+ * Feldman share checks of validate_collect (refresh_message.rs:177-188, curv
+ * VerifiableSS::validate_share_public): verdict[k*n + i] = 1 iff
+ * commit[k*n + i] == sum_j vss[k][j] * (i+1)^j.  vss: [n_msgs][t+1][16],
+ * commit: [n_msgs*n][16] affine points ((0,0) = infinity). */
+int fsdkr_feldman_check(fsdkr_ctx* ctx, uint32_t n_msgs, uint32_t n, uint32_t t, const uint32_t* vss,
+                        const uint32_t* commit, uint8_t* verdict);
+/* RingPedersenProof::verify (ring_pedersen_proof.rs:126-157) for `count`
+ * independent proofs: S, T, N: [count][nl]; A: [count][M][nl]; Z: [count][M][zl].
+ * verdict[m] bit0 = Ok(()), bit1 = the reference panics (challenge shorter
+ * than M bits and every check before the panicking index passes); 0 =
+ * Err(RingPedersenProofError).  Called by JoinMessage::collect
+ * (add_party_message.rs:146-167). */
+int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint32_t m_security, uint32_t zl,
+                               const uint32_t* S, const uint32_t* T, const uint32_t* N, const uint32_t* A,
+                               const uint32_t* Z, uint8_t* verdict);
+
 /* ---- Job 1: Paillier encryption of the shares (refresh_message.rs:72-84) ----
  * out[k] = (1 + m[k] N) * r[k]^N mod N^2, N = ns[n_idx[k]]  (kzen-paillier
  * encrypt_with_chosen_randomness).  m: [count][ml], r: [count][nl] (< N),

@@ -94,3 +94,40 @@ def load_raw(name):
 
 def load(name, classes):
     return dec(load_raw(name), classes)
+
+
+# ------------------------------------------------------------- tamper ops ----
+# A tamper vector is a list of ops applied to {"msgs": [...], "joins": [...], "self": ...}:
+# {"path": [...], "set": encoded value} or {"path": [...], "truncate": len}.
+def _get(root, path):
+    x = root
+    for p in path:
+        x = x[p] if isinstance(p, int) else (x[p] if isinstance(x, dict) else getattr(x, p))
+    return x
+
+
+def _set(x, path, value):
+    """Functional update along `path` (frozen dataclasses are rebuilt)."""
+    if not path:
+        return value
+    p, rest = path[0], path[1:]
+    if isinstance(p, int):
+        cur = list(x)
+        cur[p] = _set(cur[p], rest, value)
+        return tuple(cur) if isinstance(x, tuple) else cur
+    if isinstance(x, dict):
+        y = dict(x)
+        y[p] = _set(x[p], rest, value)
+        return y
+    return dataclasses.replace(x, **{p: _set(getattr(x, p), rest, value)})
+
+
+def apply_ops(state, ops, decode=lambda v: v):
+    """state: {"msgs": [...], "joins": [...]}; ops: [{"path", "set"} | {"path", "truncate"}]."""
+    for op in ops:
+        path = op["path"]
+        if "truncate" in op:
+            state = _set(state, path, list(_get(state, path))[:op["truncate"]])
+        else:
+            state = _set(state, path, decode(op["set"]))
+    return state
