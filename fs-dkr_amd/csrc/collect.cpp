@@ -95,7 +95,7 @@ struct CollectPlan {
   uint32_t s1l = 0, n_mods_nl = 0;
   // output offsets
   size_t x_epdl, x_pbits, x_ppanic, x_Bpdl, x_gs1, x_J[10], x_invc, x_invz, x_unn, x_uzA, x_uzp, x_eq2, x_eq3, x_u,
-      x_w, x_fel, x_pdlv, x_rng, x_scr128, x_scr64;
+      x_w, x_fel, x_pdlv, x_rng;
   // descriptor offsets + counts
   size_t d_J[10], d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_p3nn, d_p3nl, d_p3m,
       d_ahn, d_ahc, d_alpre;
@@ -332,8 +332,6 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   const size_t x_eq3 = L.out(n_eqnl * 4);           // [u3 P | RP Mt*M | CK Mt*11 | DLog 2J]
   const size_t x_u = L.out((size_t)P * nn * 4), x_w = L.out((size_t)P * nl * 4);
   const size_t x_fel = L.out(P), x_pdlv = L.out(P), x_rng = L.out(P);
-  const size_t x_scr128 = L.out((size_t)6 * (nn + 2) * 2 * P * 4);
-  const size_t x_scr64 = L.out((size_t)6 * (nl + 2) * 2 * P * 4);
 
   // single device allocation: [inputs | descriptors | outputs]; descriptors are
   // appended to the input image below once the device base address is known.
@@ -576,7 +574,7 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   }
   pl.x_invc = x_invc; pl.x_invz = x_invz; pl.x_unn = x_unn; pl.x_uzA = x_uzA; pl.x_uzp = x_uzp;
   pl.x_eq2 = x_eq2; pl.x_eq3 = x_eq3; pl.x_u = x_u; pl.x_w = x_w; pl.x_fel = x_fel; pl.x_pdlv = x_pdlv;
-  pl.x_rng = x_rng; pl.x_scr128 = x_scr128; pl.x_scr64 = x_scr64;
+  pl.x_rng = x_rng;
   pl.d_bs = d_bs; pl.d_bn = d_bn; pl.d_iynn = d_iynn; pl.d_imnn = d_imnn; pl.d_iynl = d_iynl; pl.d_imnl = d_imnl;
   pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_p3nn = d_p3nn;
   pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc; pl.d_alpre = d_alpre;
@@ -610,7 +608,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   const size_t x_epdl = pl.x_epdl, x_pbits = pl.x_pbits, x_ppanic = pl.x_ppanic, x_Bpdl = pl.x_Bpdl, x_gs1 = pl.x_gs1;
   const size_t x_invc = pl.x_invc, x_invz = pl.x_invz, x_unn = pl.x_unn, x_uzA = pl.x_uzA, x_uzp = pl.x_uzp;
   const size_t x_eq2 = pl.x_eq2, x_eq3 = pl.x_eq3, x_u = pl.x_u, x_w = pl.x_w, x_fel = pl.x_fel, x_pdlv = pl.x_pdlv;
-  const size_t x_rng = pl.x_rng, x_scr128 = pl.x_scr128, x_scr64 = pl.x_scr64;
+  const size_t x_rng = pl.x_rng;
   const size_t d_bs = pl.d_bs, d_bn = pl.d_bn, d_iynn = pl.d_iynn, d_imnn = pl.d_imnn, d_iynl = pl.d_iynl;
   const size_t d_imnl = pl.d_imnl, d_eqnn = pl.d_eqnn, d_eqnnm = pl.d_eqnnm, d_eqnl = pl.d_eqnl, d_eqnlm = pl.d_eqnlm;
   const size_t d_p3nn = pl.d_p3nn, d_p3nl = pl.d_p3nl, d_p3m = pl.d_p3m, d_ahn = pl.d_ahn, d_ahc = pl.d_ahc;
@@ -667,7 +665,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     if ((rc = launch_group(k, ss))) return rc;
     if (k == 2) {  // nn inverses right behind the challenges' modexps
       InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
-                    PX(x_scr128), pl.n_inv_nn};
+                    nullptr, pl.n_inv_nn};
       c->mark("inverse", true, ss);
       rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
       c->mark("inverse", false, ss);
@@ -688,13 +686,13 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   if ((rc = launch_group(3, st))) return rc;
   {
     InverseArgs b1{(const uint64_t*)(dev + d_iynl), (const uint64_t*)(dev + d_imnl), PX(x_invz), PX(x_uzA),
-                   PX(x_scr64), P};
+                   nullptr, P};
     c->mark("inverse", true);
     rc = c->hip_check(launch_inverse(nl, b1, st), "inverse nl");
     c->mark("inverse", false);
     if (rc) return rc;
     InverseArgs b2{(const uint64_t*)(dev + d_iynl) + P, (const uint64_t*)(dev + d_imnl) + P, nullptr, PX(x_uzp),
-                   PX(x_scr64), P};
+                   nullptr, P};
     if ((rc = c->hip_check(launch_inverse(nl, b2, st), "inverse nl 2"))) return rc;
   }
   {

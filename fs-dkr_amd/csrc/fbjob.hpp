@@ -1,0 +1,116 @@
+// Host side of a fixed-base exponentiation job (fixedbase.hip): bases shared by
+// many exponents, each instance writing base^exp mod N to its own address.
+// Used by the collect() pipeline (h1_i, h2_i, ring-Pedersen T) and by the
+// stand-alone ring-Pedersen / fixed-base entry points.
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ctx.hpp"
+#include "fixedbase.h"
+
+namespace fsdkr {
+
+struct FbJob {
+  uint32_t k32 = 0;
+  // bases
+  std::vector<uint64_t> b_ptr;
+  std::vector<uint32_t> b_len, b_mod, b_bits;
+  // instances
+  std::vector<uint64_t> e_ptr, o_ptr;
+  std::vector<uint32_t> e_len, e_base, e_mod;
+  // finalize() results
+  uint32_t w = 1, stride = 0;
+  size_t entries = 0;
+  std::vector<uint32_t> b_h, b_toff, i_h, i_toff;
+
+  uint32_t add_base(uint64_t ptr, uint32_t len, uint32_t mod) {
+    b_ptr.push_back(ptr);
+    b_len.push_back(len);
+    b_mod.push_back(mod);
+    b_bits.push_back(1);
+    return (uint32_t)b_ptr.size() - 1;
+  }
+  // ebits: bound on the exponent's bit length (sizes the base's table)
+  void add(uint32_t base, uint64_t exp, uint32_t elen, uint32_t ebits, uint64_t out) {
+    e_ptr.push_back(exp);
+    e_len.push_back(elen);
+    e_base.push_back(base);
+    e_mod.push_back(b_mod[base]);
+    o_ptr.push_back(out);
+    b_bits[base] = std::max(b_bits[base], std::max(ebits, 1u));
+  }
+  size_t count() const { return e_ptr.size(); }
+  size_t bases() const { return b_ptr.size(); }
+
+  void finalize() {
+    uint32_t maxb = 1;
+    for (uint32_t b : b_bits) maxb = std::max(maxb, b);
+    w = fb_window(maxb);
+    b_h.resize(bases());
+    b_toff.resize(bases());
+    entries = 0;
+    uint32_t hmax = 1;
+    for (size_t b = 0; b < bases(); ++b) {
+      b_h[b] = std::max(1u, (b_bits[b] + w - 1) / w);
+      b_toff[b] = (uint32_t)entries;
+      entries += b_h[b];
+      hmax = std::max(hmax, b_h[b]);
+    }
+    stride = (hmax + (1u << w) + 1) & ~1u;
+    i_h.resize(count());
+    i_toff.resize(count());
+    for (size_t i = 0; i < count(); ++i) {
+      i_h[i] = b_h[e_base[i]];
+      i_toff[i] = b_toff[e_base[i]];
+    }
+  }
+
+  // device image: descriptor arrays (inputs) appended to `img` at 256-byte
+  // alignment; offsets recorded for bind()
+  struct Offsets {
+    size_t b_ptr, b_len, b_mod, b_toff, b_h, e_ptr, e_len, i_h, i_toff, e_mod, o_ptr;
+  } off{};
+  void pack(std::vector<uint8_t>& img) {
+    auto put = [&](const void* src, size_t bytes) {
+      const size_t o = (img.size() + 255) & ~(size_t)255;
+      img.resize(o + ((bytes + 255) & ~(size_t)255) + 256, 0);
+      if (bytes) memcpy(img.data() + o, src, bytes);
+      return o;
+    };
+    off.b_ptr = put(b_ptr.data(), b_ptr.size() * 8);
+    off.b_len = put(b_len.data(), b_len.size() * 4);
+    off.b_mod = put(b_mod.data(), b_mod.size() * 4);
+    off.b_toff = put(b_toff.data(), b_toff.size() * 4);
+    off.b_h = put(b_h.data(), b_h.size() * 4);
+    off.e_ptr = put(e_ptr.data(), e_ptr.size() * 8);
+    off.e_len = put(e_len.data(), e_len.size() * 4);
+    off.i_h = put(i_h.data(), i_h.size() * 4);
+    off.i_toff = put(i_toff.data(), i_toff.size() * 4);
+    off.e_mod = put(e_mod.data(), e_mod.size() * 4);
+    off.o_ptr = put(o_ptr.data(), o_ptr.size() * 8);
+  }
+  // scratch the kernels write: table, schedules, step counts
+  size_t table_bytes(int KD) const { return entries * (size_t)KD * 4; }
+  size_t sched_bytes() const { return count() * (size_t)stride * 2; }
+  size_t nsteps_bytes() const { return count() * 4; }
+};
+
+// Device addresses of one packed FbJob.
+struct FbDev {
+  const uint8_t* img = nullptr;   // base of the packed descriptor image
+  uint32_t* table = nullptr;
+  uint16_t* sched = nullptr;
+  uint32_t* nsteps = nullptr;
+};
+
+// table, schedule and exponent kernels; `st_table` may differ from `st` (the
+// schedule kernel runs beside the table chain), the exponent kernel waits for both.
+int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag);
+// upload + launch + wait (stand-alone callers)
+int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag);
+
+}  // namespace fsdkr

@@ -1,0 +1,229 @@
+// Fixed-base exponentiation on gfx950 for the bases collect() shares across
+// many exponents (Brickell-Gordon-McCurley-Wilson windowing):
+//   h1_i, h2_i   receiver i's DLogStatement bases, shared by the 2n PDL/Alice
+//                proofs addressed to i   (zk_pdl_with_slack.rs:144-157 via
+//                commitment_unknown_order :170-188; range_proofs.rs:129-137)
+//   T            one ring-Pedersen statement, shared by its M = 256 checks
+//                T^Z_i mod N             (ring_pedersen_proof.rs:144)
+// Results are bit-identical to base^exp mod N; only the order of the
+// Montgomery products changes.
+//
+// Per base b, fb_table_kernel stores P_j = b^(2^(w j)) (Montgomery form) for
+// j < h: a chain of w*h squarings, run once per base.  For an exponent with
+// w-bit digits e_j, b^e = prod_{d=2^w-1..1} B_d with B_d = prod_{e_j >= d} P_j;
+// fb_exp_kernel keeps B in registers and A in LDS and executes the
+// instance's schedule (fb_sched_kernel): "B <- B*P_j" for every j with e_j = d,
+// then "A <- A*B", for d from the largest digit down to 1.  That is
+// nnz(e) + max(e_j) <= h + 2^w - 1 products per exponent instead of the
+// ~bits*(1 + 1/w) of a variable-base window ladder (2048-bit exponent, w = 6:
+// 405 vs 2458).
+#include "fixedbase.h"
+#include "mont29.hpp"
+
+namespace fsdkr {
+
+constexpr uint16_t FB_A_STEP = 0xFFFF;   // A <- A * B
+constexpr uint16_t FB_NOP = 0xFFFE;      // idle lanes of a wave still multiply (lockstep); result dropped
+
+// P_j = base^(2^(w j)) in Montgomery form, table[toff[b] + j][KD] in digit order.
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = 3 * KD + 4;
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t b = blockIdx.x * IPB + li;
+  if (b >= a.count) return;
+  uint32_t* stream = lds + li * KD;
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[b] * STRIDE;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
+  M.ninv = C[3 * KD];
+  uint32_t acc[L];
+  const uint32_t* B = reinterpret_cast<const uint32_t*>(a.base_ptr[b]);
+  const int blen = (int)min(a.base_len[b], (uint32_t)K32);
+#pragma unroll
+  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);
+  uint32_t* T = a.table + (size_t)a.toff[b] * KD;
+  const uint32_t h = a.h[b];
+  // step 0: acc * R^2 -> Montgomery form of the base; then w squarings per entry
+  const uint32_t n_steps = 1 + (h > 0 ? (h - 1) * a.w : 0);
+  uint32_t entry = 0;
+  for (uint32_t st = 0; st < n_steps; ++st) {
+    __builtin_amdgcn_wave_barrier();
+    if (st == 0) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) stream[g * L + j] = C[2 * KD + g * L + j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < L; ++j) stream[g * L + j] = acc[j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    M.mul(acc, acc, stream);
+    if (st == 0 || (st % a.w) == 0) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) T[(size_t)entry * KD + g * L + j] = acc[j];
+      ++entry;
+    }
+  }
+}
+
+// One thread per instance: the BGMW product schedule of its exponent.
+__global__ void fb_sched_kernel(const FbSchedArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.count) return;
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[i]);
+  const uint32_t elen = a.exp_len[i];
+  const uint32_t h = a.h[i], w = a.w, mask = (1u << w) - 1;
+  auto digit = [&](uint32_t j) -> uint32_t {
+    const uint32_t p = j * w, lo = p >> 5, sh = p & 31;
+    const uint32_t v0 = (lo < elen) ? E[lo] : 0u;
+    const uint32_t v1 = (lo + 1 < elen) ? E[lo + 1] : 0u;
+    return (uint32_t)((((uint64_t)v1 << 32) | v0) >> sh) & mask;
+  };
+  uint32_t dmax = 0;
+  for (uint32_t j = 0; j < h; ++j) dmax = max(dmax, digit(j));
+  uint16_t* S = a.sched + (size_t)i * a.stride;
+  uint32_t n = 0;
+  for (uint32_t d = dmax; d >= 1; --d) {
+    for (uint32_t j = 0; j < h; ++j)
+      if (digit(j) == d) S[n++] = (uint16_t)j;
+    S[n++] = FB_A_STEP;
+  }
+  a.nsteps[i] = n;
+}
+
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK) void fb_exp_kernel(const FbExpArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = 3 * KD + 4;
+  __shared__ uint32_t lds[2 * IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * IPB + li;
+  if (inst >= a.count) return;
+  uint32_t* stream = lds + li * KD;             // streamed operand of each product
+  uint32_t* abuf = lds + (IPB + li) * KD;       // accumulator A
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
+  M.ninv = C[3 * KD];
+  const uint32_t* T = a.table + (size_t)a.toff[inst] * KD;
+  const uint16_t* S = a.sched + (size_t)inst * a.stride;
+  const uint32_t nst = a.nsteps[inst];
+  uint32_t Bd[L], r[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    Bd[j] = C[KD + g * L + j];                   // B = A = 1 (R mod N)
+    abuf[g * L + j] = Bd[j];
+  }
+  for (uint32_t st = 0;; ++st) {
+    // the wave runs until its longest schedule ends (all lanes stay in lockstep: DPP)
+    if (__builtin_amdgcn_ballot_w64(st < nst) == 0) break;
+    const uint32_t code = (st < nst) ? S[st] : FB_NOP;
+    const bool bstep = code < 0xFFFEu;
+    __builtin_amdgcn_wave_barrier();
+    if (bstep) {
+      const uint32_t* P = T + (size_t)code * KD;
+#pragma unroll
+      for (int j = 0; j < L; ++j) stream[j * G + g] = P[j * G + g];      // coalesced over the group
+    }
+    __builtin_amdgcn_wave_barrier();
+    // B-step: B * P_j (P_j staged in LDS); A-step / idle: A * B with A read in place
+    M.mul(r, Bd, bstep ? stream : abuf);
+    if (bstep) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) Bd[j] = r[j];
+    } else if (code == FB_A_STEP) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) abuf[g * L + j] = r[j];
+    }
+  }
+  // leave Montgomery form: A * 1 / R, then exact reduction
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    r[j] = abuf[g * L + j];
+    stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
+  }
+  __builtin_amdgcn_wave_barrier();
+  M.mul(r, r, stream);
+  M.carry_exact(r);
+  M.sub_if_ge(r);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < L; ++j) stream[g * L + j] = r[j];
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* O = reinterpret_cast<uint32_t*>(a.out_ptr[inst]);
+  constexpr int LO = K32 / G;
+#pragma unroll
+  for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
+}
+
+// ---- launchers ------------------------------------------------------------------
+template <int KD, int G, int K32>
+static hipError_t table_launch(const FbTableArgs& a, hipStream_t st) {
+  constexpr int IPB = BLOCK / G;
+  hipLaunchKernelGGL((fb_table_kernel<KD, G, K32>), dim3((a.count + IPB - 1) / IPB), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+template <int KD, int G, int K32>
+static hipError_t exp_launch(const FbExpArgs& a, hipStream_t st) {
+  constexpr int IPB = BLOCK / G;
+  hipLaunchKernelGGL((fb_exp_kernel<KD, G, K32>), dim3((a.count + IPB - 1) / IPB), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fb_table(uint32_t k32, const FbTableArgs& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  // few bases, long chains: the most lanes per instance the width allows
+  switch (k32) {
+    case 64: return table_launch<72, 8, 64>(a, st);
+    case 96: return table_launch<108, 4, 96>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_fb_sched(const FbSchedArgs& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  hipLaunchKernelGGL(fb_sched_kernel, dim3((a.count + 63) / 64), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fb_exp(uint32_t k32, const FbExpArgs& a, int group, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  switch (k32) {
+    case 64:
+      switch (group) {
+        case 8: return exp_launch<72, 8, 64>(a, st);
+        case 2: return exp_launch<72, 2, 64>(a, st);
+        default: return exp_launch<72, 4, 64>(a, st);
+      }
+    case 96: return exp_launch<108, 4, 96>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+uint32_t fb_window(uint32_t ebits) {
+  // products per exponent ~ ceil(bits/w) + 2^w - 1 (the table chain is per base)
+  uint32_t best = 1, cost = 0xFFFFFFFFu;
+  for (uint32_t w = 1; w <= 8; ++w) {
+    const uint32_t c = (ebits + w - 1) / w + (1u << w) - 1;
+    if (c < cost) {
+      cost = c;
+      best = w;
+    }
+  }
+  return best;
+}
+
+}  // namespace fsdkr

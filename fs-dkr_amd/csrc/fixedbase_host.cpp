@@ -1,0 +1,138 @@
+// Launch sequencing of fixed-base jobs (fbjob.hpp) and the stand-alone C ABI
+// entry fsdkr_fixed_base_modexp.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "fbjob.hpp"
+#include "fsdkr/fsdkr.h"
+#include "kernels.h"
+
+namespace fsdkr {
+
+static int fb_group(Ctx* c, size_t count) {
+  if (c->modexp_group == 2 || c->modexp_group == 4 || c->modexp_group == 8) return (int)c->modexp_group;
+  constexpr size_t kLaneCapacity = 256ull * 4 * 2 * 64;   // CUs x SIMDs x resident waves x lanes
+  if (count * 8 <= kLaneCapacity) return 8;
+  if (count * 4 <= kLaneCapacity) return 4;
+  return 2;
+}
+
+int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag) {
+  if (j.count() == 0) return FSDKR_OK;
+  const uint8_t* I = d.img;
+  auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
+  auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(I + o); };
+  FbTableArgs ta{U64(j.off.b_ptr), U32(j.off.b_len), U32(j.off.b_mod), U32(j.off.b_toff), U32(j.off.b_h),
+                 consts, d.table, j.w, (uint32_t)j.bases()};
+  FbSchedArgs sa{U64(j.off.e_ptr), U32(j.off.e_len), U32(j.off.i_h), d.sched, d.nsteps, j.stride, j.w,
+                 (uint32_t)j.count()};
+  FbExpArgs ea{U32(j.off.i_toff), U32(j.off.e_mod), U64(j.off.o_ptr), consts, d.table, d.sched, d.nsteps, j.stride,
+               (uint32_t)j.count()};
+  int rc;
+  size_t m = c->tbeg("fb_table", st);
+  rc = c->hip_check(launch_fb_table(j.k32, ta, st), "fb_table launch");
+  c->tend(m, st);
+  if (rc) return rc;
+  if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
+  m = c->tbeg("fb_exp", st);
+  rc = c->hip_check(launch_fb_exp(j.k32, ea, fb_group(c, j.count()), st), tag);
+  c->tend(m, st);
+  return rc;
+}
+
+int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag) {
+  if (j.count() == 0) return FSDKR_OK;
+  const int KD = shape_digits(j.k32);
+  std::vector<uint8_t> img;
+  j.pack(img);
+  const size_t o_tab = (img.size() + 255) & ~(size_t)255;
+  const size_t o_sch = o_tab + ((j.table_bytes(KD) + 255) & ~(size_t)255);
+  const size_t o_ns = o_sch + ((j.sched_bytes() + 255) & ~(size_t)255);
+  const size_t total = o_ns + j.nsteps_bytes() + 256;
+  std::string name = std::string("fb_") + tag;
+  uint8_t* dev = (uint8_t*)c->buf(name.c_str(), total);
+  if (!dev) {
+    c->fail("%s: device allocation failed (%zu bytes)", tag, total);
+    return FSDKR_E_OOM;
+  }
+  int rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, c->stream), "H2D fb");
+  if (rc) return rc;
+  FbDev d{dev, (uint32_t*)(dev + o_tab), (uint16_t*)(dev + o_sch), (uint32_t*)(dev + o_ns)};
+  rc = fb_launch(c, j, d, consts, c->stream, tag);
+  if (rc) return rc;
+  // `img` is a local host buffer: the async copy must finish before it goes away
+  return c->hip_check(hipStreamSynchronize(c->stream), "sync fb");
+}
+
+}  // namespace fsdkr
+
+using namespace fsdkr;
+
+extern "C" int fsdkr_fixed_base_modexp(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t n_bases, const uint32_t* bases,
+                                       const uint32_t* base_mod_idx, const uint32_t* mods, uint32_t n_mod,
+                                       uint32_t count, const uint32_t* base_idx, const uint32_t* exp,
+                                       uint32_t exp_limbs, uint32_t* out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!bases || !base_mod_idx || !mods || !base_idx || !exp || !out || !n_bases || !n_mod || !exp_limbs) {
+    c->fail("fsdkr_fixed_base_modexp: bad argument");
+    return FSDKR_E_ARG;
+  }
+  if (mod_limbs != 64 && mod_limbs != 96) {
+    c->fail("fsdkr_fixed_base_modexp: unsupported modulus width %u limbs", mod_limbs);
+    return FSDKR_E_UNSUPPORTED;
+  }
+  for (uint32_t m = 0; m < n_mod; ++m)
+    if (!(mods[(size_t)m * mod_limbs] & 1u)) {
+      c->fail("fsdkr_fixed_base_modexp: modulus %u is even", m);
+      return FSDKR_E_ARG;
+    }
+  for (uint32_t b = 0; b < n_bases; ++b)
+    if (base_mod_idx[b] >= n_mod) {
+      c->fail("fsdkr_fixed_base_modexp: base_mod_idx[%u] out of range", b);
+      return FSDKR_E_ARG;
+    }
+  const size_t nb = (size_t)n_bases * mod_limbs * 4, nm = (size_t)n_mod * mod_limbs * 4;
+  const size_t ne = (size_t)count * exp_limbs * 4, no = (size_t)count * mod_limbs * 4;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  uint8_t* d = (uint8_t*)c->buf("fbx_io", al(nb) + al(nm) + al(ne) + al(no));
+  if (!d) {
+    c->fail("fsdkr_fixed_base_modexp: device allocation failed");
+    return FSDKR_E_OOM;
+  }
+  uint8_t *d_b = d, *d_m = d + al(nb), *d_e = d_m + al(nm), *d_o = d_e + al(ne);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_b, bases, nb, hipMemcpyHostToDevice, c->stream), "H2D bases")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_m, mods, nm, hipMemcpyHostToDevice, c->stream), "H2D mods")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_e, exp, ne, hipMemcpyHostToDevice, c->stream), "H2D exp")))
+    return rc;
+  uint32_t* consts = nullptr;
+  if ((rc = setup_moduli(c, mod_limbs, (const uint32_t*)d_m, n_mod, &consts, "fbx"))) return rc;
+  FbJob j;
+  j.k32 = mod_limbs;
+  for (uint32_t b = 0; b < n_bases; ++b)
+    j.add_base((uint64_t)(uintptr_t)(d_b + (size_t)b * mod_limbs * 4), mod_limbs, base_mod_idx[b]);
+  for (uint32_t i = 0; i < count; ++i) {
+    if (base_idx[i] >= n_bases) {
+      c->fail("fsdkr_fixed_base_modexp: base_idx[%u] out of range", i);
+      return FSDKR_E_ARG;
+    }
+    const uint32_t* e = exp + (size_t)i * exp_limbs;
+    uint32_t bits = 0;
+    for (int k = (int)exp_limbs - 1; k >= 0; --k)
+      if (e[k]) {
+        bits = 32u * (uint32_t)k + 32u - (uint32_t)__builtin_clz(e[k]);
+        break;
+      }
+    j.add(base_idx[i], (uint64_t)(uintptr_t)(d_e + (size_t)i * exp_limbs * 4), exp_limbs, bits,
+          (uint64_t)(uintptr_t)(d_o + (size_t)i * mod_limbs * 4));
+  }
+  j.finalize();
+  if ((rc = fb_run(c, j, consts, "fbx"))) return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(out, d_o, no, hipMemcpyDeviceToHost, c->stream), "D2H out"))) return rc;
+  return c->sync();
+}

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "fbjob.hpp"
 #include "fsdkr/fsdkr.h"
 #include "kernels.h"
 #include "verify.h"
@@ -104,15 +105,16 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
   one[0] = 1;
   std::vector<EqOperand> ops(I);
   std::vector<uint32_t> mod_idx(I);
-  ModexpJob job;
+  // T^Z_k mod N (ring_pedersen_proof.rs:144): T is shared by the M checks of a proof -> fixed-base job
+  FbJob job;
   job.k32 = nl;
   uint32_t zmax = 1;
   for (size_t k = 0; k < I; ++k) zmax = std::max(zmax, bit_len(Z + k * zl, zl));
+  for (uint32_t m = 0; m < count; ++m) job.add_base(DA(oT + (size_t)m * nl * 4), nl, m);
   for (uint32_t m = 0; m < count; ++m)
     for (uint32_t k = 0; k < M; ++k) {
       const size_t q = (size_t)m * M + k;
-      // T^Z_k mod N  (ring_pedersen_proof.rs:144)
-      job.add(DA(oT + (size_t)m * nl * 4), nl, DA(oZ + q * zl * 4), zl, zmax, m);
+      job.add(m, DA(oZ + q * zl * 4), zl, zmax, DA(oTZ + q * nl * 4));
       // T^Z_k == A_k * S^(e_k) mod N  (:144-148)
       EqOperand& e = ops[q];
       e.a = DA(oTZ + q * nl * 4);
@@ -150,7 +152,8 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
   rc = c->hip_check(launch_ped_hash(h, hs), "ped_hash");
   c->mark("ped_hash", false, hs);
   (void)hipEventRecord(hashed, hs);
-  if (!rc) rc = launch_modexp_job(c, job, cons, (uint32_t*)(d + oTZ), "rp");
+  job.finalize();
+  if (!rc) rc = fb_run(c, job, cons, "rp");
   (void)hipStreamWaitEvent(st, hashed, 0);
   (void)hipEventDestroy(ready);
   (void)hipEventDestroy(hashed);

@@ -1,0 +1,155 @@
+// secp256k1 kernels of the batched collect() job (gfx950, secp256k1.hpp):
+//   pdl_u1          G*s1 + Q*(q-e) == u1                       zk_pdl_with_slack.rs:124-127
+//   feldman         S_i == sum_k A_k (i+1)^k                   refresh_message.rs:177-188
+//   ec_msm          sum_j s_j P_j (pk_vec, G*x)                refresh_message.rs:446-464
+#include "secp256k1.hpp"
+#include "verify.h"
+#include <cstdlib>
+
+namespace fsdkr {
+
+__device__ __forceinline__ const uint32_t* P32(uint64_t a) { return reinterpret_cast<const uint32_t*>(a); }
+static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 1) / per; }
+
+// ------------------------------------------------------------- secp256k1 ------
+// scalar (len limbs, any size) mod q
+__device__ __forceinline__ void bigint_mod_q(uint32_t* r, const uint32_t* x, uint32_t len) {
+  // Horner over 32-bit limbs from the top: r = r*2^32 + limb (mod q)
+  // q = 2^256 - c, c = 0x14551231950b75fc4402da1732fc9bebf (129 bits)
+  const uint32_t C5[5] = {0x2FC9BEBFu, 0x402DA173u, 0x50B75FC4u, 0x45512319u, 0x1u};
+  for (int i = 0; i < 8; ++i) r[i] = 0;
+  for (int k = (int)len - 1; k >= 0; --k) {
+    // t = r * 2^32 + x[k]  (288 bits): hi = top limb of r
+    const uint32_t hi = r[7];
+    for (int i = 7; i > 0; --i) r[i] = r[i - 1];
+    r[0] = x[k];
+    // r += hi * c   (hi*c < 2^161)
+    uint64_t cc = 0;
+    for (int i = 0; i < 8; ++i) {
+      cc += (uint64_t)r[i] + (i < 5 ? (uint64_t)hi * C5[i] : 0ull);
+      r[i] = (uint32_t)cc;
+      cc >>= 32;
+    }
+    // overflow (2^256) == c mod q
+    while (cc) {
+      const uint64_t ov = cc;
+      cc = 0;
+      for (int i = 0; i < 8; ++i) {
+        cc += (uint64_t)r[i] + (i < 5 ? ov * C5[i] : 0ull);
+        r[i] = (uint32_t)cc;
+        cc >>= 32;
+      }
+    }
+    ec::scalar_reduce(r);
+  }
+  ec::scalar_reduce(r);
+}
+
+__global__ void pdl_u1_kernel(const PdlU1Args a) {
+  using namespace ec;
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.count) return;
+  uint32_t k1[8], k2[8];
+  bigint_mod_q(k1, a.s1 + (size_t)p * a.s1_len, a.s1_len);
+  // k2 = (q - (e mod q)) mod q
+  const uint32_t* e = a.e + (size_t)p * 8;
+  uint32_t em[8];
+  for (int i = 0; i < 8; ++i) em[i] = e[i];
+  scalar_reduce(em);
+  bool ez = true;
+  for (int i = 0; i < 8; ++i) ez = ez && em[i] == 0;
+  int64_t br = 0;
+  for (int i = 0; i < 8; ++i) {
+    const int64_t d = (int64_t)Q_LIMBS[i] - em[i] + br;
+    k2[i] = ez ? 0u : (uint32_t)d;
+    br = d >> 32;
+  }
+  Fe gx, gy, qx, qy, ux, uy;
+  fe_load(gx, GX_LIMBS);
+  fe_load(gy, GY_LIMBS);
+  const bool qinf = aff_load(qx, qy, a.Q + (size_t)p * 16);
+  const bool uinf = aff_load(ux, uy, a.u1 + (size_t)p * 16);
+  Jac r1, r2, r;
+  scalar_mul_aff(r1, k1, gx, gy);
+  if (qinf) {
+    jac_set_inf(r2);
+  } else {
+    scalar_mul_aff(r2, k2, qx, qy);
+  }
+  jac_add(r, r1, r2);
+  const bool eq = jac_eq_aff(r, ux, uy, uinf);
+  a.verdict[p] = (uint8_t)((a.verdict[p] & ~1u) | (eq ? 1u : 0u));
+}
+
+// S_{k,i} == Horner(A_k, i+1)
+__global__ void feldman_kernel(const FeldmanArgs a) {
+  using namespace ec;
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.count) return;
+  const uint32_t k = p / a.n, i = p % a.n;
+  const uint32_t* A = a.vss + (size_t)k * (a.t + 1) * 16;
+  const uint32_t idx = i + 1;
+  Jac acc;
+  Fe x, y;
+  if (aff_load(x, y, A + (size_t)a.t * 16)) {
+    jac_set_inf(acc);
+  } else {
+    acc.X = x;
+    acc.Y = y;
+    fe_set_u32(acc.Z, 1);
+  }
+  for (int j = (int)a.t - 1; j >= 0; --j) {
+    // acc = acc * idx
+    Jac r;
+    jac_set_inf(r);
+    for (int b = 31 - __builtin_clz(idx); b >= 0; --b) {
+      jac_dbl(r, r);
+      if ((idx >> b) & 1u) jac_add(r, r, acc);
+    }
+    acc = r;
+    if (!aff_load(x, y, A + (size_t)j * 16)) jac_add_aff(acc, acc, x, y);
+  }
+  const bool sinf = aff_load(x, y, a.S + (size_t)p * 16);
+  a.verdict[p] = jac_eq_aff(acc, x, y, sinf) ? 1u : 0u;
+}
+
+// out[o] = sum_j s[o][j] * P[o][j]   (affine out, terms affine points)
+__global__ void ec_msm_kernel(const EcMsmArgs a) {
+  using namespace ec;
+  const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= a.count) return;
+  Jac acc;
+  jac_set_inf(acc);
+  for (uint32_t j = 0; j < a.terms; ++j) {
+    const uint32_t* pt = P32(a.pt_ptr[(size_t)o * a.terms + j]);
+    const uint32_t* sc = a.scalars + ((size_t)o * a.terms + j) * 8;
+    Fe x, y;
+    if (aff_load(x, y, pt)) continue;
+    uint32_t k[8];
+    for (int i = 0; i < 8; ++i) k[i] = sc[i];
+    scalar_reduce(k);
+    Jac r;
+    scalar_mul_aff(r, k, x, y);
+    jac_add(acc, acc, r);
+  }
+  jac_to_aff(a.out + (size_t)o * 16, acc);
+}
+
+// ------------------------------------------------------------- launchers -------
+hipError_t launch_pdl_u1(const PdlU1Args& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  hipLaunchKernelGGL(pdl_u1_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_feldman(const FeldmanArgs& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  hipLaunchKernelGGL(feldman_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_ec_msm(const EcMsmArgs& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  hipLaunchKernelGGL(ec_msm_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace fsdkr

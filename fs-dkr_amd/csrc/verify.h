@@ -46,7 +46,7 @@ struct InverseArgs {
   const uint64_t* m_ptr;    // odd modulus (K32 limbs)
   uint32_t* out;            // [count][K32] inverse (may be null)
   uint32_t* unit;           // [count] 1 if gcd(y, m) == 1
-  uint32_t* scratch;        // 6 * (K32+2) * count words
+  uint32_t* scratch;        // unused (lane-cooperative inverse keeps its state in registers)
   uint32_t count;
 };
 
@@ -108,7 +108,7 @@ hipError_t launch_pdl_hash(const PdlHashArgs& a, hipStream_t st);
 hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st);
 hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st);
 hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);
-// lane-cooperative variant (inverse.hip): registers + DPP, no scratch
+// lane-cooperative Pornin inverse (inverse.hip): registers + DPP
 hipError_t launch_inverse_coop(uint32_t k32, const InverseArgs& a, hipStream_t st);
 hipError_t launch_eq_check(uint32_t k32, const EqCheckArgs& a, hipStream_t st);
 hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st);

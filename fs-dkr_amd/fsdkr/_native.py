@@ -104,6 +104,9 @@ def lib():
     L.fsdkr_mod_inverse.restype = ctypes.c_int
     L.fsdkr_ec_msm.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
     L.fsdkr_ec_msm.restype = ctypes.c_int
+    L.fsdkr_fixed_base_modexp.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, ctypes.c_uint32,
+                                          ctypes.c_uint32, u32p, u32p, ctypes.c_uint32, u32p]
+    L.fsdkr_fixed_base_modexp.restype = ctypes.c_int
     L.fsdkr_feldman_check.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u8p]
     L.fsdkr_feldman_check.restype = ctypes.c_int
     L.fsdkr_ring_pedersen_verify.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -192,6 +195,22 @@ class Context:
         O = np.zeros((count, mod_limbs), dtype=np.uint32)
         self.check(self._lib.fsdkr_modexp_batch(self._h, mod_limbs, count, _ptr(B), _ptr(E), exp_limbs, _ptr(I),
                                                 _ptr(Mo), len(mods), _ptr(O)))
+        return limbs_to_ints(O)
+
+    def fixed_base_modexp(self, bases, base_mod_idx, mods, base_idx, exps, mod_limbs):
+        """[bases[base_idx[i]] ^ exps[i] mod mods[base_mod_idx[base_idx[i]]]] via the fixed-base engine."""
+        count = len(exps)
+        if count == 0:
+            return []
+        exp_limbs = max(1, (max(e.bit_length() for e in exps) + 31) // 32)
+        B = ints_to_limbs(bases, mod_limbs)
+        Bm = np.ascontiguousarray(np.asarray(base_mod_idx, dtype=np.uint32))
+        Mo = ints_to_limbs(mods, mod_limbs)
+        Bi = np.ascontiguousarray(np.asarray(base_idx, dtype=np.uint32))
+        E = ints_to_limbs(exps, exp_limbs)
+        O = np.zeros((count, mod_limbs), dtype=np.uint32)
+        self.check(self._lib.fsdkr_fixed_base_modexp(self._h, mod_limbs, len(bases), _ptr(B), _ptr(Bm), _ptr(Mo),
+                                                     len(mods), count, _ptr(Bi), _ptr(E), exp_limbs, _ptr(O)))
         return limbs_to_ints(O)
 
     def set_modexp_group(self, lanes):

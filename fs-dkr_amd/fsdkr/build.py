@@ -2,7 +2,8 @@
 
 Objects go to fs-dkr_amd/build/, the shared library to
 fs-dkr_amd/fsdkr/libfsdkr.so (git-ignored, but shipped to the GPU box by
-gpurun).  Incremental on source/header mtimes."""
+gpurun).  Incremental: each object is rebuilt when its source or any header it
+includes (hipcc -MMD dependency file) is newer."""
 import concurrent.futures as cf
 import os
 import subprocess
@@ -18,20 +19,40 @@ LIB = os.path.join(PKG, "libfsdkr.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["modexp.hip", "verify.hip", "inverse.hip", "capi.cpp", "collect.cpp", "recover.cpp", "standalone.cpp"]
+SOURCES = ["modexp.hip", "fixedbase.hip", "inverse.hip", "vhash.hip", "vmont.hip", "vec.hip",
+           "capi.cpp", "collect.cpp", "recover.cpp", "standalone.cpp", "fixedbase_host.cpp"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
           "-Wno-unused-result"]
 
 
-def _headers():
-    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".h", ".hpp"))]
-    hs += [os.path.join(INCLUDE, "fsdkr", f) for f in os.listdir(os.path.join(INCLUDE, "fsdkr"))]
-    return hs
+def _obj(src):
+    return os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+
+
+def _deps(src):
+    """Files the object depends on, from the -MMD file of its last build."""
+    dep = _obj(src)[:-2] + ".d"
+    if not os.path.exists(dep):
+        return None
+    text = open(dep).read().replace("\\\n", " ")
+    files = text.split(":", 1)[1].split() if ":" in text else []
+    return [f for f in files if f.endswith((".h", ".hpp", ".hip", ".cpp"))]
+
+
+def _stale(src, force):
+    obj = _obj(src)
+    if force or not os.path.exists(obj):
+        return True
+    deps = _deps(src)
+    if deps is None:
+        return True
+    t = os.path.getmtime(obj)
+    return any(not os.path.exists(f) or os.path.getmtime(f) > t for f in deps + [os.path.join(CSRC, src)])
 
 
 def _compile(src, verbose):
-    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
-    cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+    obj = _obj(src)
+    cmd = [HIPCC] + CFLAGS + ["-MMD", "-MF", obj[:-2] + ".d", "-c", os.path.join(CSRC, src), "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -42,15 +63,8 @@ def _compile(src, verbose):
 
 def build(verbose=False, force=False):
     os.makedirs(BUILD, exist_ok=True)
-    hdr_mtime = max(os.path.getmtime(h) for h in _headers())
-    todo, objs = [], []
-    for src in SOURCES:
-        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
-        objs.append(obj)
-        stale = force or not os.path.exists(obj) or \
-            os.path.getmtime(obj) < max(os.path.getmtime(os.path.join(CSRC, src)), hdr_mtime)
-        if stale:
-            todo.append(src)
+    todo = [s for s in SOURCES if _stale(s, force)]
+    objs = [_obj(s) for s in SOURCES]
     if todo:
         with cf.ThreadPoolExecutor(max_workers=min(8, len(todo))) as ex:
             list(ex.map(lambda s: _compile(s, verbose), todo))

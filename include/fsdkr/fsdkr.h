@@ -181,6 +181,17 @@ typedef struct fsdkr_error {
  * NULL when the threshold or size check already fails.  Pure host logic. */
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out);
 
+/* Fixed-base batch: out[i] = bases[base_idx[i]] ^ exp[i] mod mods[base_mod_idx[base_idx[i]]]
+ * (exact).  The GPU builds one table of base^(2^(w j)) per base and evaluates
+ * every exponent with Brickell-Gordon-McCurley-Wilson windowing; results are
+ * identical to fsdkr_modexp_batch.  This is the engine behind the bases the
+ * reference exponentiates many times with curv BigInt::mod_pow: h1, h2 of a
+ * receiver's DLogStatement (zk_pdl_with_slack.rs:144-157, range_proofs.rs:129-137)
+ * and ring-Pedersen T (ring_pedersen_proof.rs:144).  mod_limbs in {64, 96}. */
+int fsdkr_fixed_base_modexp(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t n_bases, const uint32_t* bases,
+                            const uint32_t* base_mod_idx, const uint32_t* mods, uint32_t n_mod, uint32_t count,
+                            const uint32_t* base_idx, const uint32_t* exp, uint32_t exp_limbs, uint32_t* out);
+
 /* ---- Stand-alone checks (JoinMessage::collect, per-proof callers) ---------
  * Feldman share checks of validate_collect (refresh_message.rs:177-188, curv
  * VerifiableSS::validate_share_public): verdict[k*n + i] = 1 iff
