@@ -20,6 +20,10 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
+# collect() runs seven concurrent streams (csrc/collect.cpp stream plan); HIP's
+# default of 4 hardware queues per process would serialise three of them.  Must
+# be set before the HIP runtime initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402
 

@@ -112,7 +112,7 @@ uint32_t choose_window(uint32_t ebits) {
 // Launch one modexp job whose descriptors are already in device memory.
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st, const char* table_tag,
-                       uint32_t prio) {
+                       uint32_t prio, uint32_t group) {
   if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
   const int KD = shape_digits(k32);
@@ -143,7 +143,7 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.table = d_table;
   a.count = count;
   a.prio = prio;
-  a.group = c->modexp_group;
+  a.group = c->modexp_group ? c->modexp_group : group;   // a forced context setting wins (tuning, tests)
   const size_t tm = c->tbeg("modexp", st);
   int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
   c->tend(tm, st);

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "fbjob.hpp"
 #include "fsdkr/fsdkr.h"
 #include "hostbn.hpp"
 #include "kernels.h"
@@ -103,6 +104,11 @@ struct CollectPlan {
   uint32_t n_inv_nn = 0, n_eq_nn = 0, n_eq_nl = 0;
   std::vector<uint32_t> cpdl_extra, ae_bits;
   std::vector<uint8_t> ck_pre, dlog_pre;
+  FbJob fb;                 // h1_i, h2_i, ring-Pedersen T: fixed-base job
+  size_t d_FB = 0;          // its descriptor image (input region)
+  uint32_t* fb_table = nullptr;   // its scratch (separate context buffer)
+  uint16_t* fb_sched = nullptr;
+  uint32_t* fb_nsteps = nullptr;
 };
 
 void free_collect_plan(Ctx* c) {
@@ -315,15 +321,17 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   //   GA (nn, long)  = J1 s2^N | s^N  [2P]  ++  J9 (N+1)^s1 for s1 >= N  [<= P]
   //   J2 (nn, short) = c^e_pdl | c^e_A  [2P]
   //   J5 (nl, short) = z^e_pdl | zA^e_A [2P]
-  //   GD (nl, long)  = J4 h2^s3 | h2^s2A [2P] ++ J7 g^y1 | ni^y2 [2J] ++ J6 T^Z | sigma^n [Mt(M+11)]
-  //                    ++ J3 h1^s1 | h1^s1A [2P] ++ J8 ni^e1 | g^e2 [2J]      (longest exponents first)
+  //   GD (nl, long)  = J7 g^y1 | ni^y2 [2J] ++ J6 sigma^n [Mt*11] ++ J8 ni^e1 | g^e2 [2J]
+  //   FB (nl, fixed bases h1_i, h2_i, T_m; any slot) = J4 h2^s3 | h2^s2A [2P], J3 h1^s1 | h1^s1A [2P],
+  //                    RP T^Z [Mt*M]
   const size_t x_GA = L.out((size_t)3 * P * nn * 4 + 4);
   const size_t x_J1 = x_GA, x_J9 = x_GA + (size_t)2 * P * nn * 4;
   const size_t x_J2 = L.out((size_t)2 * P * nn * 4);
   const size_t x_J5 = L.out((size_t)2 * P * nl * 4);
-  const size_t x_GD = L.out(((size_t)4 * P + 4 * J + (size_t)Mt * (M + CK_M2) + 1) * nl * 4);
-  const size_t x_J4 = x_GD, x_J7 = x_J4 + (size_t)2 * P * nl * 4, x_J6 = x_J7 + (size_t)2 * J * nl * 4;
-  const size_t x_J3 = x_J6 + (size_t)Mt * (M + CK_M2) * nl * 4, x_J8 = x_J3 + (size_t)2 * P * nl * 4;
+  const size_t x_GD = L.out(((size_t)4 * J + (size_t)Mt * CK_M2 + 1) * nl * 4);
+  const size_t x_J7 = x_GD, x_J6 = x_J7 + (size_t)2 * J * nl * 4, x_J8 = x_J6 + (size_t)Mt * CK_M2 * nl * 4;
+  const size_t x_FB = L.out(((size_t)4 * P + (size_t)Mt * M + 1) * nl * 4);
+  const size_t x_J4 = x_FB, x_J3 = x_J4 + (size_t)2 * P * nl * 4, x_RP = x_J3 + (size_t)2 * P * nl * 4;
   const size_t x_invc = L.out((size_t)2 * P * nn * 4), x_invz = L.out((size_t)P * nl * 4);
   const size_t x_unn = L.out((size_t)2 * P * 4);    // unit flags of the nn inverses (c^eA, then extra c^e_pdl)
   const size_t x_uzA = L.out((size_t)P * 4), x_uzp = L.out((size_t)P * 4);
@@ -342,7 +350,7 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   const size_t desc_bound = (n_inst_nn + n_inst_nl) * 32 + 16 * 256 +
                             ((size_t)P + (size_t)Mt * M + (size_t)Mt * CK_M2 + 2 * J + P) * sizeof(EqOperand) +
                             2 * (size_t)P * sizeof(Prod3Operand) + (size_t)(2 * P + 2 * P) * 16 + (size_t)4 * P * 8 +
-                            (size_t)(2 * P + 2 * P) * 4 + 64 * 1024;
+                            (size_t)(2 * P + 2 * P) * 4 + (size_t)(3 * n + Mt) * 32 + 64 * 1024;
   const size_t total = Layout::al(in_bytes_pre + desc_bound) + L.out_bytes;
   uint8_t* dev = (uint8_t*)c->buf("collect_arena", total);
   if (!dev) {
@@ -356,9 +364,20 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   auto PI = [&](size_t o) { return (const uint32_t*)(dev + o); };
 
   // ---------------- modexp jobs
-  ModexpJob J1, J2, J3, J4, J5, J6, J7, J8, J9;
+  ModexpJob J1, J2, J5, J6, J7, J8, J9;
   J1.k32 = J2.k32 = J9.k32 = nn;
-  J3.k32 = J4.k32 = J5.k32 = J6.k32 = J7.k32 = J8.k32 = nl;
+  J5.k32 = J6.k32 = J7.k32 = J8.k32 = nl;
+  // receiver bases h1_i, h2_i (mod N~_i = nl-table row i) and ring-Pedersen T_m (row n + m):
+  // shared by 2n resp. M exponents -> BGMW tables (fixedbase.hip)
+  FbJob& FB = pl.fb;
+  FB = FbJob();
+  FB.k32 = nl;
+  std::vector<uint32_t> fb_h1(n), fb_h2(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    fb_h1[i] = FB.add_base(DI(o_h1 + (size_t)i * nl * 4), nl, i);
+    fb_h2[i] = FB.add_base(DI(o_h2 + (size_t)i * nl * 4), nl, i);
+  }
+  for (uint32_t m = 0; m < Mt; ++m) FB.add_base(DI(o_pT + (size_t)m * nl * 4), nl, n + m);
   std::vector<uint32_t> j9_pairs;
   for (int which = 0; which < 2; ++which)
     for (uint32_t p = 0; p < P; ++p) {
@@ -370,16 +389,16 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
       const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
       if (which == 0) J2.add(cp, nn, DX(x_epdl + (size_t)p * 32), 8, 256, i);
       else J2.add(cp, nn, DI(o_ae + (size_t)p * b->el * 4), b->el, a_e_max, i);
-      // J3: h1^s1 | J4: h2^s3 (s2 for Alice) | J5: z^e
-      const uint64_t h1 = DI(o_h1 + (size_t)i * nl * 4), h2 = DI(o_h2 + (size_t)i * nl * 4);
+      // fixed bases (FB): h1^s1 -> J3 slot | h2^s3 (s2 for Alice) -> J4 slot;  J5: z^e
+      const size_t slot = (size_t)which * P + p;
       if (which == 0) {
-        J3.add(h1, nl, DI(o_ps1 + (size_t)p * b->s1l * 4), b->s1l, pdl_s1_max, i);
-        J4.add(h2, nl, DI(o_ps3 + (size_t)p * b->s3l * 4), b->s3l, pdl_s3_max, i);
+        FB.add(fb_h1[i], DI(o_ps1 + (size_t)p * b->s1l * 4), b->s1l, pdl_s1_max, DX(x_J3 + slot * nl * 4));
+        FB.add(fb_h2[i], DI(o_ps3 + (size_t)p * b->s3l * 4), b->s3l, pdl_s3_max, DX(x_J4 + slot * nl * 4));
         J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DX(x_epdl + (size_t)p * 32), 8, 256, i);
       } else {
         const bool use = alice_pre[p];
-        J3.add(h1, nl, DI(o_as1 + (size_t)p * b->s1l * 4), use ? b->s1l : 0, a_s1_max, i);
-        J4.add(h2, nl, DI(o_as2 + (size_t)p * b->s3l * 4), use ? b->s3l : 0, a_s2_max, i);
+        FB.add(fb_h1[i], DI(o_as1 + (size_t)p * b->s1l * 4), use ? b->s1l : 0, a_s1_max, DX(x_J3 + slot * nl * 4));
+        FB.add(fb_h2[i], DI(o_as2 + (size_t)p * b->s3l * 4), use ? b->s3l : 0, a_s2_max, DX(x_J4 + slot * nl * 4));
         J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * b->el * 4), use ? b->el : 0, a_e_max, i);
       }
     }
@@ -391,7 +410,7 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     }
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k)  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144)
-      J6.add(DI(o_pT + (size_t)m * nl * 4), nl, DI(o_pZ + ((size_t)m * M + k) * b->zl * 4), b->zl, z_max, n + m);
+      FB.add(2 * n + m, DI(o_pZ + ((size_t)m * M + k) * b->zl * 4), b->zl, z_max, DX(x_RP + ((size_t)m * M + k) * nl * 4));
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < CK_M2; ++k)  // correct-key sigma_k^n mod n
       J6.add(DI(o_cks + ((size_t)m * CK_M2 + k) * nl * 4), nl, DI(o_ckn + (size_t)m * nl * 4), nl,
@@ -410,13 +429,19 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     j.pack(L.host);
     return o;
   };
-  ModexpJob GA = J1, GD = J4;
+  ModexpJob GA = J1, GD = J7;
   GA.append(J9);
-  GD.append(J7);
   GD.append(J6);
-  GD.append(J3);
   GD.append(J8);
   const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD);
+  FB.finalize();
+  const size_t d_FB = Layout::al(L.host.size());
+  {
+    std::vector<uint8_t> img;
+    FB.pack(img);
+    L.host.resize(d_FB);
+    L.host.insert(L.host.end(), img.begin(), img.end());
+  }
 
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N
   std::vector<uint64_t> bs_ptr(2 * (size_t)P), bn_ptr(2 * (size_t)P);
@@ -486,7 +511,7 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N)
       EqOperand e;
-      e.a = DX(x_J6 + ((size_t)m * M + k) * nl * 4);
+      e.a = DX(x_RP + ((size_t)m * M + k) * nl * 4);
       e.b = DI(o_one);
       e.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
       e.d = DI(o_pS + (size_t)m * nl * 4);
@@ -499,7 +524,7 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < CK_M2; ++k) {  // correct key: sigma^n == rho (mod n)
       EqOperand e;
-      e.a = DX(x_J6 + ((size_t)Mt * M + (size_t)m * CK_M2 + k) * nl * 4);
+      e.a = DX(x_J6 + ((size_t)m * CK_M2 + k) * nl * 4);
       e.b = DI(o_one);
       e.c = DI(o_rho + ((size_t)m * CK_M2 + k) * nl * 4);
       e.d = DI(o_one);
@@ -547,6 +572,20 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     c->fail("internal: descriptor bound exceeded");
     return FSDKR_E_ARG;
   }
+  // fixed-base scratch (power tables, schedules, step counts): its own context buffer
+  {
+    const int KD = shape_digits(nl);
+    const size_t tb = Layout::al(FB.table_bytes(KD)), sb = Layout::al(FB.sched_bytes());
+    uint8_t* fbs = (uint8_t*)c->buf("collect_fb", tb + sb + FB.nsteps_bytes() + 256);
+    if (!fbs) {
+      c->fail("fsdkr_verify_collect: fixed-base scratch allocation failed");
+      return FSDKR_E_OOM;
+    }
+    pl.fb_table = (uint32_t*)fbs;
+    pl.fb_sched = (uint16_t*)(fbs + tb);
+    pl.fb_nsteps = (uint32_t*)(fbs + tb + sb);
+  }
+  pl.d_FB = d_FB;
 
   // ---------------- record the plan and upload the image (the only host->device copy)
   pl.el = b->el;
@@ -629,11 +668,65 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   uint32_t *cons_nn = nullptr, *cons_nl = nullptr;
   if ((rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn, "collect_nn"))) return rc;
   if ((rc = setup_moduli(c, nl, PI(o_mods), n_mods_nl, &cons_nl, "collect_nl"))) return rc;
-  // ---- stream plan (HIP maps streams onto 4 hardware queues, so at most 4 lanes of work):
-  //   st      : pdl_hash, binom x2 | fork | ped_hash, J5, nl inverses, pdl_u1, Feldman | join | eq, prod3, alice
-  //   side 0  : GA  (nn, long exponents)
-  //   side 1  : GD  (nl, long exponents)
-  //   side 2  : J2 (nn, 256-bit challenges) -> nn inverses
+  // ---- stream plan (seven concurrent lanes of work: give HIP >= 7 hardware queues,
+  //      GPU_MAX_HW_QUEUES, or streams share queues and serialise):
+  //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
+  //   side 1  : FB (fixed bases h1, h2, T: schedules, tables, exponents)
+  //   side 3  : ped_hash (serial SHA-256 chains, priority)
+  //   side 4  : GD (nl: correct-key, DLog; priority)
+  //   st      : pdl_hash, binom x2 | fork | J5, nl inverses | join | eq, prod3, alice
+  //   side 2  :                    J2 (nn, 256-bit challenges) -> nn inverses
+  //   side 5  :                    pdl_u1, Feldman (secp256k1)
+  std::vector<hipEvent_t> done;
+  auto fork = [&](hipStream_t from, hipEvent_t* ev) -> int {
+    int r = c->hip_check(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event");
+    if (!r) (void)hipEventRecord(*ev, from);
+    return r;
+  };
+  auto join_later = [&](hipStream_t ss) -> int {
+    hipEvent_t ev;
+    int r = c->hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event");
+    if (r) return r;
+    (void)hipEventRecord(ev, ss);
+    done.push_back(ev);
+    return FSDKR_OK;
+  };
+  static const char* tags[4] = {"mxt_GA", "mxt_GD", "mxt_J2", "mxt_J5"};
+  // prio: s_setprio level of the launch's waves (latency-critical chains); group: lanes per instance
+  auto launch_group = [&](int k, hipStream_t ss, uint32_t prio, uint32_t group) -> int {
+    if (!pl.jcount[k]) return FSDKR_OK;
+    const uint32_t* cons = (pl.jk32[k] == nn) ? cons_nn : cons_nl;
+    return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
+                              tags[k], prio, group);
+  };
+  // (1) chains that need only the inputs and the moduli constants start at once
+  hipEvent_t consts_ready;
+  if ((rc = fork(st, &consts_ready))) return rc;
+  {  // GA: s2^N, s^N mod N^2 (4096-bit, 2048-bit exponents): the longest chains
+    hipStream_t ss = c->side_stream(0);
+    (void)hipStreamWaitEvent(ss, consts_ready, 0);
+    if ((rc = launch_group(0, ss, 2, 0)) || (rc = join_later(ss))) return rc;
+  }
+  {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
+    hipStream_t ss = c->side_stream(1);
+    (void)hipStreamWaitEvent(ss, consts_ready, 0);
+    FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps};
+    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect")) || (rc = join_later(ss))) return rc;
+  }
+  {  // ring-Pedersen challenges: one serial SHA-256 chain per message, needed only by the final checks
+    hipStream_t ss = c->side_stream(3);
+    PedHashArgs h{PI(o_pA), M, nl, PX(x_pbits), PX(x_ppanic), Mt};
+    c->mark("ped_hash", true, ss);
+    rc = c->hip_check(launch_ped_hash(h, ss), "ped_hash");
+    c->mark("ped_hash", false, ss);
+    if (rc || (rc = join_later(ss))) return rc;
+  }
+  {  // GD: correct-key sigma^n, DLog g^y / ni^e (2048-bit exponents, few instances)
+    hipStream_t ss = c->side_stream(4);
+    (void)hipStreamWaitEvent(ss, consts_ready, 0);
+    if ((rc = launch_group(1, ss, 2, 0)) || (rc = join_later(ss))) return rc;
+  }
+  // (2) PDL challenges, then the jobs that exponentiate by them
   {
     PdlHashArgs a{PI(o_Q), PI(o_enc), PI(o_pz), PI(o_pu1), PI(o_pu2), PI(o_pu3), nn, nl, PX(x_epdl), P};
     c->mark("pdl_hash", true);
@@ -648,42 +741,35 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     if ((rc = c->hip_check(launch_binom(a2, st), "binom"))) return rc;
   }
   hipEvent_t ready;
-  if ((rc = c->hip_check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event"))) return rc;
-  (void)hipEventRecord(ready, st);
-  std::vector<hipEvent_t> done;
-  static const char* tags[4] = {"mxt_GA", "mxt_GD", "mxt_J2", "mxt_J5"};
-  auto launch_group = [&](int k, hipStream_t ss) -> int {
-    if (!pl.jcount[k]) return FSDKR_OK;
-    const uint32_t* cons = (pl.jk32[k] == nn) ? cons_nn : cons_nl;
-    // GA (4096-bit moduli, 2048-bit exponents) is the longest chain: its waves get issue priority
-    return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
-                              tags[k], k == 0 ? 1u : 0u);
-  };
-  for (int k = 0; k < 3; ++k) {
-    hipStream_t ss = c->side_stream(k);
+  if ((rc = fork(st, &ready))) return rc;
+  {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses
+    hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
-    if ((rc = launch_group(k, ss))) return rc;
-    if (k == 2) {  // nn inverses right behind the challenges' modexps
-      InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
-                    nullptr, pl.n_inv_nn};
-      c->mark("inverse", true, ss);
-      rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
-      c->mark("inverse", false, ss);
-      if (rc) return rc;
-    }
-    hipEvent_t ev;
-    if ((rc = c->hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return rc;
-    (void)hipEventRecord(ev, ss);
-    done.push_back(ev);
+    if ((rc = launch_group(2, ss, 0, 4))) return rc;
+    InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
+                  nullptr, pl.n_inv_nn};
+    c->mark("inverse", true, ss);
+    rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
+    c->mark("inverse", false, ss);
+    if (rc || (rc = join_later(ss))) return rc;
   }
-  {
-    PedHashArgs h{PI(o_pA), M, nl, PX(x_pbits), PX(x_ppanic), Mt};
-    c->mark("ped_hash", true);
-    rc = c->hip_check(launch_ped_hash(h, st), "ped_hash");
-    c->mark("ped_hash", false);
+  {  // secp256k1 checks (one thread per pair, latency-bound): Feldman + PDL u1 off the main chain
+    hipStream_t ss = c->side_stream(5);
+    (void)hipStreamWaitEvent(ss, ready, 0);
+    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
+    c->mark("ec", true, ss);
+    rc = c->hip_check(launch_pdl_u1(u, ss), "pdl_u1");
+    c->mark("ec", false, ss);
     if (rc) return rc;
+    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
+    c->mark("ec", true, ss);
+    rc = c->hip_check(launch_feldman(f, ss), "feldman");
+    c->mark("ec", false, ss);
+    if (rc || (rc = join_later(ss))) return rc;
   }
-  if ((rc = launch_group(3, st))) return rc;
+  (void)hipEventDestroy(consts_ready);
+  (void)hipEventDestroy(ready);
+  if ((rc = launch_group(3, st, 1, 8))) return rc;   // J5: z^e (2048-bit, 256-bit challenges)
   {
     InverseArgs b1{(const uint64_t*)(dev + d_iynl), (const uint64_t*)(dev + d_imnl), PX(x_invz), PX(x_uzA),
                    nullptr, P};
@@ -695,23 +781,10 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
                    nullptr, P};
     if ((rc = c->hip_check(launch_inverse(nl, b2, st), "inverse nl 2"))) return rc;
   }
-  {
-    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
-    c->mark("ec", true);
-    rc = c->hip_check(launch_pdl_u1(u, st), "pdl_u1");
-    c->mark("ec", false);
-    if (rc) return rc;
-    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
-    c->mark("ec", true);
-    rc = c->hip_check(launch_feldman(f, st), "feldman");
-    c->mark("ec", false);
-    if (rc) return rc;
-  }
   for (hipEvent_t ev : done) {
     (void)hipStreamWaitEvent(st, ev, 0);
     (void)hipEventDestroy(ev);
   }
-  (void)hipEventDestroy(ready);
   // equality checks and exact products
   {
     EqCheckArgs a{(const EqOperand*)(dev + d_eqnn), PI(d_eqnnm), cons_nn, PX(x_pbits), DI(o_one), PX(x_eq2),

@@ -37,6 +37,8 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   const int li = threadIdx.x / G;
   const uint32_t b = blockIdx.x * IPB + li;
   if (b >= a.count) return;
+  // the table chain heads the fixed-base pipeline: its waves win issue arbitration
+  __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* C = a.consts + (size_t)a.mod_idx[b] * STRIDE;
   MT M;
@@ -73,29 +75,52 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   }
 }
 
-// One thread per instance: the BGMW product schedule of its exponent.
-__global__ void fb_sched_kernel(const FbSchedArgs a) {
+// One thread per instance: the BGMW product schedule of its exponent, by a
+// counting sort of its w-bit digits (O(h + 2^w)): for d = max digit .. 1 the
+// windows j with e_j = d (ascending j), then one A-step.
+constexpr int FB_SCHED_BLOCK = 64;
+constexpr int FB_MAX_W = 8;
+__global__ __launch_bounds__(FB_SCHED_BLOCK) void fb_sched_kernel(const FbSchedArgs a) {
+  __shared__ uint16_t cnt_lds[FB_SCHED_BLOCK * (1 << FB_MAX_W)];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.count) return;
   const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[i]);
   const uint32_t elen = a.exp_len[i];
-  const uint32_t h = a.h[i], w = a.w, mask = (1u << w) - 1;
+  const uint32_t h = a.h[i], w = a.w, nd = 1u << w, mask = nd - 1;
+  uint16_t* cnt = cnt_lds + threadIdx.x * (1 << FB_MAX_W);
   auto digit = [&](uint32_t j) -> uint32_t {
     const uint32_t p = j * w, lo = p >> 5, sh = p & 31;
     const uint32_t v0 = (lo < elen) ? E[lo] : 0u;
     const uint32_t v1 = (lo + 1 < elen) ? E[lo + 1] : 0u;
     return (uint32_t)((((uint64_t)v1 << 32) | v0) >> sh) & mask;
   };
+  for (uint32_t d = 0; d < nd; ++d) cnt[d] = 0;
   uint32_t dmax = 0;
-  for (uint32_t j = 0; j < h; ++j) dmax = max(dmax, digit(j));
-  uint16_t* S = a.sched + (size_t)i * a.stride;
-  uint32_t n = 0;
-  for (uint32_t d = dmax; d >= 1; --d) {
-    for (uint32_t j = 0; j < h; ++j)
-      if (digit(j) == d) S[n++] = (uint16_t)j;
-    S[n++] = FB_A_STEP;
+  for (uint32_t j = 0; j < h; ++j) {
+    const uint32_t d = digit(j);
+    cnt[d] = (uint16_t)(cnt[d] + 1);
+    dmax = max(dmax, d);
   }
-  a.nsteps[i] = n;
+  // start offset of digit d's windows: digits above d first, one A-step after each digit value
+  uint32_t pos = 0;
+  for (uint32_t d = dmax; d >= 1; --d) {
+    const uint32_t c = cnt[d];
+    cnt[d] = (uint16_t)pos;
+    pos += c + 1;
+  }
+  uint16_t* S = a.sched + (size_t)i * a.stride;
+  for (uint32_t d = dmax; d >= 1; --d) {          // A-step slots (the position after each group)
+    const uint32_t end = (d > 1) ? cnt[d - 1] : pos;
+    S[end - 1] = FB_A_STEP;
+  }
+  for (uint32_t j = 0; j < h; ++j) {
+    const uint32_t d = digit(j);
+    if (d) {
+      S[cnt[d]] = (uint16_t)j;
+      cnt[d] = (uint16_t)(cnt[d] + 1);
+    }
+  }
+  a.nsteps[i] = pos;
 }
 
 template <int KD, int G, int K32>
@@ -195,7 +220,9 @@ hipError_t launch_fb_table(uint32_t k32, const FbTableArgs& a, hipStream_t st) {
 
 hipError_t launch_fb_sched(const FbSchedArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
-  hipLaunchKernelGGL(fb_sched_kernel, dim3((a.count + 63) / 64), dim3(64), 0, st, a);
+  if (a.w > FB_MAX_W) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fb_sched_kernel, dim3((a.count + FB_SCHED_BLOCK - 1) / FB_SCHED_BLOCK), dim3(FB_SCHED_BLOCK), 0,
+                     st, a);
   return hipGetLastError();
 }
 

@@ -32,11 +32,11 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
   FbExpArgs ea{U32(j.off.i_toff), U32(j.off.e_mod), U64(j.off.o_ptr), consts, d.table, d.sched, d.nsteps, j.stride,
                (uint32_t)j.count()};
   int rc;
+  if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
   size_t m = c->tbeg("fb_table", st);
   rc = c->hip_check(launch_fb_table(j.k32, ta, st), "fb_table launch");
   c->tend(m, st);
   if (rc) return rc;
-  if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
   m = c->tbeg("fb_exp", st);
   rc = c->hip_check(launch_fb_exp(j.k32, ea, fb_group(c, j.count()), st), tag);
   c->tend(m, st);

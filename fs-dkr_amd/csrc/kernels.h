@@ -22,7 +22,7 @@ struct ModexpArgs {
   uint32_t* out;             // [count][K32]
   uint32_t* table;           // [count][2^window][KD] scratch
   uint32_t count;
-  uint32_t prio;             // 1: latency-critical launch, waves raise their issue priority (s_setprio)
+  uint32_t prio;             // > 0: latency-critical launch, its waves raise their issue priority to s_setprio(prio)
   uint32_t group;            // lanes per instance (0 = choose by batch size)
 };
 

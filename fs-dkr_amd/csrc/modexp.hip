@@ -95,7 +95,9 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   if (inst >= a.count) return;
   // a latency-critical launch sharing the chip with throughput launches on other
   // streams: its waves win the SIMD issue arbitration
-  if (a.prio) __builtin_amdgcn_s_setprio(3);
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
   MT M;

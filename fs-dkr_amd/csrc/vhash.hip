@@ -94,6 +94,7 @@ __global__ void pdl_hash_kernel(const PdlHashArgs a) {
 __global__ void ped_hash_kernel(const PedHashArgs a) {
   const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= a.count) return;
+  __builtin_amdgcn_s_setprio(3);   // a long serial chain sharing SIMDs with exponentiation waves
   __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
   Sha256 h;
   h.init(sha_w + threadIdx.x * 16);

@@ -165,8 +165,6 @@ hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
   return launch_inverse_coop(k32, a, st);
 }
-  return hipGetLastError();
-}
 template <int KD, int G, int K32>
 static hipError_t eq_launch(const EqCheckArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((eq_check_kernel<KD, G, K32>), dim3(blocks_for(a.count, BLOCK / G)), dim3(BLOCK), 0, st, a);

@@ -7,6 +7,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (REPO, os.path.join(REPO, "fs-dkr_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
+# the collect() pipeline runs seven concurrent streams (see bench.py)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 
 def pytest_configure(config):
