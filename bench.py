@@ -20,10 +20,11 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
-# collect() runs seven concurrent streams (csrc/collect.cpp stream plan); HIP's
-# default of 4 hardware queues per process would serialise three of them.  Must
-# be set before the HIP runtime initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# collect() runs seven concurrent streams (csrc/collect.cpp stream plan); with
+# HIP's default of 4 hardware queues per process (exported as 4 on the GPU
+# boxes) three of them would share queues and serialise.  Raise it (never
+# lower it) before the HIP runtime initialises.
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 import numpy as np  # noqa: E402
 
@@ -178,6 +179,8 @@ def main():
     ap.add_argument("--modexp-count", type=int, default=65536)
     ap.add_argument("--cpu-pairs", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--emulate-shard", type=int, default=0,
+                    help="analysis only: run rank 0's slice of a W-way shard on one GPU and report its step time")
     a = ap.parse_args()
 
     import torch
@@ -198,8 +201,9 @@ def main():
     gen_s = time.perf_counter() - tg
     # shard: contiguous slices of the refresh messages and of the joins (fsdkr.shard)
     from fsdkr import shard
-    r0, r1 = shard.shard_range(R, world, rank)
-    j0, j1 = shard.shard_range(J, world, rank)
+    sw = a.emulate_shard if (a.emulate_shard and world == 1) else world
+    r0, r1 = shard.shard_range(R, sw, rank)
+    j0, j1 = shard.shard_range(J, sw, rank)
     batch = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], 256, a.key_bits, n_recv=n)
     ctx.collect_prepare(batch)
     P = R * n
@@ -213,6 +217,15 @@ def main():
 
     for _ in range(a.warmup):
         res = step()
+    if sw != world:       # emulated shard: verdicts cover only this slice; report its step time
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        print(json.dumps({"emulated_shard": sw, "refresh_slice": [r0, r1], "join_slice": [j0, j1],
+                          "ms_per_step": (time.perf_counter() - t0) / a.steps * 1e3}), flush=True)
+        return
     # correctness gate: every synthetic proof verifies
     assert res.feldman[:P].all() and (res.pdl[:P] == 7).all() and res.range[:P].all() and \
         (res.ped[:R + J] == 1).all() and res.ck[:R + J].all() and (res.dlog[:J] == 3).all(), \

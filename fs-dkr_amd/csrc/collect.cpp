@@ -10,6 +10,7 @@
 //   -> alice_hash, pdl_u1, feldman -> one D2H copy of the verdict words.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -705,7 +706,19 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   {  // GA: s2^N, s^N mod N^2 (4096-bit, 2048-bit exponents): the longest chains
     hipStream_t ss = c->side_stream(0);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    if ((rc = launch_group(0, ss, 2, 0)) || (rc = join_later(ss))) return rc;
+    // lanes per instance: GA shares the chip with six other streams, so it takes
+    // the largest group that keeps it within about half the resident lanes
+    // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); few instances
+    // (multi-GPU shards) get 16 lanes for latency.  FSDKR_COLLECT_GA_G overrides.
+    static const uint32_t ga_forced = [] {
+      const char* e = getenv("FSDKR_COLLECT_GA_G");
+      return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    uint32_t ga_group = 4;
+    for (uint32_t g : {8u, 16u})
+      if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
+    if (ga_forced) ga_group = ga_forced;
+    if ((rc = launch_group(0, ss, 2, ga_group)) || (rc = join_later(ss))) return rc;
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);

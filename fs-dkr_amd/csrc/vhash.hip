@@ -91,15 +91,91 @@ __global__ void pdl_hash_kernel(const PdlHashArgs a) {
 // e = H(A_0 .. A_{M-1}); bits[m][i/32] bit i%32 = Lsb0 bit i of e.to_bytes();
 // panic[m] != 0 if e.to_bytes() is shorter than M bits (BitVec index panic at bit
 // panic[m]-1; checks before that index still run and may fail first).
-__global__ void ped_hash_kernel(const PedHashArgs a) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+//
+// One wave per message.  The M values are absorbed PED_CHUNK at a time: the 64
+// lanes load the chunk's limbs (coalesced) into LDS, lanes 0..PED_CHUNK-1 find
+// each value's minimal big-endian length, and all lanes scatter the bytes of
+// the chunk's to_bytes() encodings into one contiguous LDS byte stream behind
+// the previous chunk's unconsumed tail; lane 0 then runs the serial SHA-256
+// compressions straight from LDS.  (One thread per message reading limbs from
+// global memory word by word exposed the load latency on every 4 bytes.)
+constexpr int PED_CHUNK = 16;
+constexpr int PED_MAX_LIMBS = 96;   // 3072-bit moduli
+__global__ __launch_bounds__(64) void ped_hash_kernel(const PedHashArgs a) {
+  const uint32_t m = blockIdx.x;
   if (m >= a.count) return;
   __builtin_amdgcn_s_setprio(3);   // a long serial chain sharing SIMDs with exponentiation waves
-  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
+  const int lane = threadIdx.x;
+  __shared__ uint32_t lim[PED_CHUNK * PED_MAX_LIMBS];
+  __shared__ uint8_t stream[64 + PED_CHUNK * PED_MAX_LIMBS * 4 + 64];
+  __shared__ uint32_t len[PED_CHUNK], off[PED_CHUNK + 1];
+  __shared__ uint32_t sha_w[16];
+  const uint32_t nl = a.a_len;
+  const uint32_t* A = a.A + (size_t)m * a.M * nl;
   Sha256 h;
-  h.init(sha_w + threadIdx.x * 16);
-  const uint32_t* A = a.A + (size_t)m * a.M * a.a_len;
-  for (uint32_t i = 0; i < a.M; ++i) h.bigint(A + (size_t)i * a.a_len, a.a_len);
+  if (lane == 0) h.init(sha_w);
+  uint32_t have = 0;          // unconsumed stream bytes at the front of `stream` (< 64)
+  uint64_t consumed = 0;      // bytes compressed so far
+  for (uint32_t c0 = 0; c0 < a.M; c0 += PED_CHUNK) {
+    const uint32_t cnt = min((uint32_t)PED_CHUNK, a.M - c0);
+    for (uint32_t k = lane; k < cnt * nl; k += 64) lim[k] = A[(size_t)c0 * nl + k];
+    __syncthreads();
+    if (lane < (int)cnt) {     // BigInt::to_bytes length: minimal magnitude, 0 -> one 0x00 byte
+      const uint32_t* x = lim + lane * nl;
+      int top = (int)nl - 1;
+      while (top >= 0 && x[top] == 0) --top;
+      uint32_t bytes = 1;
+      if (top >= 0) bytes = 4u * (uint32_t)top + (32u - (uint32_t)__builtin_clz(x[top]) + 7u) / 8u;
+      len[lane] = bytes;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      uint32_t o = have;
+      for (uint32_t i = 0; i < cnt; ++i) {
+        off[i] = o;
+        o += len[i];
+      }
+      off[cnt] = o;
+    }
+    __syncthreads();
+    // big-endian bytes: byte j (from the least significant end) of value i at off[i] + len[i] - 1 - j
+    for (uint32_t k = lane; k < cnt * nl; k += 64) {
+      const uint32_t i = k / nl, limb = k % nl, v = lim[k];
+      const uint32_t L = len[i], base = off[i] + L - 1;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t j = 4 * limb + b;
+        if (j < L) stream[base - j] = (uint8_t)(v >> (8 * b));
+      }
+    }
+    __syncthreads();
+    const uint32_t total = off[cnt];
+    const uint32_t blocks = total / 64;
+    if (lane == 0) {
+      for (uint32_t blk = 0; blk < blocks; ++blk) {
+        const uint8_t* s = stream + blk * 64;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          sha_w[q] = ((uint32_t)s[4 * q] << 24) | ((uint32_t)s[4 * q + 1] << 16) | ((uint32_t)s[4 * q + 2] << 8) |
+                     (uint32_t)s[4 * q + 3];
+        h.compress();
+      }
+    }
+    consumed += 64ull * blocks;
+    have = total - 64 * blocks;
+    __syncthreads();
+    // move the tail (< 64 bytes) to the front for the next chunk
+    uint8_t t = 0;
+    if (lane < (int)have) t = stream[64 * blocks + lane];
+    __syncthreads();
+    if (lane < (int)have) stream[lane] = t;
+    __syncthreads();
+  }
+  if (lane != 0) return;
+  for (int q = 0; q < 16; ++q) sha_w[q] = 0;
+  h.nbuf = 0;
+  h.total = consumed;
+  for (uint32_t k = 0; k < have; ++k) h.byte(stream[k]);
   uint32_t e[8];
   h.finish_le(e);
   // big-endian minimal bytes of e
@@ -173,7 +249,8 @@ hipError_t launch_pdl_hash(const PdlHashArgs& a, hipStream_t st) {
 }
 hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
-  hipLaunchKernelGGL(ped_hash_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
+  if (a.a_len > (uint32_t)PED_MAX_LIMBS) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ped_hash_kernel, dim3(a.count), dim3(64), 0, st, a);   // one wave per message
   return hipGetLastError();
 }
 hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st) {

@@ -90,7 +90,10 @@ class CollectBatch:
         c.n_recv = n if n_recv else 0
         self.c = c
         ref = lens[0][0] if R else 0
-        self.header_only = (R <= local_key.t or R == 0 or any(tuple(l) != (ref, ref, ref) for l in lens[:R])
+        # the threshold check (refresh_message.rs:149) is about the whole message set: a
+        # multi-GPU shard (n_recv given) holds a slice that may be <= t messages
+        below_threshold = R <= local_key.t and not n_recv
+        self.header_only = (below_threshold or R == 0 or any(tuple(l) != (ref, ref, ref) for l in lens[:R])
                             or ref < n or any(len(m.range_proofs) < n for m in msgs))
         if self.header_only:
             return

@@ -8,7 +8,7 @@ for p in (REPO, os.path.join(REPO, "fs-dkr_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
 # the collect() pipeline runs seven concurrent streams (see bench.py)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
 def pytest_configure(config):

@@ -78,6 +78,18 @@ def test_collect_valid_2048(gpu_ctx):
     _same_key(ko, kg)
 
 
+def test_collect_valid_3072(gpu_ctx):
+    """BASELINE configs[4] shape: t=1, n=3 with PAILLIER_KEY_SIZE = 3072 (96-limb N,
+    192-limb N^2), plus one tampered range proof."""
+    keys, msgs, dks, _ = _dkr(1, 3, "collect-gpu-3072", key_bits=3072)
+    ro, rg, ko, kg = _both(msgs, keys[2], dks[2], [], key_bits=3072, ctx=gpu_ctx)
+    assert ro is None and rg is None
+    _same_key(ko, kg)
+    m2 = _tampered(msgs, lambda m: _bump_range(m, 1, 2, s=m[1].range_proofs[2].s + 1))
+    ro, rg, _, _ = _both(m2, keys[0], dks[0], [], key_bits=3072, ctx=gpu_ctx)
+    assert ro == ("RangeProof", {"party_index": 2}) and rg == ro
+
+
 def _tampered(msgs, fn):
     m2 = copy.deepcopy(msgs)
     fn(m2)
