@@ -718,7 +718,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     for (uint32_t g : {8u, 16u})
       if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
     if (ga_forced) ga_group = ga_forced;
-    if ((rc = launch_group(0, ss, 2, ga_group)) || (rc = join_later(ss))) return rc;
+    if ((rc = launch_group(0, ss, 3, ga_group)) || (rc = join_later(ss))) return rc;
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);

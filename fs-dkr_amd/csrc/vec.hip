@@ -49,6 +49,7 @@ __global__ void pdl_u1_kernel(const PdlU1Args a) {
   using namespace ec;
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.count) return;
+  __builtin_amdgcn_s_setprio(1);   // one long serial EC chain per thread
   uint32_t k1[8], k2[8];
   bigint_mod_q(k1, a.s1 + (size_t)p * a.s1_len, a.s1_len);
   // k2 = (q - (e mod q)) mod q
@@ -69,14 +70,8 @@ __global__ void pdl_u1_kernel(const PdlU1Args a) {
   fe_load(gy, GY_LIMBS);
   const bool qinf = aff_load(qx, qy, a.Q + (size_t)p * 16);
   const bool uinf = aff_load(ux, uy, a.u1 + (size_t)p * 16);
-  Jac r1, r2, r;
-  scalar_mul_aff(r1, k1, gx, gy);
-  if (qinf) {
-    jac_set_inf(r2);
-  } else {
-    scalar_mul_aff(r2, k2, qx, qy);
-  }
-  jac_add(r, r1, r2);
+  Jac r;
+  shamir_mul2_aff(r, k1, gx, gy, k2, qx, qy, qinf);
   const bool eq = jac_eq_aff(r, ux, uy, uinf);
   a.verdict[p] = (uint8_t)((a.verdict[p] & ~1u) | (eq ? 1u : 0u));
 }

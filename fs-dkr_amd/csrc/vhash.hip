@@ -104,7 +104,7 @@ constexpr int PED_MAX_LIMBS = 96;   // 3072-bit moduli
 __global__ __launch_bounds__(64) void ped_hash_kernel(const PedHashArgs a) {
   const uint32_t m = blockIdx.x;
   if (m >= a.count) return;
-  __builtin_amdgcn_s_setprio(3);   // a long serial chain sharing SIMDs with exponentiation waves
+  __builtin_amdgcn_s_setprio(2);   // a serial chain sharing SIMDs with exponentiation waves
   const int lane = threadIdx.x;
   __shared__ uint32_t lim[PED_CHUNK * PED_MAX_LIMBS];
   __shared__ uint8_t stream[64 + PED_CHUNK * PED_MAX_LIMBS * 4 + 64];
