@@ -158,9 +158,11 @@ struct Mont29 {
     const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
 #pragma unroll
     for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
-    const uint64_t c = acc[s0] >> 29;
-    acc[s1] += mk64((uint32_t)c & m_lane0, (uint32_t)(c >> 32) & m_lane0);
-    acc[s0] = next64(acc[s0]);
+    // every lane carries its lowest column into the next one (value-preserving;
+    // in lane 0 that column is 0 mod 2^29 after m*n), so the digit that moves
+    // down to lane g-1 fits 29 bits: one 32-bit DPP move, no lane-0 masking
+    acc[s1] += acc[s0] >> 29;
+    acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0] & M29) & m_top);
     if constexpr (((R + 1) % NSTEP == 0) || (R + 1 == L)) norm_step<(R + 1) % L>(acc);
     __builtin_amdgcn_sched_barrier(0);
   }
