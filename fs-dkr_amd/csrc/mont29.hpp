@@ -107,6 +107,11 @@ struct Mont29 {
   static_assert(KD % G == 0, "KD must split evenly over the group");
   // normalisation points inside one L-row cycle: at most 18 rows apart (bound: 31)
   static constexpr int NSTEP = L <= 18 ? L : (L + 1) / 2 <= 18 ? (L + 1) / 2 : (L + 2) / 3;
+  // A column spends exactly L rows in a lane and leaves it as a 29-bit digit
+  // (row(): the retired column's carry stays behind), gaining < 2^59.01 per row:
+  // for L <= 24 it cannot reach 2^64 before it moves on, so only the final carry
+  // passes of mul() are needed.  Longer lanes normalise every NSTEP rows.
+  static constexpr bool NORM_IN_CYCLE = L > 24;
 
   uint32_t n[L];
   uint32_t ninv;      // -N^-1 mod 2^29
@@ -163,7 +168,7 @@ struct Mont29 {
     // down to lane g-1 fits 29 bits: one 32-bit DPP move, no lane-0 masking
     acc[s1] += acc[s0] >> 29;
     acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0] & M29) & m_top);
-    if constexpr (((R + 1) % NSTEP == 0) || (R + 1 == L)) norm_step<(R + 1) % L>(acc);
+    if constexpr (NORM_IN_CYCLE && (((R + 1) % NSTEP == 0) || (R + 1 == L))) norm_step<(R + 1) % L>(acc);
     __builtin_amdgcn_sched_barrier(0);
   }
 
