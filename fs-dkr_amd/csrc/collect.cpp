@@ -714,8 +714,8 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
       const char* e = getenv("FSDKR_COLLECT_GA_G");
       return e ? (uint32_t)atoi(e) : 0u;
     }();
-    uint32_t ga_group = 4;
-    for (uint32_t g : {8u, 16u})
+    uint32_t ga_group = 8;
+    for (uint32_t g : {16u})
       if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
     if (ga_forced) ga_group = ga_forced;
     if ((rc = launch_group(0, ss, 3, ga_group)) || (rc = join_later(ss))) return rc;
@@ -758,7 +758,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
-    if ((rc = launch_group(2, ss, 0, 4))) return rc;
+    if ((rc = launch_group(2, ss, 0, 8))) return rc;
     InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
                   nullptr, pl.n_inv_nn};
     c->mark("inverse", true, ss);

@@ -15,9 +15,8 @@ namespace fsdkr {
 static int fb_group(Ctx* c, size_t count) {
   if (c->modexp_group == 2 || c->modexp_group == 4 || c->modexp_group == 8) return (int)c->modexp_group;
   constexpr size_t kLaneCapacity = 256ull * 4 * 2 * 64;   // CUs x SIMDs x resident waves x lanes
-  if (count * 8 <= kLaneCapacity) return 8;
-  if (count * 4 <= kLaneCapacity) return 4;
-  return 2;
+  // 4 lanes (L = 18, no in-cycle normalisation) is the most efficient per MAC
+  return count * 8 <= kLaneCapacity ? 8 : 4;
 }
 
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag) {

@@ -221,12 +221,14 @@ hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_
   }
 }
 
-// Lanes per instance.  G with L = KD/G = 36 digits per lane is the most
-// efficient per MAC once a launch fills the chip; a launch that cannot fill it
-// runs with more lanes per instance (L = 18 or 9) for lower latency: the
-// largest G whose lanes still fit the resident-wave capacity.
+// Lanes per instance.  L = KD/G = 18 digits per lane is the most efficient per
+// MAC once a launch fills the chip (no in-cycle normalisation, 3 waves/SIMD:
+// profiles/r01_modexp_group_sweep_*); a launch that cannot fill it runs with
+// more lanes per instance (L = 9) for lower latency: the largest G whose lanes
+// still fit the resident-wave capacity.  G = 2 (2048-bit) / 4 (4096-bit) only
+// when forced.
 // ModexpArgs.group or FSDKR_MODEXP_G=<G> force a group size (tuning, tests).
-static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int> allowed) {
+static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int> allowed, int min_auto) {
   static int forced_env = -1;
   if (forced_env < 0) {
     const char* e = getenv("FSDKR_MODEXP_G");
@@ -236,29 +238,29 @@ static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int>
   for (int g : allowed)
     if (g == forced) return g;
   constexpr uint64_t kLaneCapacity = 256ull * 4 * 3 * 64;   // CUs x SIMDs x resident waves x lanes
-  int best = *allowed.begin();
+  int best = min_auto;
   for (int g : allowed)
-    if ((uint64_t)count * (uint64_t)g <= kLaneCapacity) best = g;
+    if (g > best && (uint64_t)count * (uint64_t)g <= kLaneCapacity) best = g;
   return best;
 }
 
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
   switch (k32) {
     case 64:
-      switch (pick_group(a.count, (int)a.group, {2, 4, 8})) {
+      switch (pick_group(a.count, (int)a.group, {2, 4, 8}, 4)) {
         case 8: return launch_modexp<72, 8, 64>(a, st);
         case 4: return launch_modexp<72, 4, 64>(a, st);
         default: return launch_modexp<72, 2, 64>(a, st);
       }
     case 96: return launch_modexp<108, 4, 96>(a, st);
     case 128:
-      switch (pick_group(a.count, (int)a.group, {4, 8, 16})) {
+      switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 8)) {
         case 16: return launch_modexp<144, 16, 128>(a, st);
         case 8: return launch_modexp<144, 8, 128>(a, st);
         default: return launch_modexp<144, 4, 128>(a, st);
       }
     case 192:
-      return pick_group(a.count, (int)a.group, {4, 8}) == 8 ? launch_modexp<216, 8, 192>(a, st)
+      return pick_group(a.count, (int)a.group, {4, 8}, 4) == 8 ? launch_modexp<216, 8, 192>(a, st)
                                                             : launch_modexp<216, 4, 192>(a, st);
     default: return hipErrorInvalidValue;
   }

@@ -143,13 +143,29 @@ def _mask(key_len, seed):
     return sum(H(seed, j) << (256 * j) for j in range(msklen))
 
 
-def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256):
+def synth_collect_tiled(ctx, R, t, seed, unique, key_bits=2048, M=256):
+    """A collect() batch of R refresh messages (no joins) over n = R receivers
+    built from `unique` distinct messages: message k is a copy of message
+    k mod unique under party index k+1.  Every copy is a valid message (its
+    proofs are for the same receivers) and the verifier recomputes every pair
+    independently, so the verification work equals that of R distinct
+    messages; only the prover-side generation (CPU/GPU minutes at n = 256) is
+    saved.  Used for the n = 256 measurement (BASELINE configs[3])."""
+    import dataclasses
+    msgs, joins, lk = synth_collect(ctx, unique, 0, t, seed, key_bits, M, n_recv=R)
+    tiled = [dataclasses.replace(msgs[k % unique], party_index=k + 1, old_party_index=k + 1) for k in range(R)]
+    return tiled, joins, lk
+
+
+def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
     """Messages for one collect() with R refresh and J join messages (n = R+J
-    receivers): returns (refresh_messages, join_messages, local_key of party 1).
-    Party k (1-based) of the refresh set has party_index = old_party_index = k;
-    joiners take indices R+1..n (the replace() layout)."""
+    receivers, or n_recv when J = 0): returns (refresh_messages,
+    join_messages, local_key of party 1).  Party k (1-based) of the refresh set
+    has party_index = old_party_index = k; joiners take indices R+1..n (the
+    replace() layout)."""
     rnd = random.Random(seed)
-    n = R + J
+    assert n_recv is None or J == 0
+    n = n_recv or (R + J)
     Mt = R + J
     nk = 2 * n + 2 * Mt                     # receivers: Paillier + N~; messages: new ek + RP key
     kp = _keypairs(gen_primes(ctx, 2 * nk, key_bits // 2, rnd))
