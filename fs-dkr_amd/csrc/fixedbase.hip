@@ -37,9 +37,9 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   const int li = threadIdx.x / G;
   const uint32_t b = blockIdx.x * IPB + li;
   if (b >= a.count) return;
-  // the table chain heads the fixed-base pipeline: its waves win issue
-  // arbitration over throughput launches (below the 4096-bit chains, level 3)
-  __builtin_amdgcn_s_setprio(2);
+  // the table chain heads the fixed-base pipeline (the h2 chain is 2816
+  // squarings long, as long as the 4096-bit s^N chains): few waves, top priority
+  __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* C = a.consts + (size_t)a.mod_idx[b] * STRIDE;
   MT M;
