@@ -669,15 +669,16 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   uint32_t *cons_nn = nullptr, *cons_nl = nullptr;
   if ((rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn, "collect_nn"))) return rc;
   if ((rc = setup_moduli(c, nl, PI(o_mods), n_mods_nl, &cons_nl, "collect_nl"))) return rc;
-  // ---- stream plan (seven concurrent lanes of work: give HIP >= 7 hardware queues,
+  // ---- stream plan (eight concurrent lanes of work: give HIP >= 8 hardware queues,
   //      GPU_MAX_HW_QUEUES, or streams share queues and serialise):
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
   //   side 1  : FB (fixed bases h1, h2, T: schedules, tables, exponents)
   //   side 3  : ped_hash (serial SHA-256 chains, priority)
   //   side 4  : GD (nl: correct-key, DLog; priority)
+  //   side 6  : Feldman (secp256k1 Horner per pair)
   //   st      : pdl_hash, binom x2 | fork | J5, nl inverses | join | eq, prod3, alice
   //   side 2  :                    J2 (nn, 256-bit challenges) -> nn inverses
-  //   side 5  :                    pdl_u1, Feldman (secp256k1)
+  //   side 5  :                    pdl_u1 (secp256k1)
   std::vector<hipEvent_t> done;
   auto fork = [&](hipStream_t from, hipEvent_t* ev) -> int {
     int r = c->hip_check(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event");
@@ -734,6 +735,15 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     c->mark("ped_hash", false, ss);
     if (rc || (rc = join_later(ss))) return rc;
   }
+  {  // Feldman share checks (inputs only; one Horner chain per pair)
+    hipStream_t ss = c->side_stream(6);
+    (void)hipStreamWaitEvent(ss, consts_ready, 0);
+    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
+    c->mark("ec", true, ss);
+    rc = c->hip_check(launch_feldman(f, ss), "feldman");
+    c->mark("ec", false, ss);
+    if (rc || (rc = join_later(ss))) return rc;
+  }
   {  // GD: correct-key sigma^n, DLog g^y / ni^e (2048-bit exponents, few instances)
     hipStream_t ss = c->side_stream(4);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
@@ -766,7 +776,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     c->mark("inverse", false, ss);
     if (rc || (rc = join_later(ss))) return rc;
   }
-  {  // secp256k1 checks (one thread per pair, latency-bound): Feldman + PDL u1 off the main chain
+  {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
     hipStream_t ss = c->side_stream(5);
     (void)hipStreamWaitEvent(ss, ready, 0);
     PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
@@ -774,11 +784,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     rc = c->hip_check(launch_pdl_u1(u, ss), "pdl_u1");
     c->mark("ec", false, ss);
     if (rc) return rc;
-    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
-    c->mark("ec", true, ss);
-    rc = c->hip_check(launch_feldman(f, ss), "feldman");
-    c->mark("ec", false, ss);
-    if (rc || (rc = join_later(ss))) return rc;
+    if ((rc = join_later(ss))) return rc;
   }
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
