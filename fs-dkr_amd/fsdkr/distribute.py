@@ -291,3 +291,74 @@ def distribute(old_party_index, local_key, new_n, rng=None, ctx=None, key_bits=2
                          remove_party_indices=[], public_key=local_key.y_sum_s,
                          ring_pedersen_statement=rp_st, ring_pedersen_proof=rp_pf)
     return msg, dk
+
+
+# ------------------------------------------------------------ join / replace ----
+def generate_h1_h2_n_tilde(ctx, rng, key_bits):
+    """add_party_message.rs:50-66: a fresh modulus N~ with h2 = h1^xhi, returns
+    (N~, h1, h2, xhi, xhi_inv) with the reference's final negation mod phi."""
+    ek, dk = keypair_with_modulus_size(ctx, rng, key_bits)
+    phi = (dk.p - 1) * (dk.q - 1)
+    h1 = rng.sample_below(ek.n)
+    while True:
+        xhi = rng.sample_below(phi)
+        if math.gcd(xhi, phi) == 1:
+            xhi_inv = pow(xhi, -1, phi)
+            break
+    h2 = ctx.modexp_batch([h1], [xhi], [ek.n], [0], _width(ek.n.bit_length()))[0]
+    return ek.n, h1, h2, phi - xhi, phi - xhi_inv
+
+
+def join_distribute(rng=None, ctx=None, key_bits=2048, m_security=256):
+    """JoinMessage::distribute (add_party_message.rs:101-124) -> (JoinMessage, Keys)."""
+    from .types import DLogStatement, JoinMessage, Keys
+    ctx = _ctx(ctx)
+    rng = rng or SystemRng()
+    ek, dk = keypair_with_modulus_size(ctx, rng, key_bits)
+    Nt, h1, h2, xhi, xhi_inv = generate_h1_h2_n_tilde(ctx, rng, key_bits)
+    st1, st2 = DLogStatement(Nt, h1, h2), DLogStatement(Nt, h2, h1)
+    # the draws of the two composite proofs come one proof at a time in the reference
+    p1 = _one_dlog_proof(ctx, rng, st1, xhi)
+    p2 = _one_dlog_proof(ctx, rng, st2, xhi_inv)
+    rp_st, rp_pf = ring_pedersen_generate_and_prove(ctx, rng, key_bits, m_security)
+    msg = JoinMessage(ek=ek, dk_correctness_proof=correct_key_proof(ctx, dk), party_index=None, dlog_statement=st1,
+                      composite_dlog_proof_base_h1=p1, composite_dlog_proof_base_h2=p2,
+                      ring_pedersen_statement=rp_st, ring_pedersen_proof=rp_pf)
+    return msg, Keys(ek, dk)
+
+
+def _one_dlog_proof(ctx, rng, st, secret):
+    from .types import CompositeDLogProof
+    r = rng.sample_below((1 << (128 + 128 + 256)) * st.N)
+    x = ctx.modexp_batch([st.g], [r], [st.N], [0], _width(st.N.bit_length()))[0]
+    return CompositeDLogProof(x, r + chain_bigint(x, st.g, st.N, st.ni) * secret)
+
+
+def replace(join_messages, local_key, old_to_new, new_n, rng=None, ctx=None, key_bits=2048, m_security=256):
+    """RefreshMessage::replace (refresh_message.rs:239-319): re-index the
+    existing parties' keys by `old_to_new`, insert the joiners' keys, then
+    distribute() under the party's new index.  The reference walks a HashMap
+    (unspecified order); new indices are applied in ascending order here."""
+    current_len = len(local_key.paillier_key_vec)
+    remap = {old_to_new[old]: (local_key.paillier_key_vec[old - 1], local_key.h1_h2_n_tilde_vec[old - 1])
+             for old in old_to_new}
+    for new in sorted(remap):
+        if new <= current_len:
+            local_key.paillier_key_vec[new - 1], local_key.h1_h2_n_tilde_vec[new - 1] = remap[new]
+        else:
+            local_key.paillier_key_vec.insert(new - 1, remap[new][0])
+            local_key.h1_h2_n_tilde_vec.insert(new - 1, remap[new][1])
+    for jm in join_messages:
+        if jm.party_index is None:
+            raise FsDkrError("NewPartyUnassignedIndexError")
+        pi = jm.party_index
+        if pi <= current_len:
+            local_key.paillier_key_vec[pi - 1] = jm.ek
+            local_key.h1_h2_n_tilde_vec[pi - 1] = jm.dlog_statement
+        else:
+            local_key.paillier_key_vec.insert(pi - 1, jm.ek)
+            local_key.h1_h2_n_tilde_vec.insert(pi - 1, jm.dlog_statement)
+    old_party_index = local_key.i
+    local_key.i = old_to_new[local_key.i]
+    local_key.n = new_n
+    return distribute(old_party_index, local_key, new_n, rng, ctx, key_bits, m_security)

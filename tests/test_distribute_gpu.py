@@ -53,3 +53,37 @@ def test_distribute_chosen_randomness_and_errors(gpu_ctx):
     assert mg.points_encrypted_vec == mo.points_encrypted_vec
     with pytest.raises(refresh.FsDkrPanic):           # assert!(t <= new_n / 2), refresh_message.rs:56
         distribute.distribute(1, keys[0].clone(), 1, Rng("x"), ctx=gpu_ctx, key_bits=1024)
+
+
+def test_join_distribute_and_replace_match_oracle(gpu_ctx):
+    """JoinMessage::distribute (add_party_message.rs:101-124) and
+    RefreshMessage::replace (refresh_message.rs:239-319) against the oracle,
+    then the GPU-made messages through RefreshMessage::collect (an old party)
+    and JoinMessage::collect (the joiner) on the GPU."""
+    from fsdkr import distribute, join, refresh
+    kb, t, n = 1024, 1, 4
+    all_keys = protocol.simulate_keygen(t, n, Rng("jd-keys"), kb)
+    jo, jko = protocol.join_distribute(Rng("jd"), kb)
+    jg, jkg = distribute.join_distribute(Rng("jd"), ctx=gpu_ctx, key_bits=kb)
+    assert codec.enc(jg) == codec.enc(jo)
+    assert (jkg.dk.p, jkg.dk.q) == (jko.dk.p, jko.dk.q)
+    jg.party_index = 4
+    old_to_new = {1: 1, 2: 2, 3: 3}
+    msgs, dks, keys = [], [], []
+    for key in all_keys[:3]:
+        ko, kg = key.clone(), key.clone()
+        jo2 = copy.deepcopy(jo)
+        jo2.set_party_index(4)
+        mo, dko = protocol.replace([jo2], ko, old_to_new, n, Rng(f"rep-{key.i}"), kb)
+        mg, dkg = distribute.replace([jg], kg, old_to_new, n, Rng(f"rep-{key.i}"), ctx=gpu_ctx, key_bits=kb)
+        assert codec.enc(mg) == codec.enc(mo)
+        assert [e.n for e in kg.paillier_key_vec] == [e.n for e in ko.paillier_key_vec]
+        msgs.append(mg)
+        dks.append(dkg)
+        keys.append(kg)
+    k1 = keys[1]
+    refresh.collect(copy.deepcopy(msgs), k1, dks[1], [copy.deepcopy(jg)], ctx=gpu_ctx, key_bits=kb)
+    lk = join.collect(jg, copy.deepcopy(msgs), jkg, [], t, n, ctx=gpu_ctx)
+    assert lk.i == 4 and lk.y_sum_s == msgs[0].public_key
+    # both ends of the refresh agree on the joiner's public share
+    assert k1.pk_vec[3] == lk.pk_vec[3]
