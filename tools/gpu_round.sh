@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-# collect() runs 7 concurrent streams; rocprofv3's preload initialises HIP before
+# collect() runs 8 concurrent streams; rocprofv3's preload initialises HIP before
 # bench.py can set this, so export it here (bench.py/conftest set it otherwise)
 export GPU_MAX_HW_QUEUES=8
 for step in "$@"; do
