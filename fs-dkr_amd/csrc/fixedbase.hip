@@ -35,7 +35,7 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
-  const uint32_t b = blockIdx.x * IPB + li;
+  const uint32_t b = blockIdx.x * (blockDim.x / G) + li;   // few bases: one wave per block
   if (b >= a.count) return;
   // the table chain heads the fixed-base pipeline (the h2 chain is 2816
   // squarings long, as long as the 4096-bit s^N chains): few waves, top priority
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(BLOCK) void fb_exp_kernel(const FbExpArgs a) {
   __shared__ uint32_t lds[2 * IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
-  const uint32_t inst = blockIdx.x * IPB + li;
+  const uint32_t inst = blockIdx.x * (blockDim.x / G) + li;
   if (inst >= a.count) return;
   uint32_t* stream = lds + li * KD;             // streamed operand of each product
   uint32_t* abuf = lds + (IPB + li) * KD;       // accumulator A
@@ -196,16 +196,19 @@ __global__ __launch_bounds__(BLOCK) void fb_exp_kernel(const FbExpArgs a) {
 }
 
 // ---- launchers ------------------------------------------------------------------
+// launches with fewer waves than SIMDs: one wave per block (see modexp.hip)
+static inline uint32_t fb_block_threads(uint32_t lanes) { return lanes <= 256u * 4u * 64u ? 64u : (uint32_t)BLOCK; }
+
 template <int KD, int G, int K32>
 static hipError_t table_launch(const FbTableArgs& a, hipStream_t st) {
-  constexpr int IPB = BLOCK / G;
-  hipLaunchKernelGGL((fb_table_kernel<KD, G, K32>), dim3((a.count + IPB - 1) / IPB), dim3(BLOCK), 0, st, a);
+  const uint32_t bs = fb_block_threads(a.count * G), ipb = bs / G;
+  hipLaunchKernelGGL((fb_table_kernel<KD, G, K32>), dim3((a.count + ipb - 1) / ipb), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 template <int KD, int G, int K32>
 static hipError_t exp_launch(const FbExpArgs& a, hipStream_t st) {
-  constexpr int IPB = BLOCK / G;
-  hipLaunchKernelGGL((fb_exp_kernel<KD, G, K32>), dim3((a.count + IPB - 1) / IPB), dim3(BLOCK), 0, st, a);
+  const uint32_t bs = fb_block_threads(a.count * G), ipb = bs / G;
+  hipLaunchKernelGGL((fb_exp_kernel<KD, G, K32>), dim3((a.count + ipb - 1) / ipb), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
-  const uint32_t inst = blockIdx.x * IPB + li;
+  const uint32_t inst = blockIdx.x * (blockDim.x / G) + li;   // blocks of BLOCK or 64 threads (small launches)
   if (inst >= a.count) return;
   // a latency-critical launch sharing the chip with throughput launches on other
   // streams: its waves win the SIMD issue arbitration
@@ -192,12 +192,19 @@ static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* c
   hipLaunchKernelGGL((mod_setup_kernel<KD, G, K32>), dim3(blocks), dim3(BLOCK), 0, st, mods, n_mod, consts);
   return hipGetLastError();
 }
+// A launch with fewer waves than the chip has SIMDs runs one wave per block,
+// so the dispatcher can give every wave its own SIMD (a latency-bound chain
+// sharing a SIMD with another wave runs up to 2x slower).
+constexpr uint32_t kSmallLaunchLanes = 256u * 4u * 64u;
+static inline uint32_t block_threads(uint32_t lanes) { return lanes <= kSmallLaunchLanes ? 64u : (uint32_t)BLOCK; }
+
 template <int KD, int G, int K32>
 static hipError_t launch_modexp(const ModexpArgs& a, hipStream_t st) {
-  constexpr int IPB = BLOCK / G;
-  const uint32_t blocks = (a.count + IPB - 1) / IPB;
+  const uint32_t bs = block_threads(a.count * G);
+  const uint32_t ipb = bs / G;
+  const uint32_t blocks = (a.count + ipb - 1) / ipb;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((modexp_kernel<KD, G, K32>), dim3(blocks), dim3(BLOCK), 0, st, a);
+  hipLaunchKernelGGL((modexp_kernel<KD, G, K32>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
