@@ -10,6 +10,7 @@
 //   -> alice_hash, pdl_u1, feldman -> one D2H copy of the verdict words.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -680,6 +681,14 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   //   side 2  :                    J2 (nn, 256-bit challenges) -> nn inverses
   //   side 5  :                    pdl_u1 (secp256k1)
   std::vector<hipEvent_t> done;
+  // issue-priority levels of the serial chains (tuning knob FSDKR_PRIO="GA,FB,GD,J5";
+  // measured defaults)
+  static const uint32_t* prio = [] {
+    static uint32_t p[4] = {3, 3, 2, 1};
+    if (const char* e = getenv("FSDKR_PRIO")) sscanf(e, "%u,%u,%u,%u", &p[0], &p[1], &p[2], &p[3]);
+    return p;
+  }();
+  pl.fb.table_prio = prio[1];
   auto fork = [&](hipStream_t from, hipEvent_t* ev) -> int {
     int r = c->hip_check(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event");
     if (!r) (void)hipEventRecord(*ev, from);
@@ -719,7 +728,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     for (uint32_t g : {16u})
       if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
     if (ga_forced) ga_group = ga_forced;
-    if ((rc = launch_group(0, ss, 3, ga_group)) || (rc = join_later(ss))) return rc;
+    if ((rc = launch_group(0, ss, prio[0], ga_group)) || (rc = join_later(ss))) return rc;
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);
@@ -747,7 +756,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   {  // GD: correct-key sigma^n, DLog g^y / ni^e (2048-bit exponents, few instances)
     hipStream_t ss = c->side_stream(4);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    if ((rc = launch_group(1, ss, 2, 0)) || (rc = join_later(ss))) return rc;
+    if ((rc = launch_group(1, ss, prio[2], 0)) || (rc = join_later(ss))) return rc;
   }
   // (2) PDL challenges, then the jobs that exponentiate by them
   {
@@ -788,7 +797,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   }
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
-  if ((rc = launch_group(3, st, 1, 8))) return rc;   // J5: z^e (2048-bit, 256-bit challenges)
+  if ((rc = launch_group(3, st, prio[3], 8))) return rc;   // J5: z^e (2048-bit, 256-bit challenges)
   {
     InverseArgs b1{(const uint64_t*)(dev + d_iynl), (const uint64_t*)(dev + d_imnl), PX(x_invz), PX(x_uzA),
                    nullptr, P};

@@ -16,6 +16,7 @@ namespace fsdkr {
 
 struct FbJob {
   uint32_t k32 = 0;
+  uint32_t table_prio = 3;   // s_setprio of the table chain (a long serial chain, few waves)
   // bases
   std::vector<uint64_t> b_ptr;
   std::vector<uint32_t> b_len, b_mod, b_bits;

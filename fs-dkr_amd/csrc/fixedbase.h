@@ -19,6 +19,7 @@ struct FbTableArgs {            // table[toff[b] + j] = base_b^(2^(w j)) * R mod
   uint32_t* table;              // [sum h][KD] digits
   uint32_t w;
   uint32_t count;
+  uint32_t prio;                // s_setprio level of the chain's waves
 };
 
 struct FbSchedArgs {            // per-instance BGMW product schedule

@@ -39,7 +39,9 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   if (b >= a.count) return;
   // the table chain heads the fixed-base pipeline (the h2 chain is 2816
   // squarings long, as long as the 4096-bit s^N chains): few waves, top priority
-  __builtin_amdgcn_s_setprio(3);
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* C = a.consts + (size_t)a.mod_idx[b] * STRIDE;
   MT M;

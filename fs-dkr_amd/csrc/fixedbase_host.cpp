@@ -25,7 +25,7 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(I + o); };
   FbTableArgs ta{U64(j.off.b_ptr), U32(j.off.b_len), U32(j.off.b_mod), U32(j.off.b_toff), U32(j.off.b_h),
-                 consts, d.table, j.w, (uint32_t)j.bases()};
+                 consts, d.table, j.w, (uint32_t)j.bases(), j.table_prio};
   FbSchedArgs sa{U64(j.off.e_ptr), U32(j.off.e_len), U32(j.off.i_h), d.sched, d.nsteps, j.stride, j.w,
                  (uint32_t)j.count()};
   FbExpArgs ea{U32(j.off.i_toff), U32(j.off.e_mod), U64(j.off.o_ptr), consts, d.table, d.sched, d.nsteps, j.stride,
