@@ -6,6 +6,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -71,10 +72,45 @@ void Ctx::tend(size_t idx, hipStream_t st) {
   pending[idx].e1 = ev;
 }
 
+std::vector<uint32_t> Ctx::cu_mask(bool reserved) const {
+  int ncu = 0;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  if (ncu <= 0) ncu = 256;
+  std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+  std::vector<bool> res(ncu, false);
+  // R/8 CUs per XCD.  Bit i = 32 j + (j + s (32/per)) mod 32 is balanced over the 8
+  // XCDs whether the driver maps mask bits to XCDs contiguously (i / 32) or
+  // interleaved (i mod 8).
+  const uint32_t per = reserve_cus / 8;
+  if (ncu == 256 && per)
+    for (uint32_t j = 0; j < 8; ++j)
+      for (uint32_t s = 0; s < per; ++s) res[32 * j + (j + s * (32 / per)) % 32] = true;
+  for (int i = 0; i < ncu; ++i)
+    if (res[i] == reserved) m[i / 32] |= 1u << (i % 32);
+  return m;
+}
+
+static hipStream_t make_stream(const Ctx* c, int masked /* 0 none, 1 reserved, 2 complement */) {
+  hipStream_t s = nullptr;
+  if (masked) {
+    std::vector<uint32_t> m = c->cu_mask(masked == 1);
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()) == hipSuccess) return s;
+    s = nullptr;
+  }
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+  return s;
+}
+
 hipStream_t Ctx::side_stream(int k) {
   k %= NSIDE;
-  if (!side[k] && hipStreamCreateWithFlags(&side[k], hipStreamNonBlocking) != hipSuccess) side[k] = nullptr;
+  if (!side[k]) side[k] = make_stream(this, (reserve_cus && reserve_excl) ? 2 : 0);
   return side[k] ? side[k] : stream;
+}
+
+hipStream_t Ctx::crit_stream() {
+  if (!reserve_cus) return nullptr;
+  if (!crit) crit = make_stream(this, 1);
+  return crit;
 }
 
 int Ctx::sync() {
@@ -265,6 +301,11 @@ int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out) {
   }
   c->device = dev;
   c->timing = cfg && (cfg->flags & FSDKR_CFG_TIMING);
+  if (const char* e = getenv("FSDKR_RESERVE_CUS")) {
+    const int r = atoi(e);
+    c->reserve_cus = (r > 0 && r % 8 == 0 && r <= 128) ? (uint32_t)r : 0u;
+  }
+  if (const char* e = getenv("FSDKR_RESERVE_EXCL")) c->reserve_excl = atoi(e) != 0;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return FSDKR_E_HIP;
@@ -281,6 +322,7 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
     if (kv.second.ptr) (void)hipFree(kv.second.ptr);
   for (auto& sd : c->side)
     if (sd) (void)hipStreamDestroy(sd);
+  if (c->crit) (void)hipStreamDestroy(c->crit);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   fsdkr::free_collect_plan(c);
   delete c;
@@ -296,6 +338,14 @@ int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes) {
   if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16)) return FSDKR_E_ARG;
   c->modexp_group = lanes;
   return FSDKR_OK;
+}
+
+int fsdkr_ctx_set_timing(fsdkr_ctx* ctx, int on) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  int rc = c->sync();   // fold events of launches made under the old setting
+  c->timing = on != 0;
+  return rc;
 }
 
 int fsdkr_mod_inverse(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* y, const uint32_t* m,

@@ -683,11 +683,9 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   std::vector<hipEvent_t> done;
   // issue-priority levels of the serial chains (tuning knob FSDKR_PRIO="GA,FB,GD,J5";
   // measured defaults)
-  static const uint32_t* prio = [] {
-    static uint32_t p[4] = {3, 3, 2, 1};
-    if (const char* e = getenv("FSDKR_PRIO")) sscanf(e, "%u,%u,%u,%u", &p[0], &p[1], &p[2], &p[3]);
-    return p;
-  }();
+  // (knobs are read per call so one process can A/B them: tools/ab_collect.py)
+  uint32_t prio[4] = {3, 3, 2, 1};
+  if (const char* e = getenv("FSDKR_PRIO")) sscanf(e, "%u,%u,%u,%u", &prio[0], &prio[1], &prio[2], &prio[3]);
   pl.fb.table_prio = prio[1];
   auto fork = [&](hipStream_t from, hipEvent_t* ev) -> int {
     int r = c->hip_check(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event");
@@ -710,6 +708,14 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
                               tags[k], prio, group);
   };
+  // GA-first ordering (tuning knob FSDKR_GA_FIRST, bit mask): the throughput jobs
+  // fb_exp (1), J2 (2) and J5 (4) wait for GA, so GA's ~1 wave per SIMD runs beside
+  // only the few-wave chains
+  const uint32_t ga_first = [] {
+    const char* e = getenv("FSDKR_GA_FIRST");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  hipEvent_t ga_done = nullptr;
   // (1) chains that need only the inputs and the moduli constants start at once
   hipEvent_t consts_ready;
   if ((rc = fork(st, &consts_ready))) return rc;
@@ -720,7 +726,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     // the largest group that keeps it within about half the resident lanes
     // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); few instances
     // (multi-GPU shards) get 16 lanes for latency.  FSDKR_COLLECT_GA_G overrides.
-    static const uint32_t ga_forced = [] {
+    const uint32_t ga_forced = [] {
       const char* e = getenv("FSDKR_COLLECT_GA_G");
       return e ? (uint32_t)atoi(e) : 0u;
     }();
@@ -729,12 +735,19 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
       if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
     if (ga_forced) ga_group = ga_forced;
     if ((rc = launch_group(0, ss, prio[0], ga_group)) || (rc = join_later(ss))) return rc;
+    if (ga_first && (rc = fork(ss, &ga_done))) return rc;
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
     FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps};
-    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect")) || (rc = join_later(ss))) return rc;
+    // the table chains (thousands of dependent squarings, few waves) run on the
+    // reserved CUs when FSDKR_RESERVE_CUS is set
+    hipStream_t ts = c->crit_stream();
+    if (ts) (void)hipStreamWaitEvent(ts, consts_ready, 0);
+    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, (ga_first & 1) ? ga_done : nullptr)) ||
+        (rc = join_later(ss)))
+      return rc;
   }
   {  // ring-Pedersen challenges: one serial SHA-256 chain per message, needed only by the final checks
     hipStream_t ss = c->side_stream(3);
@@ -777,6 +790,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
+    if (ga_first & 2) (void)hipStreamWaitEvent(ss, ga_done, 0);
     if ((rc = launch_group(2, ss, 0, 8))) return rc;
     InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
                   nullptr, pl.n_inv_nn};
@@ -797,18 +811,30 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   }
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
-  if ((rc = launch_group(3, st, prio[3], 8))) return rc;   // J5: z^e (2048-bit, 256-bit challenges)
-  {
+  {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses; a side stream when CUs are
+     // reserved (the main stream is unmasked), else the main stream
+    hipStream_t js = st;
+    if (c->reserve_cus) {
+      js = c->side_stream(7);
+      hipEvent_t r2;
+      if ((rc = fork(st, &r2))) return rc;
+      (void)hipStreamWaitEvent(js, r2, 0);
+      (void)hipEventDestroy(r2);
+    }
+    if (ga_first & 4) (void)hipStreamWaitEvent(js, ga_done, 0);
+    if ((rc = launch_group(3, js, prio[3], 8))) return rc;
     InverseArgs b1{(const uint64_t*)(dev + d_iynl), (const uint64_t*)(dev + d_imnl), PX(x_invz), PX(x_uzA),
                    nullptr, P};
-    c->mark("inverse", true);
-    rc = c->hip_check(launch_inverse(nl, b1, st), "inverse nl");
-    c->mark("inverse", false);
+    c->mark("inverse", true, js);
+    rc = c->hip_check(launch_inverse(nl, b1, js), "inverse nl");
+    c->mark("inverse", false, js);
     if (rc) return rc;
     InverseArgs b2{(const uint64_t*)(dev + d_iynl) + P, (const uint64_t*)(dev + d_imnl) + P, nullptr, PX(x_uzp),
                    nullptr, P};
-    if ((rc = c->hip_check(launch_inverse(nl, b2, st), "inverse nl 2"))) return rc;
+    if ((rc = c->hip_check(launch_inverse(nl, b2, js), "inverse nl 2"))) return rc;
+    if (js != st && (rc = join_later(js))) return rc;
   }
+  if (ga_done) (void)hipEventDestroy(ga_done);
   for (hipEvent_t ev : done) {
     (void)hipStreamWaitEvent(st, ev, 0);
     (void)hipEventDestroy(ev);

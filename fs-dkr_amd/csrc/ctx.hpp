@@ -51,6 +51,17 @@ struct Ctx {
   size_t last_mark = (size_t)-1;
   uint32_t modexp_group = 0;   // lanes per modexp instance (0 = by batch size)
   hipStream_t side_stream(int k);
+  // CU reservation for latency-critical serial chains (FSDKR_RESERVE_CUS = R, a
+  // multiple of 8): crit_stream() runs on R CUs spread evenly over the 8 XCDs and
+  // every side stream on the complement, so a chain of dependent products (the
+  // fixed-base table squarings) never shares a CU with the throughput jobs.
+  // 0 = no reservation (crit_stream() returns nullptr: run on the caller's stream).
+  uint32_t reserve_cus = 0;
+  bool reserve_excl = true;   // side streams on the complement (false: unmasked)
+  hipStream_t crit = nullptr;
+  hipStream_t crit_stream();
+  // CU mask words of the reserved set (reserved = true) or of its complement
+  std::vector<uint32_t> cu_mask(bool reserved) const;
   // synchronise the stream and fold pending events into `times`
   int sync();
 };

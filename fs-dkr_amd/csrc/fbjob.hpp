@@ -110,7 +110,10 @@ struct FbDev {
 
 // table, schedule and exponent kernels; `st_table` may differ from `st` (the
 // schedule kernel runs beside the table chain), the exponent kernel waits for both.
-int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag);
+// table_st: stream of the table chain (nullptr = st); st waits for it (and for
+// exp_wait, if given) before fb_exp
+int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
+              hipStream_t table_st = nullptr, hipEvent_t exp_wait = nullptr);
 // upload + launch + wait (stand-alone callers)
 int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag);
 

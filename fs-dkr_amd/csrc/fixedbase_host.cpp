@@ -19,7 +19,8 @@ static int fb_group(Ctx* c, size_t count) {
   return count * 8 <= kLaneCapacity ? 8 : 4;
 }
 
-int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag) {
+int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
+              hipStream_t table_st, hipEvent_t exp_wait) {
   if (j.count() == 0) return FSDKR_OK;
   const uint8_t* I = d.img;
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
@@ -32,10 +33,20 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
                (uint32_t)j.count()};
   int rc;
   if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
-  size_t m = c->tbeg("fb_table", st);
-  rc = c->hip_check(launch_fb_table(j.k32, ta, st), "fb_table launch");
-  c->tend(m, st);
+  // the table chain may run on its own (CU-reserved) stream; the exponent kernel waits for it
+  hipStream_t ts = table_st ? table_st : st;
+  size_t m = c->tbeg("fb_table", ts);
+  rc = c->hip_check(launch_fb_table(j.k32, ta, ts), "fb_table launch");
+  c->tend(m, ts);
   if (rc) return rc;
+  if (exp_wait) (void)hipStreamWaitEvent(st, exp_wait, 0);
+  if (ts != st) {
+    hipEvent_t ev;
+    if ((rc = c->hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "event"))) return rc;
+    (void)hipEventRecord(ev, ts);
+    (void)hipStreamWaitEvent(st, ev, 0);
+    (void)hipEventDestroy(ev);
+  }
   m = c->tbeg("fb_exp", st);
   rc = c->hip_check(launch_fb_exp(j.k32, ea, fb_group(c, j.count()), st), tag);
   c->tend(m, st);

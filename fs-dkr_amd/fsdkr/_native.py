@@ -100,6 +100,8 @@ def lib():
     L.fsdkr_paillier_encrypt.restype = ctypes.c_int
     L.fsdkr_ctx_set_modexp_group.argtypes = [vp, ctypes.c_uint32]
     L.fsdkr_ctx_set_modexp_group.restype = ctypes.c_int
+    L.fsdkr_ctx_set_timing.argtypes = [vp, ctypes.c_int]
+    L.fsdkr_ctx_set_timing.restype = ctypes.c_int
     L.fsdkr_mod_inverse.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p]
     L.fsdkr_mod_inverse.restype = ctypes.c_int
     L.fsdkr_ec_msm.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
@@ -216,6 +218,10 @@ class Context:
     def set_modexp_group(self, lanes):
         """Force the lanes per modexp instance (0 = automatic)."""
         self.check(self._lib.fsdkr_ctx_set_modexp_group(self._h, lanes))
+
+    def set_timing(self, on):
+        """Per-kernel HIP-event timing on/off (kernel_time needs it on)."""
+        self.check(self._lib.fsdkr_ctx_set_timing(self._h, 1 if on else 0))
 
     def mod_inverse(self, ys, ms, mod_limbs):
         """[(y^-1 mod m or None)] on the GPU (None where gcd(y, m) != 1)."""

@@ -51,6 +51,10 @@ const char* fsdkr_last_error(const fsdkr_ctx* ctx);
 /* Lanes cooperating on one modexp instance (2, 4, 8, 16; unsupported values
  * for a width fall back to the automatic choice); 0 = choose by batch size. */
 int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes);
+/* Switch per-kernel HIP-event timing (FSDKR_CFG_TIMING) on or off after
+ * creation.  The events cost ~9 ms per n = 64 collect (eight streams, one
+ * event pair per launch), so timed benchmark regions run with it off. */
+int fsdkr_ctx_set_timing(fsdkr_ctx* ctx, int on);
 /* 1 if the shared library was built with gfx950 kernels and a device is present. */
 int fsdkr_device_available(void);
 
