@@ -30,6 +30,9 @@
 namespace fsdkr {
 
 constexpr uint32_t M29 = (1u << 29) - 1;
+#ifndef FSDKR_ROW_FENCE_MIN_L
+#define FSDKR_ROW_FENCE_MIN_L 12
+#endif
 
 // ---- intra-group DPP helpers --------------------------------------------------
 // G <= 4: quad_perm inside one DPP quad.  G = 8/16: row_shr/row_shl:1 inside a
@@ -112,6 +115,11 @@ struct Mont29 {
   // for L <= 24 it cannot reach 2^64 before it moves on, so only the final carry
   // passes of mul() are needed.  Longer lanes normalise every NSTEP rows.
   static constexpr bool NORM_IN_CYCLE = L > 24;
+  // Scheduling fence at the end of each row.  Long lanes (throughput shapes,
+  // 3 waves/SIMD) need it to hold VGPRs down; short lanes (latency shapes, one
+  // wave per SIMD) drop it so the next row's a*b products can fill the m-digit
+  // dependency chain (v_mul_lo -> DPP broadcast -> m*n[0] -> carry).
+  static constexpr bool ROW_FENCE = L > FSDKR_ROW_FENCE_MIN_L;
 
   uint32_t n[L];
   uint32_t ninv;      // -N^-1 mod 2^29
@@ -169,7 +177,7 @@ struct Mont29 {
     acc[s1] += acc[s0] >> 29;
     acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0] & M29) & m_top);
     if constexpr (NORM_IN_CYCLE && (((R + 1) % NSTEP == 0) || (R + 1 == L))) norm_step<(R + 1) % L>(acc);
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ROW_FENCE) __builtin_amdgcn_sched_barrier(0);
   }
 
   template <int... Rs>

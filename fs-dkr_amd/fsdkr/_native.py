@@ -8,7 +8,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfsdkr.so")
+# FSDKR_LIB: alternative build of the same library (A/B timing tools only)
+LIB_PATH = os.environ.get("FSDKR_LIB") or os.path.join(_HERE, "libfsdkr.so")
 
 FSDKR_OK = 0
 FSDKR_E_ARG = -1
