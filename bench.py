@@ -20,11 +20,11 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
-# collect() runs eight concurrent streams (csrc/collect.cpp stream plan); with
+# collect() runs up to eleven concurrent streams (csrc/collect.cpp stream plan); with
 # HIP's default of 4 hardware queues per process (exported as 4 on the GPU
-# boxes) four of them would share queues and serialise.  Raise it (never
+# boxes) several of them would share queues and serialise.  Raise it (never
 # lower it) before the HIP runtime initialises.
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 import numpy as np  # noqa: E402
 

@@ -670,10 +670,12 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   uint32_t *cons_nn = nullptr, *cons_nl = nullptr;
   if ((rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn, "collect_nn"))) return rc;
   if ((rc = setup_moduli(c, nl, PI(o_mods), n_mods_nl, &cons_nl, "collect_nl"))) return rc;
-  // ---- stream plan (eight concurrent lanes of work: give HIP >= 8 hardware queues,
-  //      GPU_MAX_HW_QUEUES, or streams share queues and serialise):
+  // ---- stream plan (up to eleven concurrent lanes of work: give HIP >= 12 hardware
+  //      queues, GPU_MAX_HW_QUEUES, or streams share queues and serialise):
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
-  //   side 1  : FB (fixed bases h1, h2, T: schedules, tables, exponents)
+  //   side 8  : FB table chains (h1, h2, T: the longest dependent chain), top priority
+  //   side 1  : FB schedules, then (after the tables) fixed-base exponents
+  //   side 7  : J5 + nl inverses instead of st when CUs are reserved (FSDKR_RESERVE_CUS)
   //   side 3  : ped_hash (serial SHA-256 chains, priority)
   //   side 4  : GD (nl: correct-key, DLog; priority)
   //   side 6  : Feldman (secp256k1 Horner per pair)
@@ -734,6 +736,10 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     for (uint32_t g : {16u})
       if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
     if (ga_forced) ga_group = ga_forced;
+    // small batches (multi-GPU shards): the h2 fixed-base table chain (2816
+    // dependent squarings) is the critical path, so GA steps down one issue
+    // priority level below it (8-way shard: 33.4 -> 31.7 ms, tools/ab_hwq.sh)
+    if (ga_group == 16 && !getenv("FSDKR_PRIO")) prio[0] = 2;
     if ((rc = launch_group(0, ss, prio[0], ga_group)) || (rc = join_later(ss))) return rc;
     if (ga_first && (rc = fork(ss, &ga_done))) return rc;
   }
@@ -744,7 +750,8 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     // the table chains (thousands of dependent squarings, few waves) run on the
     // reserved CUs when FSDKR_RESERVE_CUS is set
     hipStream_t ts = c->crit_stream();
-    if (ts) (void)hipStreamWaitEvent(ts, consts_ready, 0);
+    if (!ts) ts = c->side_stream(8);   // own stream: the chain starts beside fb_sched
+    (void)hipStreamWaitEvent(ts, consts_ready, 0);
     if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, (ga_first & 1) ? ga_done : nullptr)) ||
         (rc = join_later(ss)))
       return rc;

@@ -34,7 +34,7 @@ struct Ctx {
   std::map<std::string, TimeAcc> times;
   std::vector<PendingEvent> pending;
   std::vector<uint8_t> staging;   // host staging for descriptor uploads
-  static constexpr int NSIDE = 8;
+  static constexpr int NSIDE = 10;
   hipStream_t side[NSIDE] = {};   // concurrent streams for independent jobs (lazily created)
   void* plan = nullptr;           // prepared collect() batch (collect.cpp)
 

@@ -32,13 +32,14 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
   FbExpArgs ea{U32(j.off.i_toff), U32(j.off.e_mod), U64(j.off.o_ptr), consts, d.table, d.sched, d.nsteps, j.stride,
                (uint32_t)j.count()};
   int rc;
-  if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
-  // the table chain may run on its own (CU-reserved) stream; the exponent kernel waits for it
+  // the table chain may run on its own stream (from t = 0, beside fb_sched); the
+  // exponent kernel waits for it
   hipStream_t ts = table_st ? table_st : st;
   size_t m = c->tbeg("fb_table", ts);
   rc = c->hip_check(launch_fb_table(j.k32, ta, ts), "fb_table launch");
   c->tend(m, ts);
   if (rc) return rc;
+  if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
   if (exp_wait) (void)hipStreamWaitEvent(st, exp_wait, 0);
   if (ts != st) {
     hipEvent_t ev;

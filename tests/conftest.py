@@ -7,8 +7,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (REPO, os.path.join(REPO, "fs-dkr_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
-# the collect() pipeline runs eight concurrent streams (see bench.py)
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(8, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+# the collect() pipeline runs up to eleven concurrent streams (see bench.py)
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
 def pytest_configure(config):

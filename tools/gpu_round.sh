@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 # collect() runs 8 concurrent streams; rocprofv3's preload initialises HIP before
 # bench.py can set this, so export it here (bench.py/conftest set it otherwise)
-export GPU_MAX_HW_QUEUES=8
+export GPU_MAX_HW_QUEUES=12
 for step in "$@"; do
   case $step in
     tests) timeout -k 10 600 python -m pytest $R/tests -m gpu -x -q > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -30 $OUT/tests.log; exit 1; } ;;

@@ -7,7 +7,7 @@ TAG=${1:-sweep}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-export TMPDIR=/tmp GPU_MAX_HW_QUEUES=8
+export TMPDIR=/tmp GPU_MAX_HW_QUEUES=12
 i=0
 for a in "$@"; do
   i=$((i+1))
