@@ -151,7 +151,11 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
                        uint32_t prio, uint32_t group) {
   if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
-  const int KD = shape_digits(k32);
+  // a forced context setting wins (tuning, tests), except that the 32-lane shape
+  // runs only where the caller asked for it (it prepared KD = 160 constants)
+  uint32_t grp = c->modexp_group ? c->modexp_group : group;
+  if (grp == kWideGroup && (group != kWideGroup || k32 != 128)) grp = 16;
+  const int KD = shape_digits_g(k32, grp);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
     return FSDKR_E_UNSUPPORTED;
@@ -179,7 +183,7 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.table = d_table;
   a.count = count;
   a.prio = prio;
-  a.group = c->modexp_group ? c->modexp_group : group;   // a forced context setting wins (tuning, tests)
+  a.group = grp;
   const size_t tm = c->tbeg("modexp", st);
   int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
   c->tend(tm, st);
@@ -201,7 +205,8 @@ void ModexpJob::pack(std::vector<uint8_t>& dst) const {
 }
 
 // Upload a modexp descriptor set and launch it against prepared constants.
-int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag) {
+int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
+                      uint32_t group) {
   const uint32_t count = (uint32_t)job.size();
   if (count == 0) return FSDKR_OK;
   std::string dname = std::string("mxdesc_") + tag;
@@ -218,11 +223,13 @@ int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, ui
   // the staging buffer is reused by the next call: make this copy complete first
   rc = c->hip_check(hipStreamSynchronize(c->stream), "sync desc");
   if (rc) return rc;
-  return launch_modexp_desc(c, job.k32, count, job.exp_bits, d_desc, d_consts, d_out);
+  return launch_modexp_desc(c, job.k32, count, job.exp_bits, d_desc, d_consts, d_out, nullptr, "mxtable", 0,
+                            group);
 }
 
-int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag) {
-  const int KD = shape_digits(k32);
+int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
+                 uint32_t group) {
+  const int KD = shape_digits_g(k32, group);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
     return FSDKR_E_UNSUPPORTED;
@@ -234,7 +241,7 @@ int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, u
     return FSDKR_E_OOM;
   }
   c->mark("mod_setup", true);
-  int rc = c->hip_check(mod_setup(k32, d_mods, n_mod, *d_consts, c->stream), "mod_setup launch");
+  int rc = c->hip_check(mod_setup_g(k32, group, d_mods, n_mod, *d_consts, c->stream), "mod_setup launch");
   c->mark("mod_setup", false);
   return rc;
 }
@@ -245,7 +252,9 @@ int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_ba
                       uint32_t n_mod, uint32_t* d_out) {
   if (count == 0) return FSDKR_OK;
   uint32_t* d_consts = nullptr;
-  int rc = setup_moduli(c, k32, d_mods, n_mod, &d_consts, "generic");
+  // a context forced to the 32-lane shape (tuning, tests) gets KD = 160 constants here
+  const uint32_t wide = (c->modexp_group == kWideGroup && k32 == 128) ? kWideGroup : 0u;
+  int rc = setup_moduli(c, k32, d_mods, n_mod, &d_consts, wide ? "generic_wide" : "generic", wide);
   if (rc) return rc;
   ModexpJob job;
   job.k32 = k32;
@@ -266,7 +275,7 @@ int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_ba
   if (rc) return rc;
   rc = c->hip_check(hipStreamSynchronize(c->stream), "sync");
   if (rc) return rc;
-  return launch_modexp_job(c, job, d_consts, d_out, "generic");
+  return launch_modexp_job(c, job, d_consts, d_out, "generic", wide);
 }
 
 }  // namespace fsdkr
@@ -335,7 +344,7 @@ const char* fsdkr_last_error(const fsdkr_ctx* ctx) {
 
 int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
-  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16)) return FSDKR_E_ARG;
+  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32)) return FSDKR_E_ARG;
   c->modexp_group = lanes;
   return FSDKR_OK;
 }

@@ -670,6 +670,24 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   uint32_t *cons_nn = nullptr, *cons_nl = nullptr;
   if ((rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn, "collect_nn"))) return rc;
   if ((rc = setup_moduli(c, nl, PI(o_mods), n_mods_nl, &cons_nl, "collect_nl"))) return rc;
+  // GA lanes per instance: GA shares the chip with the other streams, so it takes
+  // the largest group that keeps it within about half the resident lanes
+  // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
+  // (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants) for latency.
+  // FSDKR_COLLECT_GA_G overrides.
+  const uint32_t ga_forced = [] {
+    const char* e = getenv("FSDKR_COLLECT_GA_G");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  uint32_t ga_group = 8;
+  for (uint32_t g : {16u, kWideGroup})
+    if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
+  if (ga_forced) ga_group = ga_forced;
+  uint32_t* cons_nn_w = nullptr;
+  if (ga_group == kWideGroup && nn == 128 && pl.jcount[0] &&
+      (rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup)))
+    return rc;
+  if (ga_group == kWideGroup && nn != 128) ga_group = 16;
   // ---- stream plan (up to eleven concurrent lanes of work: give HIP >= 12 hardware
   //      queues, GPU_MAX_HW_QUEUES, or streams share queues and serialise):
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
@@ -706,7 +724,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   // prio: s_setprio level of the launch's waves (latency-critical chains); group: lanes per instance
   auto launch_group = [&](int k, hipStream_t ss, uint32_t prio, uint32_t group) -> int {
     if (!pl.jcount[k]) return FSDKR_OK;
-    const uint32_t* cons = (pl.jk32[k] == nn) ? cons_nn : cons_nl;
+    const uint32_t* cons = (pl.jk32[k] == nn) ? (group == kWideGroup ? cons_nn_w : cons_nn) : cons_nl;
     return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
                               tags[k], prio, group);
   };
@@ -724,22 +742,10 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   {  // GA: s2^N, s^N mod N^2 (4096-bit, 2048-bit exponents): the longest chains
     hipStream_t ss = c->side_stream(0);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    // lanes per instance: GA shares the chip with six other streams, so it takes
-    // the largest group that keeps it within about half the resident lanes
-    // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); few instances
-    // (multi-GPU shards) get 16 lanes for latency.  FSDKR_COLLECT_GA_G overrides.
-    const uint32_t ga_forced = [] {
-      const char* e = getenv("FSDKR_COLLECT_GA_G");
-      return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    uint32_t ga_group = 8;
-    for (uint32_t g : {16u})
-      if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
-    if (ga_forced) ga_group = ga_forced;
     // small batches (multi-GPU shards): the h2 fixed-base table chain (2816
     // dependent squarings) is the critical path, so GA steps down one issue
     // priority level below it (8-way shard: 33.4 -> 31.7 ms, tools/ab_hwq.sh)
-    if (ga_group == 16 && !getenv("FSDKR_PRIO")) prio[0] = 2;
+    if (ga_group >= 16 && !getenv("FSDKR_PRIO")) prio[0] = 2;
     if ((rc = launch_group(0, ss, prio[0], ga_group)) || (rc = join_later(ss))) return rc;
     if (ga_first && (rc = fork(ss, &ga_done))) return rc;
   }

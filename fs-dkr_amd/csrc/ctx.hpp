@@ -113,11 +113,14 @@ inline uint8_t ped_verdict(const uint32_t* eq, uint32_t M, uint32_t panic_word) 
   return panic_word ? 2 : 1;
 }
 void free_collect_plan(Ctx* c);
-int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag);
+int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
+                      uint32_t group = 0);
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st = nullptr,
                        const char* table_tag = "mxtable", uint32_t prio = 0, uint32_t group = 0);
-int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag);
+// group: kWideGroup prepares the KD = 160 constants of the 32-lane 4096-bit shape
+int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
+                 uint32_t group = 0);
 int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
                       uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,
                       uint32_t n_mod, uint32_t* d_out);

@@ -27,7 +27,14 @@ struct ModexpArgs {
 };
 
 int shape_digits(uint32_t k32);   // KD for a K32-limb modulus class (0 if unsupported)
+// The 32-lane 4096-bit latency shape uses KD = 160 digits (L = 5 per lane), so its
+// Montgomery constants (R = 2^(29 KD)) differ from the 144-digit class: a launch
+// with group kWideGroup needs consts from mod_setup_g(k32, kWideGroup, ...).
+constexpr uint32_t kWideGroup = 32;
+int shape_digits_g(uint32_t k32, uint32_t group);
 hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st);
+hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint32_t n_mod, uint32_t* consts,
+                       hipStream_t st);
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st);
 
 }  // namespace fsdkr

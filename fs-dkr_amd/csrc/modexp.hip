@@ -218,6 +218,16 @@ int shape_digits(uint32_t k32) {
   }
 }
 
+int shape_digits_g(uint32_t k32, uint32_t group) {
+  return (k32 == 128 && group == kWideGroup) ? 160 : shape_digits(k32);
+}
+
+hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint32_t n_mod, uint32_t* consts,
+                       hipStream_t st) {
+  if (k32 == 128 && group == kWideGroup) return launch_setup<160, 8, 128>(mods, n_mod, consts, st);
+  return mod_setup(k32, mods, n_mod, consts, st);
+}
+
 hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
   switch (k32) {
     case 64: return launch_setup<72, 2, 64>(mods, n_mod, consts, st);
@@ -261,6 +271,8 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
       }
     case 96: return launch_modexp<108, 4, 96>(a, st);
     case 128:
+      // 32 lanes only on explicit request: it needs KD = 160 constants (mod_setup_g)
+      if (a.group == kWideGroup) return launch_modexp<160, 32, 128>(a, st);
       switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 8)) {
         case 16: return launch_modexp<144, 16, 128>(a, st);
         case 8: return launch_modexp<144, 8, 128>(a, st);

@@ -8,7 +8,7 @@
 // resolved by a cheap parallel normalisation every 18 rows.
 //
 // Layout: a KD-digit integer is owned by G consecutive lanes (G in {2,4,8,16}:
-// one DPP quad or part of one 16-lane DPP row); lane g holds digits
+// one DPP quad or part of one 16-lane DPP row; G = 32: two rows, see below); lane g holds digits
 // [g*L, g*L+L), L = KD/G.  Larger G = lower latency per instance (small
 // batches), smaller G = fewer cross-lane ops per MAC (full chip).  Row-oriented CIOS:
 // row i broadcasts digit a_i of the streamed operand (LDS) to the group, every
@@ -42,9 +42,17 @@ constexpr uint32_t M29 = (1u << 29) - 1;
 #define FSDKR_DPP_BANK(old, v, ctrl, bank) \
   ((uint32_t)__builtin_amdgcn_update_dpp((int)(old), (int)(v), (ctrl), 0xF, (bank), false))
 
+// G = 32 (4096-bit latency shape, two instances per wave): the group spans two
+// DPP rows, so the carry moves use the GFX9 wavefront shifts (wave_shl/shr:1)
+// and the lane-0 broadcast is row_newbcast:0 followed by row_bcast:15 into the
+// odd rows.
 template <int G>
 __device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
   if constexpr (G == 1) return v;
+  else if constexpr (G == 32) {
+    const uint32_t t = FSDKR_DPP(v, 0x150);                                   // row_newbcast:0
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)t, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+  }
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0x00);   // [0,0,0,0]
   else if constexpr (G == 8) return FSDKR_DPP_BANK(FSDKR_DPP_BANK(v, v, 0x150, 0x3), v, 0x158, 0xC);
@@ -53,6 +61,7 @@ __device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
 template <int G>
 __device__ __forceinline__ uint32_t bcast_top(uint32_t v) {
   if constexpr (G == 1) return v;
+  else if constexpr (G == 32) return (uint32_t)__shfl((int)v, (int)((__lane_id() & ~31u) + 31u));   // rare: once per modexp
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xF5);   // [1,1,3,3]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0xFF);   // [3,3,3,3]
   else if constexpr (G == 8) return FSDKR_DPP_BANK(FSDKR_DPP_BANK(v, v, 0x157, 0x3), v, 0x15F, 0xC);
@@ -62,6 +71,7 @@ __device__ __forceinline__ uint32_t bcast_top(uint32_t v) {
 template <int G>
 __device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
   if constexpr (G == 1) return v;
+  else if constexpr (G == 32) return FSDKR_DPP(v, 0x130);   // wave_shl:1
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xF5);   // [1,1,3,3]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0xF9);   // [1,2,3,3]
   else return FSDKR_DPP(v, 0x101);                        // row_shl:1
@@ -70,6 +80,7 @@ __device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
 template <int G>
 __device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {
   if constexpr (G == 1) return v;
+  else if constexpr (G == 32) return FSDKR_DPP(v, 0x138);   // wave_shr:1
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0x90);   // [0,0,1,2]
   else return FSDKR_DPP(v, 0x111);                        // row_shr:1
@@ -81,6 +92,7 @@ __device__ __forceinline__ int group_max(int v) {
   if constexpr (G >= 4) v = max(v, (int)FSDKR_DPP(v, 0x4E));   // [2,3,0,1]
   if constexpr (G >= 8) v = max(v, (int)FSDKR_DPP(v, 0x141));  // row_half_mirror
   if constexpr (G >= 16) v = max(v, (int)FSDKR_DPP(v, 0x140)); // row_mirror
+  if constexpr (G >= 32) v = max(v, __shfl_xor(v, 16));
   return v;
 }
 
