@@ -8,13 +8,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
+#include <thread>
 #include <string>
 #include <vector>
 
 #include "ctx.hpp"
 #include "kernels.h"
-#include "verify.h"
 #include "verify.h"
 
 using namespace fsdkr;
@@ -51,6 +52,38 @@ void* Ctx::buf(const char* name, size_t bytes) {
   }
   b.bytes = want;
   return b.ptr;
+}
+
+uint8_t* Ctx::host_arena(size_t bytes) {
+  if (pinned && pinned_bytes >= bytes) return pinned;
+  if (pinned) (void)hipHostFree(pinned);
+  pinned = nullptr;
+  pinned_bytes = 0;
+  const size_t want = bytes + bytes / 4 + (1u << 20);
+  if (hipHostMalloc((void**)&pinned, want, hipHostMallocDefault) != hipSuccess) {
+    pinned = nullptr;
+    return nullptr;
+  }
+  pinned_bytes = want;
+  return pinned;
+}
+
+hipStream_t Ctx::aux_stream() {
+  if (!aux && hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess) aux = nullptr;
+  return aux ? aux : stream;
+}
+
+unsigned host_threads() {
+  static unsigned n = [] {
+    for (const char* k : {"FSDKR_HOST_THREADS", "OMP_NUM_THREADS"})
+      if (const char* e = getenv(k)) {
+        const int v = atoi(e);
+        if (v > 0) return (unsigned)std::min(v, 64);
+      }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return hw ? std::min(hw, 16u) : 4u;
+  }();
+  return n;
 }
 
 size_t Ctx::tbeg(const char* name, hipStream_t st) {
@@ -115,7 +148,14 @@ hipStream_t Ctx::crit_stream() {
 
 int Ctx::sync() {
   int rc = hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+  // fold finished event pairs; pairs of work still running on another stream
+  // (a launched collect batch while the recovery stream syncs) stay pending
+  std::vector<PendingEvent> keep;
   for (auto& p : pending) {
+    if (p.e1 && hipEventQuery(p.e1) == hipErrorNotReady) {
+      keep.push_back(p);
+      continue;
+    }
     if (p.e1) {
       float ms = 0.f;
       if (hipEventElapsedTime(&ms, p.e0, p.e1) == hipSuccess) {
@@ -127,7 +167,7 @@ int Ctx::sync() {
     }
     (void)hipEventDestroy(p.e0);
   }
-  pending.clear();
+  pending.swap(keep);
   return rc;
 }
 
@@ -332,6 +372,8 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
   for (auto& sd : c->side)
     if (sd) (void)hipStreamDestroy(sd);
   if (c->crit) (void)hipStreamDestroy(c->crit);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   fsdkr::free_collect_plan(c);
   delete c;

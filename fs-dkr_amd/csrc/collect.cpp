@@ -1,19 +1,29 @@
 // Host orchestration of the batched RefreshMessage::collect verification
-// (fsdkr_verify_collect) and the first-error mapping (fsdkr_collect_first_error).
+// (fsdkr_verify_collect[_multi], prepare / launch / finish) and the first-error
+// mapping (fsdkr_collect_first_error).
 //
 // Reference: /root/reference/src/refresh_message.rs:321-467 (collect),
 // :147-191 (validate_collect); zk_pdl_with_slack.rs:113-188; range_proofs.rs:112-164;
 // ring_pedersen_proof.rs:126-157; zk-paillier NiCorrectKeyProof / CompositeDLogProof.
 //
-// Pipeline (one HIP stream, one H2D copy of inputs + descriptors):
-//   pdl_hash, ped_hash -> binom -> 9 modexp jobs -> inverses -> eq_check / prod3
-//   -> alice_hash, pdl_u1, feldman -> one D2H copy of the verdict words.
+// One call verifies one or many independent collect() sessions in ONE device
+// pass: the sessions' pairs, receivers, messages and joins are concatenated
+// into a single image (little-endian u32 limbs, one fixed width per field);
+// every descriptor addresses rows of that image.  Pipeline (streams in
+// launch()): pdl_hash, ped_hash -> binom -> modexp jobs (GA, GD, GC, J2, J5, FB)
+// -> inverses -> eq_check / prod3 -> alice_hash; pdl_u1, Feldman and the 2-adic
+// checks of even moduli beside them -> one D2H of the verdict words (finish()).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
@@ -48,69 +58,162 @@ const std::vector<uint32_t>& small_primes() {
   return ps;
 }
 
-// Device layout builder: inputs (with host data) and outputs share one allocation.
-struct Layout {
-  std::vector<uint8_t> host;   // bytes to upload (inputs + descriptors)
-  size_t out_bytes = 0;        // outputs placed after the inputs
-  static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
-  size_t in(const void* src, size_t bytes) {
-    const size_t o = al(host.size());
-    host.resize(o + al(bytes ? bytes : 1), 0);
-    if (src && bytes) memcpy(host.data() + o, src, bytes);
-    return o;
-  }
-  size_t in_vec(const std::vector<uint8_t>& v) { return in(v.data(), v.size()); }
-  template <class T>
-  size_t in_vecT(const std::vector<T>& v) { return in(v.data(), v.size() * sizeof(T)); }
-  // returns an OUTPUT offset (relative to the output region)
-  size_t out(size_t bytes) {
-    const size_t o = al(out_bytes);
-    out_bytes = o + al(bytes ? bytes : 1);
-    return o;
-  }
-};
-
-struct Sizes {
-  uint32_t R, J, n, P, Mt, M, nl, nn;
-};
+// q^3 (the Alice s1 bound, range_proofs.rs:125) as limbs
+const hbn::Limbs& q_cubed() {
+  static hbn::Limbs q3 = [] {
+    const hbn::Limbs q = hbn::from(Q_LIMBS_H, 8);
+    return hbn::mul(hbn::mul(q, q), q);
+  }();
+  return q3;
+}
 
 inline bool is_odd(const uint32_t* p) { return (p[0] & 1u) != 0; }
-inline bool all_zero(const uint32_t* p, size_t n) {
-  for (size_t k = 0; k < n; ++k)
-    if (p[k]) return false;
-  return true;
-}
 
 // to_bytes(x) absorbed for a small non-negative integer
 inline void absorb_u32(Sha256& h, uint32_t v) { h.bigint(&v, 1); }
 
+// f(begin, end) over [0, n) on up to host_threads() threads (inline when small)
+template <class F>
+void parallel_for(size_t n, size_t grain, F&& f) {
+  const size_t want = grain ? (n + grain - 1) / grain : 1;
+  const size_t chunks = std::min<size_t>(host_threads(), want);
+  if (chunks <= 1) {
+    f((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(chunks - 1);
+  for (size_t c = 1; c < chunks; ++c) th.emplace_back([&, c] { f(n * c / chunks, n * (c + 1) / chunks); });
+  f((size_t)0, n / chunks);
+  for (auto& t : th) t.join();
+}
+
+// FSDKR_PREP_PROFILE=1: host pre-pass phase times on stderr (diagnostics)
+struct PhaseClock {
+  bool on = getenv("FSDKR_PREP_PROFILE") != nullptr;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "[prep] %-16s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+
+// Image planner: offsets are assigned first, the bytes are written into the
+// pinned arena afterwards (rows re-packed to the merged limb width, in parallel).
+struct Img {
+  struct Op {
+    size_t dst;
+    const uint8_t* src;
+    size_t rows, src_stride, dst_stride;   // bytes
+  };
+  std::vector<Op> ops;
+  std::vector<std::vector<uint8_t>> owned;
+  size_t size = 0;
+  static size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+  size_t reserve(size_t bytes) {
+    const size_t o = al(size);
+    size = o + al(bytes ? bytes : 1);
+    return o;
+  }
+  // `rows` rows of w_src words written at `dst` with stride w_dst >= w_src words (zero-padded)
+  void rows_at(size_t dst, const uint32_t* src, size_t rows, uint32_t w_src, uint32_t w_dst) {
+    if (!rows) return;
+    ops.push_back({dst, reinterpret_cast<const uint8_t*>(src), rows, (size_t)w_src * 4, (size_t)w_dst * 4});
+  }
+  size_t own_at(size_t dst, std::vector<uint8_t>&& b) {
+    owned.push_back(std::move(b));
+    const std::vector<uint8_t>& v = owned.back();
+    if (!v.empty()) ops.push_back({dst, v.data(), 1, v.size(), v.size()});
+    return dst;
+  }
+  template <class T>
+  size_t own(const std::vector<T>& v) {
+    std::vector<uint8_t> b(v.size() * sizeof(T));
+    if (!b.empty()) memcpy(b.data(), v.data(), b.size());
+    const size_t o = reserve(b.size());
+    return own_at(o, std::move(b));
+  }
+  void materialize(uint8_t* base) const {
+    // split big row copies into ~1 MB pieces so the threads share the work
+    struct Piece {
+      const Op* op;
+      size_t r0, r1;
+    };
+    std::vector<Piece> pieces;
+    for (const Op& op : ops) {
+      const size_t per = std::max<size_t>(1, (1u << 20) / std::max<size_t>(op.dst_stride, 1));
+      for (size_t r = 0; r < op.rows; r += per) pieces.push_back({&op, r, std::min(op.rows, r + per)});
+    }
+    parallel_for(pieces.size(), 4, [&](size_t b, size_t e) {
+      for (size_t k = b; k < e; ++k) {
+        const Op& op = *pieces[k].op;
+        if (op.src_stride == op.dst_stride) {
+          memcpy(base + op.dst + pieces[k].r0 * op.dst_stride, op.src + pieces[k].r0 * op.src_stride,
+                 (pieces[k].r1 - pieces[k].r0) * op.dst_stride);
+          continue;
+        }
+        for (size_t r = pieces[k].r0; r < pieces[k].r1; ++r) {
+          uint8_t* d = base + op.dst + r * op.dst_stride;
+          memcpy(d, op.src + r * op.src_stride, op.src_stride);
+          memset(d + op.src_stride, 0, op.dst_stride - op.src_stride);
+        }
+      }
+    });
+  }
+};
+
+// one session's place in the merged image
+struct Sess {
+  const fsdkr_collect_batch* b;
+  uint32_t R, J, n, Mt, P, V;
+  uint32_t rbase, mbase, jbase, pbase, vbase;
+  uint32_t ckl;
+};
+
+inline uint32_t ncoef_of(const fsdkr_collect_batch* b, uint32_t k) { return b->vss_len ? b->vss_len[k] : b->t + 1; }
+
 }  // namespace
 
 // ------------------------------------------------------------------------------
-// Everything the run phase needs after the host pre-pass and the upload.
+// Everything launch()/finish() need after the host pre-pass and the upload.
 struct CollectPlan {
-  Sizes s{};
-  uint32_t el = 0, t = 0;
-  size_t in_bytes = 0, out_off = 0, total = 0;
+  // merged shape
+  uint32_t S = 0, n = 0, P = 0, Mt = 0, J = 0, M = 0, nl = 0, nn = 0, ckl = 0, s1l = 0, el = 0;
+  std::vector<Sess> ss;               // per-session offsets (batch pointers are not kept)
+  size_t out_off = 0, total = 0;
   uint8_t* dev = nullptr;
   // input offsets used by launches
-  size_t o_Q, o_enc, o_pz, o_pu1, o_pu2, o_pu3, o_ps1, o_pA, o_az, o_ae, o_vss, o_NN, o_mods, o_one, o_rn;
-  uint32_t s1l = 0, n_mods_nl = 0;
+  size_t o_Q, o_enc, o_pz, o_pu1, o_pu2, o_pu3, o_ps1, o_pA, o_az, o_ae, o_vss, o_NN, o_mods, o_ckmods, o_one;
+  size_t d_finfo = 0, d_p2 = 0;
+  uint32_t n_mods_nl = 0, n_p2 = 0;
   // output offsets
-  size_t x_epdl, x_pbits, x_ppanic, x_Bpdl, x_gs1, x_J[10], x_invc, x_invz, x_unn, x_uzA, x_uzp, x_eq2, x_eq3, x_u,
-      x_w, x_fel, x_pdlv, x_rng;
-  // descriptor offsets + counts
-  size_t d_J[10], d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_p3nn, d_p3nl, d_p3m,
-      d_ahn, d_ahc, d_alpre;
-  uint32_t jk32[10], jcount[10], jbits[10];
-  uint32_t n_inv_nn = 0, n_eq_nn = 0, n_eq_nl = 0;
-  std::vector<uint32_t> cpdl_extra, ae_bits;
-  std::vector<uint8_t> ck_pre, dlog_pre;
-  FbJob fb;                 // h1_i, h2_i, ring-Pedersen T: fixed-base job
-  size_t d_FB = 0;          // its descriptor image (input region)
-  uint32_t* fb_table = nullptr;   // its scratch (separate context buffer)
+  size_t x_epdl, x_pbits, x_ppanic, x_Bpdl, x_gs1, x_invc, x_invz, x_unn, x_uzA, x_uzp, x_eq2, x_eq3, x_eqck, x_u,
+      x_w, x_fel, x_pdlv, x_rng, x_p2;
+  // modexp jobs: 0 GA (nn long), 1 GD (nl: DLog), 2 J2 (nn short), 3 J5 (nl short), 4 GC (ckl: correct key)
+  static constexpr int NJOB = 5;
+  size_t d_J[NJOB], x_J[NJOB];
+  uint32_t jk32[NJOB], jcount[NJOB], jbits[NJOB];
+  // descriptor offsets
+  size_t d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_eqck, d_eqckm, d_p3nn, d_p3nl,
+      d_p3m, d_ahn, d_ahc, d_alpre;
+  uint32_t n_inv_nn = 0, n_eq_nn = 0, n_eq_nl = 0, n_eq_ck = 0;
+  // host-side pre-verdicts
+  std::vector<uint32_t> cpdl_extra;
+  std::vector<uint8_t> ck_pre, dlog_pre;   // dlog_pre: bit0 / bit1 per proof
+  std::vector<uint8_t> ped_mode;           // 0 regular, 1 odd part 1 (Montgomery half holds), 2 modulus 0 (abort)
+  std::vector<uint8_t> dlog_trivial;       // odd part of the DLog N is 1
+  std::vector<uint32_t> ped_p2_first, dlog_p2_first;   // first 2-adic op of an even message / join (~0: none)
+  std::vector<uint32_t> ped_zlen;          // readable Z entries (M: all); A short: ped_mode 2
+  std::vector<uint8_t> ck_short;           // sigma_vec shorter than 11 (or n = 0): zk-paillier panics
+  std::vector<uint8_t> ck_one;             // n = 1: the proof verifies trivially
+  FbJob fb;
+  size_t d_FB = 0;
+  uint32_t* fb_table = nullptr;
   uint16_t* fb_sched = nullptr;
   uint32_t* fb_nsteps = nullptr;
+  bool launched = false;
 };
 
 void free_collect_plan(Ctx* c) {
@@ -118,386 +221,594 @@ void free_collect_plan(Ctx* c) {
   c->plan = nullptr;
 }
 
-int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
-  free_collect_plan(c);
-  CollectPlan* plan = new CollectPlan();
-  c->plan = plan;
+// ------------------------------------------------------------------------------
+static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
+  free_collect_plan(c);   // a failed prepare leaves no plan behind
+  if (!bs || count == 0) {
+    c->fail("fsdkr_collect_prepare: no batch");
+    return FSDKR_E_ARG;
+  }
+  std::unique_ptr<CollectPlan> plan(new CollectPlan());
   CollectPlan& pl = *plan;
-  Sizes& s = pl.s;
-  s.R = b->n_refresh;
-  s.J = b->n_join;
-  s.n = b->n_recv ? b->n_recv : s.R + s.J;
-  s.P = s.R * s.n;
-  s.Mt = s.R + s.J;
-  s.M = b->m_security;
-  s.nl = b->nl;
-  s.nn = 2 * b->nl;
-  if (s.n < s.R || s.M == 0 || !(s.nl == 64 || s.nl == 96) || b->s1l == 0 || b->s3l == 0 || b->el == 0 ||
-      b->zl == 0 || (s.J && b->yl == 0)) {
-    c->fail("fsdkr_verify_collect: unsupported shape (R=%u nl=%u)", s.R, s.nl);
-    return FSDKR_E_UNSUPPORTED;
-  }
-  const uint32_t nl = s.nl, nn = s.nn, P = s.P, n = s.n, Mt = s.Mt, M = s.M, R = s.R, J = s.J;
-  // odd moduli are required by the Montgomery kernels
-  for (uint32_t i = 0; i < n; ++i)
-    if (!is_odd(b->recv_n + (size_t)i * nl) || !is_odd(b->recv_ntilde + (size_t)i * nl)) {
-      c->fail("receiver %u: even Paillier or DLog modulus (unsupported)", i);
+  PhaseClock clk;
+  // ---------------- shapes
+  uint32_t nl = 0, s1l = 0, s3l = 0, el = 0, zl = 0, yl = 1, ckl = 0, M = 0;
+  pl.ss.resize(count);
+  uint32_t n = 0, P = 0, Mt = 0, J = 0, V = 0;
+  for (uint32_t s = 0; s < count; ++s) {
+    const fsdkr_collect_batch* b = bs + s;
+    Sess& x = pl.ss[s];
+    x.b = b;
+    x.R = b->n_refresh;
+    x.J = b->n_join;
+    x.n = b->n_recv ? b->n_recv : x.R + x.J;
+    x.Mt = x.R + x.J;
+    x.P = x.R * x.n;
+    x.ckl = b->ckl ? b->ckl : b->nl;
+    if (x.n < x.R || x.n == 0 || b->m_security == 0 || !(b->nl == 64 || b->nl == 96) || b->s1l == 0 ||
+        b->s3l == 0 || b->el == 0 || b->zl == 0 || (x.J && b->yl == 0) || !shape_digits(x.ckl) || x.ckl < b->nl ||
+        (M && b->m_security != M) || !b->party_index) {
+      c->fail("fsdkr_collect_prepare: session %u: unsupported shape (R=%u J=%u n=%u nl=%u ckl=%u M=%u)", s, x.R, x.J,
+              x.n, b->nl, x.ckl, b->m_security);
       return FSDKR_E_UNSUPPORTED;
     }
-  for (uint32_t m = 0; m < Mt; ++m)
-    if (!is_odd(b->ped_N + (size_t)m * nl)) {
-      c->fail("message %u: even ring-Pedersen modulus (unsupported)", m);
-      return FSDKR_E_UNSUPPORTED;
-    }
-  for (uint32_t j = 0; j < J; ++j)
-    if (!is_odd(b->dlog_N + (size_t)j * nl)) {
-      c->fail("join %u: even DLog modulus (unsupported)", j);
-      return FSDKR_E_UNSUPPORTED;
-    }
-
-  // ---------------- host pre-computation (O(n) + O(P) scans, no big exponentiations)
-  // NN_i = N_i^2, N_i + 1
-  std::vector<uint32_t> NN((size_t)n * nn), NP1((size_t)n * nn);
-  for (uint32_t i = 0; i < n; ++i) {
-    hbn::Limbs N = hbn::from(b->recv_n + (size_t)i * nl, nl);
-    hbn::store(hbn::mul(N, N), NN.data() + (size_t)i * nn, nn);
-    hbn::store(hbn::add_small(N, 1), NP1.data() + (size_t)i * nn, nn);
-  }
-  // q^3 for the Alice s1 bound (range_proofs.rs:125)
-  const hbn::Limbs q = hbn::from(Q_LIMBS_H, 8);
-  const hbn::Limbs q3 = hbn::mul(hbn::mul(q, q), q);
-  std::vector<uint8_t> alice_pre(P), pdl_small(P);
-  std::vector<uint32_t> s1_bits(P), s3_bits(P), a1_bits(P), a2_bits(P);
-  std::vector<uint32_t>& ae_bits = pl.ae_bits;
-  ae_bits.assign(P, 0);
-  uint32_t pdl_s1_max = 1, pdl_s3_max = 1, a_s1_max = 1, a_s2_max = 1, a_e_max = 1;
-  bool any_big_s1 = false;
-  for (uint32_t p = 0; p < P; ++p) {
-    const uint32_t i = p % n;
-    const uint32_t Nbits = hbn::bitlen(b->recv_n + (size_t)i * nl, nl);
-    const uint32_t* s1 = b->pdl_s1 + (size_t)p * b->s1l;
-    s1_bits[p] = hbn::bitlen(s1, b->s1l);
-    // s1 < N  -> (N+1)^s1 mod N^2 = 1 + s1*N  (binomial, bit-identical)
-    bool small = s1_bits[p] < Nbits;
-    if (!small && s1_bits[p] == Nbits) small = hbn::cmp(hbn::from(s1, b->s1l), hbn::from(b->recv_n + (size_t)i * nl, nl)) < 0;
-    pdl_small[p] = small ? 1 : 0;
-    any_big_s1 = any_big_s1 || !small;
-    s3_bits[p] = hbn::bitlen(b->pdl_s3 + (size_t)p * b->s3l, b->s3l);
-    const uint32_t* as1 = b->rp_s1 + (size_t)p * b->s1l;
-    a1_bits[p] = hbn::bitlen(as1, b->s1l);
-    a2_bits[p] = hbn::bitlen(b->rp_s2 + (size_t)p * b->s3l, b->s3l);
-    ae_bits[p] = hbn::bitlen(b->rp_e + (size_t)p * b->el, b->el);
-    const bool s1_ok = hbn::cmp(hbn::from(as1, b->s1l), q3) <= 0;
-    alice_pre[p] = (s1_ok && ae_bits[p] <= 256) ? 1 : 0;
-    pdl_s1_max = std::max(pdl_s1_max, s1_bits[p]);
-    pdl_s3_max = std::max(pdl_s3_max, s3_bits[p]);
-    if (alice_pre[p]) {  // exponents of rejected proofs are never used
-      a_s1_max = std::max(a_s1_max, a1_bits[p]);
-      a_s2_max = std::max(a_s2_max, a2_bits[p]);
-      a_e_max = std::max(a_e_max, ae_bits[p]);
-    }
-  }
-  // correct-key: rho_j = mask_generation(len(n), H(n, salt, j)) mod n; primorial gcd
-  std::vector<uint32_t> RHO((size_t)Mt * CK_M2 * nl);
-  std::vector<uint8_t>& ck_pre = pl.ck_pre;
-  ck_pre.assign(Mt, 0);
-  for (uint32_t m = 0; m < Mt; ++m) {
-    const uint32_t* ckn = b->ck_n + (size_t)m * nl;
-    const hbn::Limbs N = hbn::from(ckn, nl);
-    bool ok = !N.empty();
-    for (uint32_t pr : small_primes())
-      if (ok && hbn::mod_small(N, pr) == 0) ok = false;
-    ck_pre[m] = ok ? 1 : 0;
-    const uint32_t key_len = hbn::bitlen(N);
-    const uint32_t msklen = key_len / 256 + 1;
-    const uint32_t salt_v = ((uint32_t)SALT[0] << 24) | ((uint32_t)SALT[1] << 16) | ((uint32_t)SALT[2] << 8) | SALT[3];
-    for (uint32_t j = 0; j < CK_M2; ++j) {
-      Sha256 h;
-      h.init();
-      h.bigint(ckn, nl);
-      absorb_u32(h, salt_v);
-      absorb_u32(h, j);
-      uint32_t seed[8];
-      h.finish_le(seed);
-      std::vector<uint32_t> mask((size_t)msklen * 8, 0);
-      for (uint32_t k = 0; k < msklen; ++k) {
-        Sha256 hk;
-        hk.init();
-        hk.bigint(seed, 8);
-        absorb_u32(hk, k);
-        hk.finish_le(mask.data() + (size_t)k * 8);
+    M = b->m_security;
+    // the receivers' own keys (LocalKey state, not message data) must be odd for Montgomery
+    for (uint32_t i = 0; i < x.n; ++i)
+      if (!is_odd(b->recv_n + (size_t)i * b->nl) || !is_odd(b->recv_ntilde + (size_t)i * b->nl)) {
+        c->fail("session %u receiver %u: even Paillier or DLog modulus in the LocalKey (unsupported)", s, i);
+        return FSDKR_E_UNSUPPORTED;
       }
-      if (N.empty()) continue;
-      hbn::store(hbn::mod(hbn::from(mask.data(), mask.size()), N), RHO.data() + ((size_t)m * CK_M2 + j) * nl, nl);
-    }
+    x.V = 0;
+    for (uint32_t k = 0; k < x.R; ++k) x.V += ncoef_of(b, k);
+    x.rbase = n;
+    x.mbase = Mt;
+    x.jbase = J;
+    x.pbase = P;
+    x.vbase = V;
+    n += x.n;
+    Mt += x.Mt;
+    J += x.J;
+    P += x.P;
+    V += x.V;
+    nl = std::max(nl, b->nl);
+    s1l = std::max(s1l, b->s1l);
+    s3l = std::max(s3l, b->s3l);
+    el = std::max(el, b->el);
+    zl = std::max(zl, b->zl);
+    if (x.J) yl = std::max(yl, b->yl);
+    ckl = std::max(ckl, x.ckl);
   }
-  // DLog statements: N > 2^128, gcd(g, N) = gcd(ni, N) = 1; challenges e = H(x, g, N, ni)
-  std::vector<uint8_t>& dlog_pre = pl.dlog_pre;
-  dlog_pre.assign(J, 0);
-  std::vector<uint32_t> DE((size_t)J * 2 * 8);
-  uint32_t y_max = 1;
-  for (uint32_t j = 0; j < J; ++j) {
-    const uint32_t *N = b->dlog_N + (size_t)j * nl, *g = b->dlog_g + (size_t)j * nl, *ni = b->dlog_ni + (size_t)j * nl;
-    const hbn::Limbs Nl = hbn::from(N, nl);
-    bool ok = hbn::bitlen(Nl) > 129 || (hbn::bitlen(Nl) == 129 && !(Nl.size() == 5 && Nl[4] == 1 && all_zero(N, 4)));
-    ok = ok && hbn::is_one(hbn::gcd(hbn::from(g, nl), Nl)) && hbn::is_one(hbn::gcd(hbn::from(ni, nl), Nl));
-    dlog_pre[j] = ok ? 1 : 0;
-    for (int which = 0; which < 2; ++which) {
-      const uint32_t* x = (which == 0 ? b->dlog_x1 : b->dlog_x2) + (size_t)j * nl;
-      const uint32_t* gg = which == 0 ? g : ni;
-      const uint32_t* nn_ = which == 0 ? ni : g;
-      Sha256 h;
-      h.init();
-      h.bigint(x, nl);
-      h.bigint(gg, nl);
-      h.bigint(N, nl);
-      h.bigint(nn_, nl);
-      h.finish_le(DE.data() + ((size_t)j * 2 + which) * 8);
-    }
-    y_max = std::max(y_max, hbn::bitlen(b->dlog_y1 + (size_t)j * b->yl, b->yl));
-    y_max = std::max(y_max, hbn::bitlen(b->dlog_y2 + (size_t)j * b->yl, b->yl));
+  const uint32_t nn = 2 * nl;
+  pl.S = count;
+  pl.n = n;
+  pl.P = P;
+  pl.Mt = Mt;
+  pl.J = J;
+  pl.M = M;
+  pl.nl = nl;
+  pl.nn = nn;
+  pl.ckl = ckl;
+  pl.s1l = s1l;
+  pl.el = el;
+  const uint32_t MW = (M + 31) / 32;
+  // global index -> session
+  std::vector<uint32_t> sess_of_pair(P), sess_of_recv(n), sess_of_msg(Mt), sess_of_join(J);
+  for (uint32_t s = 0; s < count; ++s) {
+    const Sess& x = pl.ss[s];
+    std::fill(sess_of_pair.begin() + x.pbase, sess_of_pair.begin() + x.pbase + x.P, s);
+    std::fill(sess_of_recv.begin() + x.rbase, sess_of_recv.begin() + x.rbase + x.n, s);
+    std::fill(sess_of_msg.begin() + x.mbase, sess_of_msg.begin() + x.mbase + x.Mt, s);
+    std::fill(sess_of_join.begin() + x.jbase, sess_of_join.begin() + x.jbase + x.J, s);
   }
-  uint32_t z_max = 1;
-  for (size_t k = 0; k < (size_t)Mt * M; ++k) z_max = std::max(z_max, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
-  uint32_t ckn_max = 1;
-  for (uint32_t m = 0; m < Mt; ++m) ckn_max = std::max(ckn_max, hbn::bitlen(b->ck_n + (size_t)m * nl, nl));
-  uint32_t recvn_max = 1;
-  for (uint32_t i = 0; i < n; ++i) recvn_max = std::max(recvn_max, hbn::bitlen(b->recv_n + (size_t)i * nl, nl));
+  std::vector<uint32_t> recv_of_pair(P);   // global receiver row of each pair
+  for (uint32_t p = 0; p < P; ++p) {
+    const Sess& x = pl.ss[sess_of_pair[p]];
+    recv_of_pair[p] = x.rbase + (p - x.pbase) % x.n;
+  }
+  clk.lap("shapes");
 
-  // ---------------- device layout: inputs
-  Layout L;
-  auto IN = [&](const uint32_t* p, size_t words) { return L.in(p, words * 4); };
-  const size_t o_rn = IN(b->recv_n, (size_t)n * nl), o_rt = IN(b->recv_ntilde, (size_t)n * nl);
-  const size_t o_h1 = IN(b->recv_h1, (size_t)n * nl), o_h2 = IN(b->recv_h2, (size_t)n * nl);
-  const size_t o_NN = IN(NN.data(), NN.size()), o_NP1 = IN(NP1.data(), NP1.size());
-  const size_t o_enc = IN(b->enc, (size_t)P * nn), o_Q = IN(b->commit, (size_t)P * 16);
-  const size_t o_pz = IN(b->pdl_z, (size_t)P * nl), o_pu1 = IN(b->pdl_u1, (size_t)P * 16);
-  const size_t o_pu2 = IN(b->pdl_u2, (size_t)P * nn), o_pu3 = IN(b->pdl_u3, (size_t)P * nl);
-  const size_t o_ps1 = IN(b->pdl_s1, (size_t)P * b->s1l), o_ps2 = IN(b->pdl_s2, (size_t)P * nl);
-  const size_t o_ps3 = IN(b->pdl_s3, (size_t)P * b->s3l);
-  const size_t o_az = IN(b->rp_z, (size_t)P * nl), o_ae = IN(b->rp_e, (size_t)P * b->el);
-  const size_t o_as = IN(b->rp_s, (size_t)P * nl), o_as1 = IN(b->rp_s1, (size_t)P * b->s1l);
-  const size_t o_as2 = IN(b->rp_s2, (size_t)P * b->s3l);
-  const size_t o_vss = IN(b->vss, (size_t)R * (b->t + 1) * 16);
-  const size_t o_pS = IN(b->ped_S, (size_t)Mt * nl), o_pT = IN(b->ped_T, (size_t)Mt * nl);
-  const size_t o_pN = IN(b->ped_N, (size_t)Mt * nl);
-  const size_t o_pA = IN(b->ped_A, (size_t)Mt * M * nl), o_pZ = IN(b->ped_Z, (size_t)Mt * M * b->zl);
-  const size_t o_ckn = IN(b->ck_n, (size_t)Mt * nl), o_cks = IN(b->ck_sigma, (size_t)Mt * CK_M2 * nl);
-  const size_t o_rho = IN(RHO.data(), RHO.size());
-  size_t o_dN = 0, o_dg = 0, o_dni = 0, o_dx1 = 0, o_dx2 = 0, o_dy1 = 0, o_dy2 = 0, o_de = 0;
+  // ---------------- host pre-pass (O(n) + O(P) scans, no big exponentiations; threaded)
+  std::vector<uint32_t> NN((size_t)n * nn), NP1((size_t)n * nn), recv_bits(n);
+  parallel_for(n, 64, [&](size_t b0, size_t b1) {
+    for (size_t r = b0; r < b1; ++r) {
+      const Sess& x = pl.ss[sess_of_recv[r]];
+      const uint32_t* Np = x.b->recv_n + (size_t)(r - x.rbase) * x.b->nl;
+      hbn::Limbs N = hbn::from(Np, x.b->nl);
+      hbn::store(hbn::mul(N, N), NN.data() + r * nn, nn);
+      hbn::store(hbn::add_small(N, 1), NP1.data() + r * nn, nn);
+      recv_bits[r] = hbn::bitlen(Np, x.b->nl);
+    }
+  });
+  const hbn::Limbs& q3 = q_cubed();
+  std::vector<uint8_t> alice_pre(P), pdl_small(P);
+  std::vector<uint32_t> ae_bits(P);
+  struct Maxes {
+    uint32_t s1 = 1, s3 = 1, as1 = 1, as2 = 1, ae = 1;
+    bool big_s1 = false;
+  };
+  std::vector<Maxes> tmax(host_threads() + 1);
+  std::atomic<uint32_t> slot{0};
+  parallel_for(P, 1024, [&](size_t b0, size_t b1) {
+    Maxes mx;
+    for (size_t p = b0; p < b1; ++p) {
+      const Sess& x = pl.ss[sess_of_pair[p]];
+      const fsdkr_collect_batch* b = x.b;
+      const size_t lp = p - x.pbase;
+      const uint32_t* Np = b->recv_n + (size_t)(lp % x.n) * b->nl;
+      const uint32_t* s1 = b->pdl_s1 + lp * b->s1l;
+      // s1 < N -> (N+1)^s1 mod N^2 = 1 + s1*N  (binomial, bit-identical)
+      const bool small = hbn::cmp_raw(s1, b->s1l, Np, b->nl) < 0;
+      pdl_small[p] = small ? 1 : 0;
+      mx.big_s1 = mx.big_s1 || !small;
+      mx.s1 = std::max(mx.s1, hbn::bitlen(s1, b->s1l));
+      mx.s3 = std::max(mx.s3, hbn::bitlen(b->pdl_s3 + lp * b->s3l, b->s3l));
+      const uint32_t* as1 = b->rp_s1 + lp * b->s1l;
+      ae_bits[p] = hbn::bitlen(b->rp_e + lp * b->el, b->el);
+      const bool s1_ok = hbn::cmp_raw(as1, b->s1l, q3.data(), q3.size()) <= 0;
+      alice_pre[p] = (s1_ok && ae_bits[p] <= 256) ? 1 : 0;
+      if (alice_pre[p]) {  // exponents of rejected proofs are never used
+        mx.as1 = std::max(mx.as1, hbn::bitlen(as1, b->s1l));
+        mx.as2 = std::max(mx.as2, hbn::bitlen(b->rp_s2 + lp * b->s3l, b->s3l));
+        mx.ae = std::max(mx.ae, ae_bits[p]);
+      }
+    }
+    tmax[slot++ % tmax.size()] = mx;   // at most host_threads() chunks
+  });
+  Maxes mx;
+  for (const Maxes& t : tmax) {
+    mx.s1 = std::max(mx.s1, t.s1);
+    mx.s3 = std::max(mx.s3, t.s3);
+    mx.as1 = std::max(mx.as1, t.as1);
+    mx.as2 = std::max(mx.as2, t.as2);
+    mx.ae = std::max(mx.ae, t.ae);
+    mx.big_s1 = mx.big_s1 || t.big_s1;
+  }
+  clk.lap("pair scan");
+  // correct-key: rho_j = mask_generation(len(n), H(n, salt, j)) mod n; primorial gcd.
+  // ring-Pedersen modulus split N = 2^k m (even N: 2-adic half in pow2.hip); S mod m.
+  std::vector<uint32_t> RHO((size_t)Mt * CK_M2 * ckl, 0u), CKMODS((size_t)Mt * ckl, 0u), CKEXP((size_t)Mt * ckl, 0u),
+      ck_bits(Mt);
+  std::vector<uint32_t> PEDN((size_t)Mt * nl, 0u), PEDS((size_t)Mt * nl, 0u), ped_tz(Mt, 0u);
+  pl.ck_pre.assign(Mt, 0);
+  pl.ped_mode.assign(Mt, 0);
+  pl.ped_zlen.assign(Mt, M);
+  pl.ck_short.assign(Mt, 0);
+  pl.ck_one.assign(Mt, 0);
+  for (uint32_t m = 0; m < Mt; ++m) {
+    const Sess& x = pl.ss[sess_of_msg[m]];
+    const uint32_t lm = m - x.mbase;
+    if (x.b->ped_lens) {
+      if (x.b->ped_lens[2 * lm] < M) pl.ped_mode[m] = 2;   // A[i] indexed by the hash loop (:131-133)
+      pl.ped_zlen[m] = std::min(M, x.b->ped_lens[2 * lm + 1]);
+    }
+    if (x.b->ck_lens && x.b->ck_lens[lm] < CK_M2) pl.ck_short[m] = 1;
+  }
+  parallel_for(Mt, 4, [&](size_t b0, size_t b1) {
+    for (size_t m = b0; m < b1; ++m) {
+      const Sess& x = pl.ss[sess_of_msg[m]];
+      const fsdkr_collect_batch* b = x.b;
+      const size_t lm = m - x.mbase;
+      const uint32_t* ckn = b->ck_n + lm * x.ckl;
+      memcpy(CKEXP.data() + m * ckl, ckn, (size_t)x.ckl * 4);
+      uint32_t* dst = CKMODS.data() + m * ckl;
+      memcpy(dst, ckn, (size_t)x.ckl * 4);
+      ck_bits[m] = hbn::bitlen(ckn, x.ckl);
+      if (ck_bits[m] == 0) pl.ck_short[m] = 1;                  // rho = mask % 0: division by zero panics
+      const bool one = ck_bits[m] == 1;                          // n = 1: every value is 0 mod 1 -> Ok
+      const bool ok = !one && ck_bits[m] != 0 && is_odd(ckn) && !hbn::has_small_factor(ckn, x.ckl, small_primes());
+      if (one) pl.ck_one[m] = 1;
+      if (ok) {
+        const uint32_t msklen = ck_bits[m] / 256 + 1;
+        const uint32_t salt_v =
+            ((uint32_t)SALT[0] << 24) | ((uint32_t)SALT[1] << 16) | ((uint32_t)SALT[2] << 8) | SALT[3];
+        const hbn::Limbs Nl = hbn::from(ckn, x.ckl);
+        std::vector<uint32_t> mask((size_t)msklen * 8, 0);
+        for (uint32_t j = 0; j < CK_M2; ++j) {
+          Sha256 h;
+          h.init();
+          h.bigint(ckn, x.ckl);
+          absorb_u32(h, salt_v);
+          absorb_u32(h, j);
+          uint32_t seed[8];
+          h.finish_le(seed);
+          for (uint32_t k = 0; k < msklen; ++k) {
+            Sha256 hk;
+            hk.init();
+            hk.bigint(seed, 8);
+            absorb_u32(hk, k);
+            hk.finish_le(mask.data() + (size_t)k * 8);
+          }
+          hbn::store(hbn::mod(hbn::from(mask.data(), mask.size()), Nl), RHO.data() + (m * CK_M2 + j) * ckl, ckl);
+        }
+      } else {   // zero / even / smooth modulus: verdict false, placeholder modulus 3 for the kernels
+        std::fill(dst, dst + ckl, 0u);
+        dst[0] = 3;
+      }
+      pl.ck_pre[m] = ok ? 1 : 0;
+      // ring-Pedersen statement modulus N = 2^tz * (odd part)
+      const uint32_t* N = b->ped_N + lm * b->nl;
+      uint32_t* on = PEDN.data() + m * nl;
+      memcpy(on, N, (size_t)b->nl * 4);
+      uint32_t* sd = PEDS.data() + m * nl;
+      memcpy(sd, b->ped_S + lm * b->nl, (size_t)b->nl * 4);
+      if (pl.ped_mode[m] == 2 || hbn::is_zero_raw(N, b->nl)) {   // A short / modulus 0: panic before any check
+        pl.ped_mode[m] = 2;
+        std::fill(on, on + nl, 0u);
+        on[0] = 3;
+        continue;
+      }
+      const uint32_t tz = hbn::ctz_raw(N, b->nl);
+      ped_tz[m] = tz;
+      if (tz) hbn::shr_raw(on, nl, tz);
+      if (on[0] == 1 && hbn::is_zero_raw(on + 1, nl - 1)) {   // odd part 1: every congruence mod 1 holds
+        pl.ped_mode[m] = 1;
+        on[0] = 3;
+        continue;
+      }
+      // S reduced mod the odd part (the eq kernel compares canonical residues of
+      // A*S; the reference reduces S^e mod N itself, ring_pedersen_proof.rs:147)
+      if (hbn::cmp_raw(sd, nl, on, nl) >= 0) hbn::store(hbn::mod(hbn::from(sd, nl), hbn::from(on, nl)), sd, nl);
+    }
+  });
+  clk.lap("ck rho+primes");
+  // DLog statements: N > 2^128, gcd(g, N) = gcd(ni, N) = 1, x < N; challenges e = H(x, g, N, ni)
+  pl.dlog_pre.assign(J, 0);
+  pl.dlog_trivial.assign(J, 0);
+  std::vector<uint32_t> DE((size_t)J * 2 * 8), DLOGN((size_t)J * nl, 0u), dlog_tz(J, 0u);
+  parallel_for(J, 2, [&](size_t b0, size_t b1) {
+    for (size_t j = b0; j < b1; ++j) {
+      const Sess& x = pl.ss[sess_of_join[j]];
+      const fsdkr_collect_batch* b = x.b;
+      const size_t lj = j - x.jbase, w = b->nl;
+      const uint32_t *N = b->dlog_N + lj * w, *g = b->dlog_g + lj * w, *ni = b->dlog_ni + lj * w;
+      const uint32_t bl = hbn::bitlen(N, w);
+      bool ok = bl > 129 || (bl == 129 && !(N[4] == 1 && hbn::is_zero_raw(N, 4)));
+      ok = ok && hbn::gcd_is_one(g, w, N, w) && hbn::gcd_is_one(ni, w, N, w);
+      uint8_t pre = 0;
+      if (ok && hbn::cmp_raw(b->dlog_x1 + lj * w, w, N, w) < 0) pre |= 1;
+      if (ok && hbn::cmp_raw(b->dlog_x2 + lj * w, w, N, w) < 0) pre |= 2;
+      pl.dlog_pre[j] = pre;
+      for (int which = 0; which < 2; ++which) {
+        const uint32_t* xx = (which == 0 ? b->dlog_x1 : b->dlog_x2) + lj * w;
+        const uint32_t* gg = which == 0 ? g : ni;
+        const uint32_t* nn_ = which == 0 ? ni : g;
+        Sha256 h;
+        h.init();
+        h.bigint(xx, w);
+        h.bigint(gg, w);
+        h.bigint(N, w);
+        h.bigint(nn_, w);
+        h.finish_le(DE.data() + (j * 2 + which) * 8);
+      }
+      uint32_t* on = DLOGN.data() + j * nl;
+      memcpy(on, N, w * 4);
+      if (!ok) {   // the checks fail before any exponentiation: placeholder modulus
+        std::fill(on, on + nl, 0u);
+        on[0] = 3;
+        continue;
+      }
+      const uint32_t tz = hbn::ctz_raw(N, w);
+      dlog_tz[j] = tz;
+      if (tz) hbn::shr_raw(on, nl, tz);
+      if (on[0] == 1 && hbn::is_zero_raw(on + 1, nl - 1)) {
+        pl.dlog_trivial[j] = 1;
+        on[0] = 3;
+      }
+    }
+  });
+  // exponent-length bounds
+  uint32_t z_max = 1, y_max = 1, ckn_max = 1, recvn_max = 1;
+  for (uint32_t s = 0; s < count; ++s) {
+    const Sess& x = pl.ss[s];
+    const fsdkr_collect_batch* b = x.b;
+    for (size_t k = 0; k < (size_t)x.Mt * M; ++k) z_max = std::max(z_max, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
+    for (uint32_t j = 0; j < x.J; ++j) {
+      y_max = std::max(y_max, hbn::bitlen(b->dlog_y1 + (size_t)j * b->yl, b->yl));
+      y_max = std::max(y_max, hbn::bitlen(b->dlog_y2 + (size_t)j * b->yl, b->yl));
+    }
+  }
+  for (uint32_t m = 0; m < Mt; ++m)
+    if (pl.ck_pre[m]) ckn_max = std::max(ckn_max, ck_bits[m]);
+  for (uint32_t r = 0; r < n; ++r) recvn_max = std::max(recvn_max, recv_bits[r]);
+  // Feldman share checks: per pair (commitment offset, count, index)
+  std::vector<FeldmanInfo> finfo(P);
+  for (uint32_t s = 0; s < count; ++s) {
+    const Sess& x = pl.ss[s];
+    uint32_t voff = x.vbase;
+    for (uint32_t k = 0; k < x.R; ++k) {
+      const uint32_t nc = ncoef_of(x.b, k);
+      for (uint32_t i = 0; i < x.n; ++i) finfo[x.pbase + (size_t)k * x.n + i] = {voff, nc, i + 1, 0};
+      voff += nc;
+    }
+  }
+  clk.lap("dlog+maxes");
+
+  // ---------------- device layout: inputs (planned; bytes written after the device allocation)
+  Img I;
+  using B = fsdkr_collect_batch;
+  // merged field: the rows of every session at the merged width W
+  auto field = [&](const uint32_t* B::*f, auto rows_of, auto width_of, uint32_t W) {
+    size_t tot = 0;
+    for (const Sess& x : pl.ss) tot += rows_of(x);
+    const size_t o = I.reserve(tot * W * 4);
+    size_t r = 0;
+    for (const Sess& x : pl.ss) {
+      const size_t rows = rows_of(x);
+      I.rows_at(o + r * W * 4, x.b->*f, rows, width_of(x), W);
+      r += rows;
+    }
+    return o;
+  };
+  auto R_recv = [](const Sess& x) { return (size_t)x.n; };
+  auto R_pair = [](const Sess& x) { return (size_t)x.P; };
+  auto R_join = [](const Sess& x) { return (size_t)x.J; };
+  auto W_nl = [](const Sess& x) { return x.b->nl; };
+  auto W_nn = [](const Sess& x) { return 2 * x.b->nl; };
+  auto W_16 = [](const Sess&) { return 16u; };
+  auto W_s1 = [](const Sess& x) { return x.b->s1l; };
+  auto W_s3 = [](const Sess& x) { return x.b->s3l; };
+  auto W_el = [](const Sess& x) { return x.b->el; };
+  auto W_yl = [](const Sess& x) { return x.b->yl; };
+  const size_t o_rn = field(&B::recv_n, R_recv, W_nl, nl), o_rt = field(&B::recv_ntilde, R_recv, W_nl, nl);
+  const size_t o_h1 = field(&B::recv_h1, R_recv, W_nl, nl), o_h2 = field(&B::recv_h2, R_recv, W_nl, nl);
+  const size_t o_NN = I.own(NN), o_NP1 = I.own(NP1);
+  const size_t o_enc = field(&B::enc, R_pair, W_nn, nn), o_Q = field(&B::commit, R_pair, W_16, 16);
+  const size_t o_pz = field(&B::pdl_z, R_pair, W_nl, nl), o_pu1 = field(&B::pdl_u1, R_pair, W_16, 16);
+  const size_t o_pu2 = field(&B::pdl_u2, R_pair, W_nn, nn), o_pu3 = field(&B::pdl_u3, R_pair, W_nl, nl);
+  const size_t o_ps1 = field(&B::pdl_s1, R_pair, W_s1, s1l), o_ps2 = field(&B::pdl_s2, R_pair, W_nl, nl);
+  const size_t o_ps3 = field(&B::pdl_s3, R_pair, W_s3, s3l);
+  const size_t o_az = field(&B::rp_z, R_pair, W_nl, nl), o_ae = field(&B::rp_e, R_pair, W_el, el);
+  const size_t o_as = field(&B::rp_s, R_pair, W_nl, nl), o_as1 = field(&B::rp_s1, R_pair, W_s1, s1l);
+  const size_t o_as2 = field(&B::rp_s2, R_pair, W_s3, s3l);
+  const size_t o_vss = I.reserve((size_t)V * 64);
+  for (const Sess& x : pl.ss) I.rows_at(o_vss + (size_t)x.vbase * 64, x.b->vss, x.V, 16, 16);
+  const size_t o_pSraw = I.reserve((size_t)Mt * nl * 4), o_pT = I.reserve((size_t)Mt * nl * 4);
+  const size_t o_pA = I.reserve((size_t)Mt * M * nl * 4), o_pZ = I.reserve((size_t)Mt * M * zl * 4);
+  for (const Sess& x : pl.ss) {
+    I.rows_at(o_pSraw + (size_t)x.mbase * nl * 4, x.b->ped_S, x.Mt, x.b->nl, nl);
+    I.rows_at(o_pT + (size_t)x.mbase * nl * 4, x.b->ped_T, x.Mt, x.b->nl, nl);
+    I.rows_at(o_pA + (size_t)x.mbase * M * nl * 4, x.b->ped_A, (size_t)x.Mt * M, x.b->nl, nl);
+    I.rows_at(o_pZ + (size_t)x.mbase * M * zl * 4, x.b->ped_Z, (size_t)x.Mt * M, x.b->zl, zl);
+  }
+  const size_t o_pS = I.own(PEDS);
+  const size_t o_cks = I.reserve((size_t)Mt * CK_M2 * ckl * 4);
+  for (const Sess& x : pl.ss)
+    I.rows_at(o_cks + (size_t)x.mbase * CK_M2 * ckl * 4, x.b->ck_sigma, (size_t)x.Mt * CK_M2, x.ckl, ckl);
+  const size_t o_ckn = I.own(CKEXP);          // exponent: the caller's ek.n
+  const size_t o_ckmods = I.own(CKMODS);      // modulus: ek.n, or placeholder 3 where the verdict is forced
+  const size_t o_rho = I.own(RHO);
+  size_t o_dg = 0, o_dni = 0, o_dx1 = 0, o_dx2 = 0, o_dy1 = 0, o_dy2 = 0, o_de = 0;
   if (J) {
-    o_dN = IN(b->dlog_N, (size_t)J * nl);
-    o_dg = IN(b->dlog_g, (size_t)J * nl);
-    o_dni = IN(b->dlog_ni, (size_t)J * nl);
-    o_dx1 = IN(b->dlog_x1, (size_t)J * nl);
-    o_dx2 = IN(b->dlog_x2, (size_t)J * nl);
-    o_dy1 = IN(b->dlog_y1, (size_t)J * b->yl);
-    o_dy2 = IN(b->dlog_y2, (size_t)J * b->yl);
-    o_de = IN(DE.data(), DE.size());
+    o_dg = field(&B::dlog_g, R_join, W_nl, nl);
+    o_dni = field(&B::dlog_ni, R_join, W_nl, nl);
+    o_dx1 = field(&B::dlog_x1, R_join, W_nl, nl);
+    o_dx2 = field(&B::dlog_x2, R_join, W_nl, nl);
+    o_dy1 = field(&B::dlog_y1, R_join, W_yl, yl);
+    o_dy2 = field(&B::dlog_y2, R_join, W_yl, yl);
+    o_de = I.own(DE);
   }
-  std::vector<uint32_t> ONE(nn, 0);
+  std::vector<uint32_t> ONE(std::max(nn, ckl), 0);
   ONE[0] = 1;
-  const size_t o_one = IN(ONE.data(), nn);
-  // nl-width moduli table: Ntilde_i | ped_N | ck_n | dlog_N   (mod_setup reads [cnt][nl])
-  std::vector<uint32_t> MODS((size_t)(n + 2 * Mt + J) * nl);
-  memcpy(MODS.data(), b->recv_ntilde, (size_t)n * nl * 4);
-  memcpy(MODS.data() + (size_t)n * nl, b->ped_N, (size_t)Mt * nl * 4);
-  for (uint32_t m = 0; m < Mt; ++m) {  // even / zero correct-key moduli: placeholder 3 (verdict forced false)
-    uint32_t* dst = MODS.data() + (size_t)(n + Mt + m) * nl;
-    memcpy(dst, b->ck_n + (size_t)m * nl, nl * 4);
-    if (!is_odd(dst)) {
-      std::fill(dst, dst + nl, 0u);
-      dst[0] = 3;
-      ck_pre[m] = 0;
-    }
+  const size_t o_one = I.own(ONE);
+  // nl-width moduli table: Ntilde_i | ring-Pedersen N (odd part) | DLog N (odd part)
+  const uint32_t n_mods_nl = n + Mt + J;
+  const size_t o_mods = I.reserve((size_t)n_mods_nl * nl * 4);
+  for (const Sess& x : pl.ss) I.rows_at(o_mods + (size_t)x.rbase * nl * 4, x.b->recv_ntilde, x.n, x.b->nl, nl);
+  {
+    std::vector<uint8_t> tail(((size_t)Mt + J) * nl * 4);
+    memcpy(tail.data(), PEDN.data(), (size_t)Mt * nl * 4);
+    if (J) memcpy(tail.data() + (size_t)Mt * nl * 4, DLOGN.data(), (size_t)J * nl * 4);
+    I.own_at(o_mods + (size_t)n * nl * 4, std::move(tail));
   }
-  if (J) memcpy(MODS.data() + (size_t)(n + 2 * Mt) * nl, b->dlog_N, (size_t)J * nl * 4);
-  const uint32_t n_mods_nl = n + 2 * Mt + J;
-  const size_t o_mods = IN(MODS.data(), MODS.size());
+  const size_t o_finfo = I.own(finfo);
+  clk.lap("layout plan");
 
-  // ---------------- device layout: outputs
-  const size_t x_epdl = L.out((size_t)P * 8 * 4);
-  const size_t x_pbits = L.out((size_t)Mt * ((M + 31) / 32) * 4), x_ppanic = L.out((size_t)Mt * 4);
-  const size_t x_Bpdl = L.out((size_t)P * nn * 4), x_gs1 = L.out((size_t)P * nn * 4);
-  // modexp outputs, laid out per merged launch (instance k of a launch writes slot k):
-  //   GA (nn, long)  = J1 s2^N | s^N  [2P]  ++  J9 (N+1)^s1 for s1 >= N  [<= P]
+  // ---------------- device layout: outputs (offsets relative to the output region)
+  size_t out_bytes = 0;
+  auto OUT = [&](size_t bytes) {
+    const size_t o = Img::al(out_bytes);
+    out_bytes = o + Img::al(bytes ? bytes : 1);
+    return o;
+  };
+  const size_t x_epdl = OUT((size_t)P * 8 * 4);
+  const size_t x_pbits = OUT((size_t)Mt * MW * 4), x_ppanic = OUT((size_t)Mt * 4);
+  const size_t x_Bpdl = OUT((size_t)P * nn * 4), x_gs1 = OUT((size_t)P * nn * 4);
+  //   GA (nn, long)  = s2^N | s^N  [2P]  ++  (N+1)^s1 for s1 >= N  [<= P]
   //   J2 (nn, short) = c^e_pdl | c^e_A  [2P]
   //   J5 (nl, short) = z^e_pdl | zA^e_A [2P]
-  //   GD (nl, long)  = J7 g^y1 | ni^y2 [2J] ++ J6 sigma^n [Mt*11] ++ J8 ni^e1 | g^e2 [2J]
-  //   FB (nl, fixed bases h1_i, h2_i, T_m; any slot) = J4 h2^s3 | h2^s2A [2P], J3 h1^s1 | h1^s1A [2P],
-  //                    RP T^Z [Mt*M]
-  const size_t x_GA = L.out((size_t)3 * P * nn * 4 + 4);
+  //   GD (nl, long)  = g^y1 | ni^y2 [2J] ++ ni^e1 | g^e2 [2J]
+  //   GC (ckl)       = sigma^n [Mt*11]
+  //   FB (nl, fixed bases h1_i, h2_i, T_m) = h2^s3 | h2^s2A [2P], h1^s1 | h1^s1A [2P], T^Z [Mt*M]
+  const size_t x_GA = OUT((size_t)3 * P * nn * 4 + 4);
   const size_t x_J1 = x_GA, x_J9 = x_GA + (size_t)2 * P * nn * 4;
-  const size_t x_J2 = L.out((size_t)2 * P * nn * 4);
-  const size_t x_J5 = L.out((size_t)2 * P * nl * 4);
-  const size_t x_GD = L.out(((size_t)4 * J + (size_t)Mt * CK_M2 + 1) * nl * 4);
-  const size_t x_J7 = x_GD, x_J6 = x_J7 + (size_t)2 * J * nl * 4, x_J8 = x_J6 + (size_t)Mt * CK_M2 * nl * 4;
-  const size_t x_FB = L.out(((size_t)4 * P + (size_t)Mt * M + 1) * nl * 4);
+  const size_t x_J2 = OUT((size_t)2 * P * nn * 4);
+  const size_t x_J5 = OUT((size_t)2 * P * nl * 4);
+  const size_t x_GD = OUT(((size_t)4 * J + 1) * nl * 4);
+  const size_t x_J7 = x_GD, x_J8 = x_J7 + (size_t)2 * J * nl * 4;
+  const size_t x_GC = OUT(((size_t)Mt * CK_M2 + 1) * ckl * 4);
+  const size_t x_FB = OUT(((size_t)4 * P + (size_t)Mt * M + 1) * nl * 4);
   const size_t x_J4 = x_FB, x_J3 = x_J4 + (size_t)2 * P * nl * 4, x_RP = x_J3 + (size_t)2 * P * nl * 4;
-  const size_t x_invc = L.out((size_t)2 * P * nn * 4), x_invz = L.out((size_t)P * nl * 4);
-  const size_t x_unn = L.out((size_t)2 * P * 4);    // unit flags of the nn inverses (c^eA, then extra c^e_pdl)
-  const size_t x_uzA = L.out((size_t)P * 4), x_uzp = L.out((size_t)P * 4);
-  const size_t x_eq2 = L.out((size_t)P * 4);
-  const size_t n_eqnl = (size_t)P + (size_t)Mt * M + (size_t)Mt * CK_M2 + 2 * J;
-  const size_t x_eq3 = L.out(n_eqnl * 4);           // [u3 P | RP Mt*M | CK Mt*11 | DLog 2J]
-  const size_t x_u = L.out((size_t)P * nn * 4), x_w = L.out((size_t)P * nl * 4);
-  const size_t x_fel = L.out(P), x_pdlv = L.out(P), x_rng = L.out(P);
+  const size_t x_invc = OUT((size_t)2 * P * nn * 4), x_invz = OUT((size_t)P * nl * 4);
+  const size_t x_unn = OUT((size_t)2 * P * 4);
+  const size_t x_uzA = OUT((size_t)P * 4), x_uzp = OUT((size_t)P * 4);
+  const size_t x_eq2 = OUT((size_t)P * 4);
+  const size_t n_eqnl = (size_t)P + (size_t)Mt * M + 2 * (size_t)J;
+  const size_t x_eq3 = OUT(n_eqnl * 4);               // [u3 P | RP Mt*M | DLog 2J]
+  const size_t x_eqck = OUT((size_t)Mt * CK_M2 * 4);
+  const size_t x_u = OUT((size_t)P * nn * 4), x_w = OUT((size_t)P * nl * 4);
+  const size_t x_fel = OUT(P), x_pdlv = OUT(P), x_rng = OUT(P);
+  // 2-adic checks of even moduli
+  uint32_t n_p2 = 0;
+  pl.ped_p2_first.assign(Mt, ~0u);
+  pl.dlog_p2_first.assign(J, ~0u);
+  for (uint32_t m = 0; m < Mt; ++m)
+    if (ped_tz[m] && pl.ped_mode[m] != 2) {
+      pl.ped_p2_first[m] = n_p2;
+      n_p2 += M;
+    }
+  for (uint32_t j = 0; j < J; ++j)
+    if (dlog_tz[j] && pl.dlog_pre[j]) {
+      pl.dlog_p2_first[j] = n_p2;
+      n_p2 += 2;
+    }
+  const size_t x_p2 = OUT((size_t)n_p2 * 4);
 
-  // single device allocation: [inputs | descriptors | outputs]; descriptors are
-  // appended to the input image below once the device base address is known.
-  const size_t in_bytes_pre = L.host.size();
-  // upper bound of descriptor bytes
-  const size_t n_inst_nn = 2 * P + 2 * P + (any_big_s1 ? P : 0);
-  const size_t n_inst_nl = 2 * P * 3 + (size_t)Mt * (M + CK_M2) + 4 * J;
-  const size_t desc_bound = (n_inst_nn + n_inst_nl) * 32 + 16 * 256 +
-                            ((size_t)P + (size_t)Mt * M + (size_t)Mt * CK_M2 + 2 * J + P) * sizeof(EqOperand) +
-                            2 * (size_t)P * sizeof(Prod3Operand) + (size_t)(2 * P + 2 * P) * 16 + (size_t)4 * P * 8 +
-                            (size_t)(2 * P + 2 * P) * 4 + (size_t)(3 * n + Mt) * 32 + 64 * 1024;
-  const size_t total = Layout::al(in_bytes_pre + desc_bound) + L.out_bytes;
+  // single device allocation: [inputs | descriptors | outputs]
+  const size_t in_bytes_pre = Img::al(I.size);
+  const size_t n_eqall = (size_t)P + n_eqnl + (size_t)Mt * CK_M2;
+  const size_t desc_bound =
+      ((size_t)7 * P + 4 * (size_t)J + (size_t)Mt * CK_M2) * 32 +                        // modexp jobs
+      (2 * (size_t)n + Mt) * 24 + (4 * (size_t)P + (size_t)Mt * M) * 32 + 24 * 512 +      // fixed-base job
+      4 * (size_t)P * 8 + 4 * (size_t)P * 16 +                                            // binom, inverses
+      n_eqall * (sizeof(EqOperand) + 4) + 2 * (size_t)P * sizeof(Prod3Operand) + 4 * (size_t)P +
+      2 * (size_t)P * 8 + P + (size_t)n_p2 * sizeof(Pow2Op) + 32 * 256 + 64 * 1024;
+  const size_t out_off = Img::al(in_bytes_pre + desc_bound);
+  const size_t total = out_off + out_bytes;
   uint8_t* dev = (uint8_t*)c->buf("collect_arena", total);
   if (!dev) {
     c->fail("fsdkr_verify_collect: device allocation of %zu bytes failed", total);
     return FSDKR_E_OOM;
   }
-  uint8_t* const out_base = dev + Layout::al(in_bytes_pre + desc_bound);
-  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };          // input address
-  auto DX = [&](size_t o) { return (uint64_t)(uintptr_t)(out_base + o); };     // output address
-  auto PX = [&](size_t o) { return (uint32_t*)(out_base + o); };
-  auto PI = [&](size_t o) { return (const uint32_t*)(dev + o); };
+  uint8_t* const out_base = dev + out_off;
+  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };        // input address
+  auto DX = [&](size_t o) { return (uint64_t)(uintptr_t)(out_base + o); };   // output address
 
-  // ---------------- modexp jobs
-  ModexpJob J1, J2, J5, J6, J7, J8, J9;
+  // ---------------- modexp jobs (descriptors addressed into the image)
+  ModexpJob J1, J2, J5, J7, J8, J9, GC;
   J1.k32 = J2.k32 = J9.k32 = nn;
-  J5.k32 = J6.k32 = J7.k32 = J8.k32 = nl;
-  // receiver bases h1_i, h2_i (mod N~_i = nl-table row i) and ring-Pedersen T_m (row n + m):
-  // shared by 2n resp. M exponents -> BGMW tables (fixedbase.hip)
+  J5.k32 = J7.k32 = J8.k32 = nl;
+  GC.k32 = ckl;
   FbJob& FB = pl.fb;
   FB = FbJob();
   FB.k32 = nl;
   std::vector<uint32_t> fb_h1(n), fb_h2(n);
-  for (uint32_t i = 0; i < n; ++i) {
-    fb_h1[i] = FB.add_base(DI(o_h1 + (size_t)i * nl * 4), nl, i);
-    fb_h2[i] = FB.add_base(DI(o_h2 + (size_t)i * nl * 4), nl, i);
+  for (uint32_t r = 0; r < n; ++r) {
+    fb_h1[r] = FB.add_base(DI(o_h1 + (size_t)r * nl * 4), nl, r);
+    fb_h2[r] = FB.add_base(DI(o_h2 + (size_t)r * nl * 4), nl, r);
   }
   for (uint32_t m = 0; m < Mt; ++m) FB.add_base(DI(o_pT + (size_t)m * nl * 4), nl, n + m);
-  std::vector<uint32_t> j9_pairs;
+  std::vector<uint32_t> j9_index(P, 0xFFFFFFFFu);
   for (int which = 0; which < 2; ++which)
     for (uint32_t p = 0; p < P; ++p) {
-      const uint32_t i = p % n;
-      const uint64_t Ni = DI(o_rn + (size_t)i * nl * 4);
+      const uint32_t r = recv_of_pair[p];
+      const uint64_t Ni = DI(o_rn + (size_t)r * nl * 4);
       // J1: s2^N (PDL, zk_pdl_with_slack.rs:129-135) | s^N (Alice, range_proofs.rs:148)
-      J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, i);
+      J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
       const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
-      if (which == 0) J2.add(cp, nn, DX(x_epdl + (size_t)p * 32), 8, 256, i);
-      else J2.add(cp, nn, DI(o_ae + (size_t)p * b->el * 4), b->el, a_e_max, i);
+      if (which == 0) J2.add(cp, nn, DX(x_epdl + (size_t)p * 32), 8, 256, r);
+      else J2.add(cp, nn, DI(o_ae + (size_t)p * el * 4), el, mx.ae, r);
       // fixed bases (FB): h1^s1 -> J3 slot | h2^s3 (s2 for Alice) -> J4 slot;  J5: z^e
       const size_t slot = (size_t)which * P + p;
       if (which == 0) {
-        FB.add(fb_h1[i], DI(o_ps1 + (size_t)p * b->s1l * 4), b->s1l, pdl_s1_max, DX(x_J3 + slot * nl * 4));
-        FB.add(fb_h2[i], DI(o_ps3 + (size_t)p * b->s3l * 4), b->s3l, pdl_s3_max, DX(x_J4 + slot * nl * 4));
-        J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DX(x_epdl + (size_t)p * 32), 8, 256, i);
+        FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
+        FB.add(fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4));
+        J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DX(x_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
-        FB.add(fb_h1[i], DI(o_as1 + (size_t)p * b->s1l * 4), use ? b->s1l : 0, a_s1_max, DX(x_J3 + slot * nl * 4));
-        FB.add(fb_h2[i], DI(o_as2 + (size_t)p * b->s3l * 4), use ? b->s3l : 0, a_s2_max, DX(x_J4 + slot * nl * 4));
-        J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * b->el * 4), use ? b->el : 0, a_e_max, i);
+        FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
+        FB.add(fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2, DX(x_J4 + slot * nl * 4));
+        J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
       }
     }
   for (uint32_t p = 0; p < P; ++p)
     if (!pdl_small[p]) {
-      const uint32_t i = p % n;
-      J9.add(DI(o_NP1 + (size_t)i * nn * 4), nn, DI(o_ps1 + (size_t)p * b->s1l * 4), b->s1l, pdl_s1_max, i);
-      j9_pairs.push_back(p);
+      const uint32_t r = recv_of_pair[p];
+      j9_index[p] = (uint32_t)J9.size();
+      J9.add(DI(o_NP1 + (size_t)r * nn * 4), nn, DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, r);
     }
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k)  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144)
-      FB.add(2 * n + m, DI(o_pZ + ((size_t)m * M + k) * b->zl * 4), b->zl, z_max, DX(x_RP + ((size_t)m * M + k) * nl * 4));
+      FB.add(2 * n + m, DI(o_pZ + ((size_t)m * M + k) * zl * 4), zl, z_max,
+             DX(x_RP + ((size_t)m * M + k) * nl * 4));
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < CK_M2; ++k)  // correct-key sigma_k^n mod n
-      J6.add(DI(o_cks + ((size_t)m * CK_M2 + k) * nl * 4), nl, DI(o_ckn + (size_t)m * nl * 4), nl,
-             std::max(ckn_max, z_max), n + Mt + m);
+      GC.add(DI(o_cks + ((size_t)m * CK_M2 + k) * ckl * 4), ckl, DI(o_ckn + (size_t)m * ckl * 4), ckl,
+             pl.ck_pre[m] ? ckn_max : 0u, m);
   for (uint32_t j = 0; j < J; ++j) {
-    const uint32_t mi = n + 2 * Mt + j;
-    J7.add(DI(o_dg + (size_t)j * nl * 4), nl, DI(o_dy1 + (size_t)j * b->yl * 4), b->yl, y_max, mi);
-    J7.add(DI(o_dni + (size_t)j * nl * 4), nl, DI(o_dy2 + (size_t)j * b->yl * 4), b->yl, y_max, mi);
+    const uint32_t mi = n + Mt + j;
+    J7.add(DI(o_dg + (size_t)j * nl * 4), nl, DI(o_dy1 + (size_t)j * yl * 4), yl, y_max, mi);
+    J7.add(DI(o_dni + (size_t)j * nl * 4), nl, DI(o_dy2 + (size_t)j * yl * 4), yl, y_max, mi);
     J8.add(DI(o_dni + (size_t)j * nl * 4), nl, DI(o_de + (size_t)(2 * j) * 32), 8, 256, mi);
     J8.add(DI(o_dg + (size_t)j * nl * 4), nl, DI(o_de + (size_t)(2 * j + 1) * 32), 8, 256, mi);
   }
-  // descriptor images appended to the input image
+  // descriptor image, placed right after the inputs (desc_base is 256-aligned, so
+  // alignment inside `desc` carries over to device addresses)
+  std::vector<uint8_t> desc;
+  const size_t desc_base = in_bytes_pre;
+  auto D_al = [&]() {
+    desc.resize(Img::al(desc.size()), 0);
+    return desc_base + desc.size();
+  };
   auto pack_job = [&](const ModexpJob& j) {
-    const size_t o = Layout::al(L.host.size());
-    L.host.resize(o);
-    j.pack(L.host);
+    const size_t o = D_al();
+    j.pack(desc);
+    return o;
+  };
+  auto put = [&](const void* src, size_t bytes) {
+    const size_t o = D_al();
+    const size_t at = desc.size();
+    desc.resize(at + bytes);
+    if (bytes) memcpy(desc.data() + at, src, bytes);
     return o;
   };
   ModexpJob GA = J1, GD = J7;
   GA.append(J9);
-  GD.append(J6);
   GD.append(J8);
-  const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD);
+  const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD),
+               d_GC = pack_job(GC);
   FB.finalize();
-  const size_t d_FB = Layout::al(L.host.size());
-  {
-    std::vector<uint8_t> img;
-    FB.pack(img);
-    L.host.resize(d_FB);
-    L.host.insert(L.host.end(), img.begin(), img.end());
-  }
-
+  FB.pack(desc);   // FbJob offsets are positions in `desc`, i.e. relative to desc_base
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N
   std::vector<uint64_t> bs_ptr(2 * (size_t)P), bn_ptr(2 * (size_t)P);
   for (uint32_t p = 0; p < P; ++p) {
-    const uint32_t i = p % n;
-    bs_ptr[p] = DI(o_ps1 + (size_t)p * b->s1l * 4);
-    bs_ptr[P + p] = DI(o_as1 + (size_t)p * b->s1l * 4);
-    bn_ptr[p] = bn_ptr[P + p] = DI(o_rn + (size_t)i * nl * 4);
+    bs_ptr[p] = DI(o_ps1 + (size_t)p * s1l * 4);
+    bs_ptr[P + p] = DI(o_as1 + (size_t)p * s1l * 4);
+    bn_ptr[p] = bn_ptr[P + p] = DI(o_rn + (size_t)recv_of_pair[p] * nl * 4);
   }
-  const size_t d_bs = L.in_vecT(bs_ptr), d_bn = L.in_vecT(bn_ptr);
+  const size_t d_bs = put(bs_ptr.data(), bs_ptr.size() * 8), d_bn = put(bn_ptr.data(), bn_ptr.size() * 8);
   // inverse descriptors: nn: c^eA (Alice; also the PDL unit test of c when eA != 0) + c^e_pdl (eA == 0)
-  std::vector<uint64_t> inv_y_nn, inv_m_nn, inv_y_nl, inv_m_nl;
-  std::vector<uint32_t>& cpdl_extra = pl.cpdl_extra;  // pairs whose PDL c unit test needs its own inverse
+  std::vector<uint64_t> inv_y_nn, inv_m_nn, inv_y_nl(2 * (size_t)P), inv_m_nl(2 * (size_t)P);
+  std::vector<uint32_t>& cpdl_extra = pl.cpdl_extra;
   cpdl_extra.clear();
+  inv_y_nn.reserve(2 * (size_t)P);
+  inv_m_nn.reserve(2 * (size_t)P);
   for (uint32_t p = 0; p < P; ++p) {
     inv_y_nn.push_back(DX(x_J2 + ((size_t)P + p) * nn * 4));
-    inv_m_nn.push_back(DI(o_NN + (size_t)(p % n) * nn * 4));
+    inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
   }
   for (uint32_t p = 0; p < P; ++p)
     if (ae_bits[p] == 0 || !alice_pre[p]) {  // c^eA does not witness c's unit-ness
       inv_y_nn.push_back(DX(x_J2 + (size_t)p * nn * 4));
-      inv_m_nn.push_back(DI(o_NN + (size_t)(p % n) * nn * 4));
+      inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
       cpdl_extra.push_back(p);
     }
   for (uint32_t p = 0; p < P; ++p) {  // zA^eA (value) then z^e_pdl (unit test)
-    inv_y_nl.push_back(DX(x_J5 + ((size_t)P + p) * nl * 4));
-    inv_m_nl.push_back(DI(o_rt + (size_t)(p % n) * nl * 4));
+    const uint64_t mt = DI(o_rt + (size_t)recv_of_pair[p] * nl * 4);
+    inv_y_nl[p] = DX(x_J5 + ((size_t)P + p) * nl * 4);
+    inv_m_nl[p] = mt;
+    inv_y_nl[P + p] = DX(x_J5 + (size_t)p * nl * 4);
+    inv_m_nl[P + p] = mt;
   }
-  for (uint32_t p = 0; p < P; ++p) {
-    inv_y_nl.push_back(DX(x_J5 + (size_t)p * nl * 4));
-    inv_m_nl.push_back(DI(o_rt + (size_t)(p % n) * nl * 4));
-  }
-  const size_t d_iynn = L.in_vecT(inv_y_nn), d_imnn = L.in_vecT(inv_m_nn);
-  const size_t d_iynl = L.in_vecT(inv_y_nl), d_imnl = L.in_vecT(inv_m_nl);
+  const size_t d_iynn = put(inv_y_nn.data(), inv_y_nn.size() * 8), d_imnn = put(inv_m_nn.data(), inv_m_nn.size() * 8);
+  const size_t d_iynl = put(inv_y_nl.data(), inv_y_nl.size() * 8), d_imnl = put(inv_m_nl.data(), inv_m_nl.size() * 8);
   // eq_check descriptors
-  std::vector<EqOperand> eq_nn, eq_nl;
-  std::vector<uint32_t> eq_nn_mod, eq_nl_mod;
-  std::vector<uint32_t> j9_index(P, 0xFFFFFFFFu);
-  for (size_t k = 0; k < j9_pairs.size(); ++k) j9_index[j9_pairs[k]] = (uint32_t)k;
+  std::vector<EqOperand> eq_nn(P), eq_nl, eq_ck;
+  std::vector<uint32_t> eq_nn_mod(P), eq_nl_mod, eq_ck_mod;
   for (uint32_t p = 0; p < P; ++p) {  // PDL u2: (N+1)^s1 * s2^N == u2 * c^e  (mod N^2), u2 < N^2
-    EqOperand e;
+    EqOperand& e = eq_nn[p];
     e.a = pdl_small[p] ? DX(x_Bpdl + (size_t)p * nn * 4) : DX(x_J9 + (size_t)j9_index[p] * nn * 4);
-    e.a_len = nn;
     e.b = DX(x_J1 + (size_t)p * nn * 4);
-    e.b_len = nn;
     e.c = DI(o_pu2 + (size_t)p * nn * 4);
-    e.c_len = nn;
     e.d = DX(x_J2 + (size_t)p * nn * 4);
-    e.d_len = nn;
+    e.a_len = e.b_len = e.c_len = e.d_len = nn;
     e.sel = 0xFFFFFFFFu;
     e.flags = 1;
-    eq_nn.push_back(e);
-    eq_nn_mod.push_back(p % n);
+    eq_nn_mod[p] = recv_of_pair[p];
   }
+  eq_nl.reserve(n_eqnl);
+  eq_nl_mod.reserve(n_eqnl);
   for (uint32_t p = 0; p < P; ++p) {  // PDL u3: h1^s1 * h2^s3 == u3 * z^e  (mod N~), u3 < N~
     EqOperand e;
     e.a = DX(x_J3 + (size_t)p * nl * 4);
@@ -508,36 +819,23 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     e.sel = 0xFFFFFFFFu;
     e.flags = 1;
     eq_nl.push_back(e);
-    eq_nl_mod.push_back(p % n);
+    eq_nl_mod.push_back(recv_of_pair[p]);
   }
   for (uint32_t m = 0; m < Mt; ++m)
-    for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N)
+    for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N; the odd part here)
       EqOperand e;
       e.a = DX(x_RP + ((size_t)m * M + k) * nl * 4);
       e.b = DI(o_one);
       e.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
       e.d = DI(o_pS + (size_t)m * nl * 4);
       e.a_len = e.b_len = e.c_len = e.d_len = nl;
-      e.sel = m * M + k;
+      e.sel = m * MW * 32 + k;
       e.flags = 0;
       eq_nl.push_back(e);
       eq_nl_mod.push_back(n + m);
     }
-  for (uint32_t m = 0; m < Mt; ++m)
-    for (uint32_t k = 0; k < CK_M2; ++k) {  // correct key: sigma^n == rho (mod n)
-      EqOperand e;
-      e.a = DX(x_J6 + ((size_t)m * CK_M2 + k) * nl * 4);
-      e.b = DI(o_one);
-      e.c = DI(o_rho + ((size_t)m * CK_M2 + k) * nl * 4);
-      e.d = DI(o_one);
-      e.a_len = e.b_len = e.c_len = e.d_len = nl;
-      e.sel = 0xFFFFFFFFu;
-      e.flags = 0;
-      eq_nl.push_back(e);
-      eq_nl_mod.push_back(n + Mt + m);
-    }
   for (uint32_t j = 0; j < J; ++j)
-    for (int which = 0; which < 2; ++which) {  // DLog: g^y * ni^e == x (mod N), x < N
+    for (int which = 0; which < 2; ++which) {  // DLog: g^y * ni^e == x (mod N; x < N checked on the host)
       EqOperand e;
       e.a = DX(x_J7 + ((size_t)2 * j + which) * nl * 4);
       e.b = DX(x_J8 + ((size_t)2 * j + which) * nl * 4);
@@ -545,39 +843,95 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
       e.d = DI(o_one);
       e.a_len = e.b_len = e.c_len = e.d_len = nl;
       e.sel = 0xFFFFFFFFu;
-      e.flags = 1;
+      e.flags = 0;
       eq_nl.push_back(e);
-      eq_nl_mod.push_back(n + 2 * Mt + j);
+      eq_nl_mod.push_back(n + Mt + j);
     }
-  const size_t d_eqnn = L.in_vecT(eq_nn), d_eqnnm = L.in_vecT(eq_nn_mod);
-  const size_t d_eqnl = L.in_vecT(eq_nl), d_eqnlm = L.in_vecT(eq_nl_mod);
+  for (uint32_t m = 0; m < Mt; ++m)
+    for (uint32_t k = 0; k < CK_M2; ++k) {  // correct key: sigma^n == rho (mod n)
+      EqOperand e;
+      e.a = DX(x_GC + ((size_t)m * CK_M2 + k) * ckl * 4);
+      e.b = DI(o_one);
+      e.c = DI(o_rho + ((size_t)m * CK_M2 + k) * ckl * 4);
+      e.d = DI(o_one);
+      e.a_len = e.b_len = e.c_len = e.d_len = ckl;
+      e.sel = 0xFFFFFFFFu;
+      e.flags = 0;
+      eq_ck.push_back(e);
+      eq_ck_mod.push_back(m);
+    }
+  const size_t d_eqnn = put(eq_nn.data(), eq_nn.size() * sizeof(EqOperand)),
+               d_eqnnm = put(eq_nn_mod.data(), eq_nn_mod.size() * 4);
+  const size_t d_eqnl = put(eq_nl.data(), eq_nl.size() * sizeof(EqOperand)),
+               d_eqnlm = put(eq_nl_mod.data(), eq_nl_mod.size() * 4);
+  const size_t d_eqck = put(eq_ck.data(), eq_ck.size() * sizeof(EqOperand)),
+               d_eqckm = put(eq_ck_mod.data(), eq_ck_mod.size() * 4);
   // prod3 descriptors: u = gs1 * s^N * (c^e)^-1  (mod N^2) | w = h1^s1 * h2^s2 * (z^e)^-1 (mod N~)
   std::vector<Prod3Operand> p3_nn(P), p3_nl(P);
-  std::vector<uint32_t> p3_mod(P);
   for (uint32_t p = 0; p < P; ++p) {
     p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), DX(x_J1 + ((size_t)P + p) * nn * 4), DX(x_invc + (size_t)p * nn * 4),
                 nn, nn, nn, 0};
     p3_nl[p] = {DX(x_J3 + ((size_t)P + p) * nl * 4), DX(x_J4 + ((size_t)P + p) * nl * 4),
                 DX(x_invz + (size_t)p * nl * 4), nl, nl, nl, 0};
-    p3_mod[p] = p % n;
   }
-  const size_t d_p3nn = L.in_vecT(p3_nn), d_p3nl = L.in_vecT(p3_nl), d_p3m = L.in_vecT(p3_mod);
+  const size_t d_p3nn = put(p3_nn.data(), p3_nn.size() * sizeof(Prod3Operand)),
+               d_p3nl = put(p3_nl.data(), p3_nl.size() * sizeof(Prod3Operand)),
+               d_p3m = put(recv_of_pair.data(), recv_of_pair.size() * 4);
   // alice hash descriptors + pre-verdicts
   std::vector<uint64_t> ah_n(P), ah_c(P);
   for (uint32_t p = 0; p < P; ++p) {
-    ah_n[p] = DI(o_rn + (size_t)(p % n) * nl * 4);
+    ah_n[p] = DI(o_rn + (size_t)recv_of_pair[p] * nl * 4);
     ah_c[p] = DI(o_enc + (size_t)p * nn * 4);
   }
-  const size_t d_ahn = L.in_vecT(ah_n), d_ahc = L.in_vecT(ah_c);
-  const size_t d_alpre = L.in_vecT(alice_pre);
-  if (Layout::al(L.host.size()) > Layout::al(in_bytes_pre + desc_bound)) {
-    c->fail("internal: descriptor bound exceeded");
+  const size_t d_ahn = put(ah_n.data(), ah_n.size() * 8), d_ahc = put(ah_c.data(), ah_c.size() * 8);
+  const size_t d_alpre = put(alice_pre.data(), alice_pre.size());
+  // 2-adic halves (even ring-Pedersen / DLog moduli): a^ea * b^eb == c * d^[bit] (mod 2^k)
+  std::vector<Pow2Op> p2(n_p2);
+  for (uint32_t m = 0; m < Mt; ++m) {
+    if (pl.ped_p2_first[m] == ~0u) continue;
+    for (uint32_t k = 0; k < M; ++k) {   // T^Z_k == A_k * S^e_k  (S unreduced: pow2 reduces mod 2^k)
+      Pow2Op& o = p2[pl.ped_p2_first[m] + k];
+      o = Pow2Op{};
+      o.a = DI(o_pT + (size_t)m * nl * 4);
+      o.a_len = nl;
+      o.ea = DI(o_pZ + ((size_t)m * M + k) * zl * 4);
+      o.ea_len = zl;
+      o.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
+      o.c_len = nl;
+      o.d = DI(o_pSraw + (size_t)m * nl * 4);
+      o.d_len = nl;
+      o.sel = m * MW * 32 + k;
+      o.kbits = ped_tz[m];
+    }
+  }
+  for (uint32_t j = 0; j < J; ++j) {
+    if (pl.dlog_p2_first[j] == ~0u) continue;
+    for (int which = 0; which < 2; ++which) {   // g^y * ni^e == x
+      Pow2Op& o = p2[pl.dlog_p2_first[j] + which];
+      o = Pow2Op{};
+      o.a = DI((which == 0 ? o_dg : o_dni) + (size_t)j * nl * 4);
+      o.a_len = nl;
+      o.ea = DI((which == 0 ? o_dy1 : o_dy2) + (size_t)j * yl * 4);
+      o.ea_len = yl;
+      o.b = DI((which == 0 ? o_dni : o_dg) + (size_t)j * nl * 4);
+      o.b_len = nl;
+      o.eb = DI(o_de + (size_t)(2 * j + which) * 32);
+      o.eb_len = 8;
+      o.c = DI((which == 0 ? o_dx1 : o_dx2) + (size_t)j * nl * 4);
+      o.c_len = nl;
+      o.sel = 0xFFFFFFFFu;
+      o.kbits = dlog_tz[j];
+    }
+  }
+  const size_t d_p2 = put(p2.data(), p2.size() * sizeof(Pow2Op));
+  if (desc_base + desc.size() > out_off) {
+    c->fail("internal: descriptor bound exceeded (%zu > %zu)", desc.size(), desc_bound);
     return FSDKR_E_ARG;
   }
   // fixed-base scratch (power tables, schedules, step counts): its own context buffer
   {
     const int KD = shape_digits(nl);
-    const size_t tb = Layout::al(FB.table_bytes(KD)), sb = Layout::al(FB.sched_bytes());
+    const size_t tb = Img::al(FB.table_bytes(KD)), sb = Img::al(FB.sched_bytes());
     uint8_t* fbs = (uint8_t*)c->buf("collect_fb", tb + sb + FB.nsteps_bytes() + 256);
     if (!fbs) {
       c->fail("fsdkr_verify_collect: fixed-base scratch allocation failed");
@@ -587,26 +941,40 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     pl.fb_sched = (uint16_t*)(fbs + tb);
     pl.fb_nsteps = (uint32_t*)(fbs + tb + sb);
   }
-  pl.d_FB = d_FB;
+  pl.d_FB = desc_base;
+  clk.lap("descriptors");
 
-  // ---------------- record the plan and upload the image (the only host->device copy)
-  pl.el = b->el;
-  pl.t = b->t;
-  pl.s1l = b->s1l;
-  pl.n_mods_nl = n_mods_nl;
-  pl.in_bytes = L.host.size();
-  pl.out_off = Layout::al(in_bytes_pre + desc_bound);
+  // ---------------- materialise the image in the pinned arena; ONE host->device copy
+  const size_t up_bytes = desc_base + desc.size();
+  uint8_t* host = c->host_arena(up_bytes);
+  if (!host) {
+    c->fail("fsdkr_verify_collect: pinned host allocation of %zu bytes failed", up_bytes);
+    return FSDKR_E_OOM;
+  }
+  I.materialize(host);
+  memcpy(host + desc_base, desc.data(), desc.size());
+  clk.lap("materialize");
+  int rc = c->hip_check(hipMemcpyAsync(dev, host, up_bytes, hipMemcpyHostToDevice, c->stream), "H2D batch");
+  if (!rc) rc = c->hip_check(hipStreamSynchronize(c->stream), "sync H2D");
+  clk.lap("H2D");
+  if (rc) return rc;
+
+  // ---------------- record the plan
+  pl.out_off = out_off;
   pl.total = total;
   pl.dev = dev;
   pl.o_Q = o_Q; pl.o_enc = o_enc; pl.o_pz = o_pz; pl.o_pu1 = o_pu1; pl.o_pu2 = o_pu2; pl.o_pu3 = o_pu3;
   pl.o_ps1 = o_ps1; pl.o_pA = o_pA; pl.o_az = o_az; pl.o_ae = o_ae; pl.o_vss = o_vss; pl.o_NN = o_NN;
-  pl.o_mods = o_mods; pl.o_one = o_one; pl.o_rn = o_rn;
+  pl.o_mods = o_mods; pl.o_ckmods = o_ckmods; pl.o_one = o_one;
+  pl.d_finfo = o_finfo;
+  pl.d_p2 = d_p2;
+  pl.n_p2 = n_p2;
+  pl.n_mods_nl = n_mods_nl;
   pl.x_epdl = x_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
-  // launch order = stream assignment in collect_run: GA, GD (long), J2, J5 (short, feed the inverses)
-  const size_t xs[4] = {x_GA, x_GD, x_J2, x_J5};
-  const size_t ds[4] = {d_GA, d_GD, d_J2, d_J5};
-  const ModexpJob* js[4] = {&GA, &GD, &J2, &J5};
-  for (int k = 0; k < 4; ++k) {
+  const size_t xs[CollectPlan::NJOB] = {x_GA, x_GD, x_J2, x_J5, x_GC};
+  const size_t ds[CollectPlan::NJOB] = {d_GA, d_GD, d_J2, d_J5, d_GC};
+  const ModexpJob* js[CollectPlan::NJOB] = {&GA, &GD, &J2, &J5, &GC};
+  for (int k = 0; k < CollectPlan::NJOB; ++k) {
     pl.x_J[k] = xs[k];
     pl.d_J[k] = ds[k];
     pl.jk32[k] = js[k]->k32;
@@ -614,62 +982,49 @@ int collect_prepare(Ctx* c, const fsdkr_collect_batch* b) {
     pl.jbits[k] = js[k]->exp_bits;
   }
   pl.x_invc = x_invc; pl.x_invz = x_invz; pl.x_unn = x_unn; pl.x_uzA = x_uzA; pl.x_uzp = x_uzp;
-  pl.x_eq2 = x_eq2; pl.x_eq3 = x_eq3; pl.x_u = x_u; pl.x_w = x_w; pl.x_fel = x_fel; pl.x_pdlv = x_pdlv;
-  pl.x_rng = x_rng;
+  pl.x_eq2 = x_eq2; pl.x_eq3 = x_eq3; pl.x_eqck = x_eqck; pl.x_u = x_u; pl.x_w = x_w; pl.x_fel = x_fel;
+  pl.x_pdlv = x_pdlv; pl.x_rng = x_rng; pl.x_p2 = x_p2;
   pl.d_bs = d_bs; pl.d_bn = d_bn; pl.d_iynn = d_iynn; pl.d_imnn = d_imnn; pl.d_iynl = d_iynl; pl.d_imnl = d_imnl;
-  pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_p3nn = d_p3nn;
-  pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc; pl.d_alpre = d_alpre;
+  pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_eqck = d_eqck;
+  pl.d_eqckm = d_eqckm; pl.d_p3nn = d_p3nn; pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc;
+  pl.d_alpre = d_alpre;
   pl.n_inv_nn = (uint32_t)inv_y_nn.size();
   pl.n_eq_nn = (uint32_t)eq_nn.size();
   pl.n_eq_nl = (uint32_t)eq_nl.size();
-  int rc = c->hip_check(hipMemcpyAsync(dev, L.host.data(), L.host.size(), hipMemcpyHostToDevice, c->stream),
-                        "H2D batch");
-  if (rc) return rc;
-  return c->hip_check(hipStreamSynchronize(c->stream), "sync H2D");
+  pl.n_eq_ck = (uint32_t)eq_ck.size();
+  for (Sess& x : pl.ss) x.b = nullptr;   // the caller's buffers are not used after prepare
+  c->plan = plan.release();
+  return FSDKR_OK;
 }
 
-// Kernel pipeline on the prepared (device-resident) batch; writes verdicts.
-int collect_run(Ctx* c, fsdkr_verdicts* v) {
+// Enqueue the kernel pipeline on the prepared (device-resident) batch.
+static int collect_launch_impl(Ctx* c) {
   CollectPlan* plan = reinterpret_cast<CollectPlan*>(c->plan);
   if (!plan) {
-    c->fail("fsdkr_collect_run: no prepared batch");
+    c->fail("fsdkr_collect_launch: no prepared batch");
     return FSDKR_E_ARG;
   }
   CollectPlan& pl = *plan;
-  const Sizes& s = pl.s;
-  const uint32_t nl = s.nl, nn = s.nn, P = s.P, n = s.n, Mt = s.Mt, M = s.M, J = s.J;
+  if (pl.launched) {
+    c->fail("fsdkr_collect_launch: the batch is already in flight (call finish first)");
+    return FSDKR_E_ARG;
+  }
+  const uint32_t nl = pl.nl, nn = pl.nn, P = pl.P, n = pl.n, Mt = pl.Mt, M = pl.M;
   uint8_t* dev = pl.dev;
   uint8_t* const out_base = dev + pl.out_off;
   auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
   auto PX = [&](size_t o) { return (uint32_t*)(out_base + o); };
   auto PI = [&](size_t o) { return (const uint32_t*)(dev + o); };
-  const size_t o_Q = pl.o_Q, o_enc = pl.o_enc, o_pz = pl.o_pz, o_pu1 = pl.o_pu1, o_pu2 = pl.o_pu2, o_pu3 = pl.o_pu3;
-  const size_t o_ps1 = pl.o_ps1, o_pA = pl.o_pA, o_az = pl.o_az, o_ae = pl.o_ae, o_vss = pl.o_vss, o_NN = pl.o_NN;
-  const size_t o_mods = pl.o_mods, o_one = pl.o_one;
-  const size_t x_epdl = pl.x_epdl, x_pbits = pl.x_pbits, x_ppanic = pl.x_ppanic, x_Bpdl = pl.x_Bpdl, x_gs1 = pl.x_gs1;
-  const size_t x_invc = pl.x_invc, x_invz = pl.x_invz, x_unn = pl.x_unn, x_uzA = pl.x_uzA, x_uzp = pl.x_uzp;
-  const size_t x_eq2 = pl.x_eq2, x_eq3 = pl.x_eq3, x_u = pl.x_u, x_w = pl.x_w, x_fel = pl.x_fel, x_pdlv = pl.x_pdlv;
-  const size_t x_rng = pl.x_rng;
-  const size_t d_bs = pl.d_bs, d_bn = pl.d_bn, d_iynn = pl.d_iynn, d_imnn = pl.d_imnn, d_iynl = pl.d_iynl;
-  const size_t d_imnl = pl.d_imnl, d_eqnn = pl.d_eqnn, d_eqnnm = pl.d_eqnnm, d_eqnl = pl.d_eqnl, d_eqnlm = pl.d_eqnlm;
-  const size_t d_p3nn = pl.d_p3nn, d_p3nl = pl.d_p3nl, d_p3m = pl.d_p3m, d_ahn = pl.d_ahn, d_ahc = pl.d_ahc;
-  const size_t d_alpre = pl.d_alpre;
-  const uint32_t n_mods_nl = pl.n_mods_nl;
-  const std::vector<uint32_t>& ae_bits = pl.ae_bits;
-  const std::vector<uint32_t>& cpdl_extra = pl.cpdl_extra;
-  const std::vector<uint8_t>& ck_pre = pl.ck_pre;
-  const std::vector<uint8_t>& dlog_pre = pl.dlog_pre;
-  (void)ae_bits;
-  // ---------------- launch
   int rc;
   hipStream_t st = c->stream;
   // the alice pre-verdicts become the initial range verdicts
-  if ((rc = c->hip_check(hipMemcpyAsync(out_base + x_rng, dev + d_alpre, P, hipMemcpyDeviceToDevice, st), "D2D")))
+  if ((rc = c->hip_check(hipMemcpyAsync(out_base + pl.x_rng, dev + pl.d_alpre, P, hipMemcpyDeviceToDevice, st), "D2D")))
     return rc;
   // moduli constants
-  uint32_t *cons_nn = nullptr, *cons_nl = nullptr;
-  if ((rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn, "collect_nn"))) return rc;
-  if ((rc = setup_moduli(c, nl, PI(o_mods), n_mods_nl, &cons_nl, "collect_nl"))) return rc;
+  uint32_t *cons_nn = nullptr, *cons_nl = nullptr, *cons_ck = nullptr;
+  if ((rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn, "collect_nn"))) return rc;
+  if ((rc = setup_moduli(c, nl, PI(pl.o_mods), pl.n_mods_nl, &cons_nl, "collect_nl"))) return rc;
+  if ((rc = setup_moduli(c, pl.ckl, PI(pl.o_ckmods), Mt, &cons_ck, "collect_ck"))) return rc;
   // GA lanes per instance: GA shares the chip with the other streams, so it takes
   // the largest group that keeps it within about half the resident lanes
   // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
@@ -683,19 +1038,19 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   for (uint32_t g : {16u, kWideGroup})
     if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
   if (ga_forced) ga_group = ga_forced;
-  uint32_t* cons_nn_w = nullptr;
-  if (ga_group == kWideGroup && nn == 128 && pl.jcount[0] &&
-      (rc = setup_moduli(c, nn, PI(o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup)))
-    return rc;
   if (ga_group == kWideGroup && nn != 128) ga_group = 16;
-  // ---- stream plan (up to eleven concurrent lanes of work: give HIP >= 12 hardware
+  uint32_t* cons_nn_w = nullptr;
+  if (ga_group == kWideGroup && pl.jcount[0] &&
+      (rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup)))
+    return rc;
+  // ---- stream plan (up to twelve concurrent lanes of work: give HIP >= 12 hardware
   //      queues, GPU_MAX_HW_QUEUES, or streams share queues and serialise):
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
   //   side 8  : FB table chains (h1, h2, T: the longest dependent chain), top priority
   //   side 1  : FB schedules, then (after the tables) fixed-base exponents
   //   side 7  : J5 + nl inverses instead of st when CUs are reserved (FSDKR_RESERVE_CUS)
-  //   side 3  : ped_hash (serial SHA-256 chains, priority)
-  //   side 4  : GD (nl: correct-key, DLog; priority)
+  //   side 3  : ped_hash (serial SHA-256 chains, priority) -> 2-adic checks of even moduli
+  //   side 4  : GD (DLog), GC (correct key) -> correct-key equalities
   //   side 6  : Feldman (secp256k1 Horner per pair)
   //   st      : pdl_hash, binom x2 | fork | J5, nl inverses | join | eq, prod3, alice
   //   side 2  :                    J2 (nn, 256-bit challenges) -> nn inverses
@@ -703,7 +1058,6 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   std::vector<hipEvent_t> done;
   // issue-priority levels of the serial chains (tuning knob FSDKR_PRIO="GA,FB,GD,J5";
   // measured defaults)
-  // (knobs are read per call so one process can A/B them: tools/ab_collect.py)
   uint32_t prio[4] = {3, 3, 2, 1};
   if (const char* e = getenv("FSDKR_PRIO")) sscanf(e, "%u,%u,%u,%u", &prio[0], &prio[1], &prio[2], &prio[3]);
   pl.fb.table_prio = prio[1];
@@ -720,17 +1074,14 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     done.push_back(ev);
     return FSDKR_OK;
   };
-  static const char* tags[4] = {"mxt_GA", "mxt_GD", "mxt_J2", "mxt_J5"};
-  // prio: s_setprio level of the launch's waves (latency-critical chains); group: lanes per instance
-  auto launch_group = [&](int k, hipStream_t ss, uint32_t prio, uint32_t group) -> int {
+  static const char* tags[CollectPlan::NJOB] = {"mxt_GA", "mxt_GD", "mxt_J2", "mxt_J5", "mxt_GC"};
+  auto launch_group = [&](int k, hipStream_t ss, uint32_t pr, uint32_t group, const uint32_t* cons) -> int {
     if (!pl.jcount[k]) return FSDKR_OK;
-    const uint32_t* cons = (pl.jk32[k] == nn) ? (group == kWideGroup ? cons_nn_w : cons_nn) : cons_nl;
     return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
-                              tags[k], prio, group);
+                              tags[k], pr, group);
   };
   // GA-first ordering (tuning knob FSDKR_GA_FIRST, bit mask): the throughput jobs
-  // fb_exp (1), J2 (2) and J5 (4) wait for GA, so GA's ~1 wave per SIMD runs beside
-  // only the few-wave chains
+  // fb_exp (1), J2 (2) and J5 (4) wait for GA
   const uint32_t ga_first = [] {
     const char* e = getenv("FSDKR_GA_FIRST");
     return e ? (uint32_t)atoi(e) : 0u;
@@ -746,15 +1097,14 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     // dependent squarings) is the critical path, so GA steps down one issue
     // priority level below it (8-way shard: 33.4 -> 31.7 ms, tools/ab_hwq.sh)
     if (ga_group >= 16 && !getenv("FSDKR_PRIO")) prio[0] = 2;
-    if ((rc = launch_group(0, ss, prio[0], ga_group)) || (rc = join_later(ss))) return rc;
+    const uint32_t* cga = (ga_group == kWideGroup) ? cons_nn_w : cons_nn;
+    if ((rc = launch_group(0, ss, prio[0], ga_group, cga)) || (rc = join_later(ss))) return rc;
     if (ga_first && (rc = fork(ss, &ga_done))) return rc;
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
     FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps};
-    // the table chains (thousands of dependent squarings, few waves) run on the
-    // reserved CUs when FSDKR_RESERVE_CUS is set
     hipStream_t ts = c->crit_stream();
     if (!ts) ts = c->side_stream(8);   // own stream: the chain starts beside fb_sched
     (void)hipStreamWaitEvent(ts, consts_ready, 0);
@@ -762,40 +1112,54 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
         (rc = join_later(ss)))
       return rc;
   }
-  {  // ring-Pedersen challenges: one serial SHA-256 chain per message, needed only by the final checks
+  {  // ring-Pedersen challenges (one serial SHA-256 chain per message), then the
+     // 2-adic halves of even-modulus checks (they read the challenge bits)
     hipStream_t ss = c->side_stream(3);
-    PedHashArgs h{PI(o_pA), M, nl, PX(x_pbits), PX(x_ppanic), Mt};
+    PedHashArgs h{PI(pl.o_pA), M, nl, PX(pl.x_pbits), PX(pl.x_ppanic), Mt};
     c->mark("ped_hash", true, ss);
     rc = c->hip_check(launch_ped_hash(h, ss), "ped_hash");
     c->mark("ped_hash", false, ss);
-    if (rc || (rc = join_later(ss))) return rc;
+    if (rc) return rc;
+    if (pl.n_p2) {
+      Pow2Args a{(const Pow2Op*)(dev + pl.d_p2), PX(pl.x_pbits), PX(pl.x_p2), pl.n_p2};
+      if ((rc = c->hip_check(launch_pow2_check(a, ss), "pow2_check"))) return rc;
+    }
+    if ((rc = join_later(ss))) return rc;
   }
   {  // Feldman share checks (inputs only; one Horner chain per pair)
     hipStream_t ss = c->side_stream(6);
-    (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    FeldmanArgs f{PI(o_vss), PI(o_Q), n, pl.t, (uint8_t*)(out_base + x_fel), P};
+    FeldmanArgs f{PI(pl.o_vss), PI(pl.o_Q), (const FeldmanInfo*)(dev + pl.d_finfo), (uint8_t*)(out_base + pl.x_fel),
+                  P};
     c->mark("ec", true, ss);
     rc = c->hip_check(launch_feldman(f, ss), "feldman");
     c->mark("ec", false, ss);
     if (rc || (rc = join_later(ss))) return rc;
   }
-  {  // GD: correct-key sigma^n, DLog g^y / ni^e (2048-bit exponents, few instances)
+  {  // GD: DLog g^y / ni^e; GC: correct-key sigma^n (2048-bit exponents, few instances)
     hipStream_t ss = c->side_stream(4);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    if ((rc = launch_group(1, ss, prio[2], 0)) || (rc = join_later(ss))) return rc;
+    if ((rc = launch_group(1, ss, prio[2], 0, cons_nl)) || (rc = launch_group(4, ss, prio[2], 0, cons_ck))) return rc;
+    EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqck), PI(pl.d_eqckm), cons_ck, PX(pl.x_pbits), DI(pl.o_one),
+                  PX(pl.x_eqck), pl.n_eq_ck};
+    c->mark("eq_check", true, ss);
+    rc = c->hip_check(launch_eq_check(pl.ckl, a, ss), "eq_check ck");
+    c->mark("eq_check", false, ss);
+    if (rc || (rc = join_later(ss))) return rc;
   }
   // (2) PDL challenges, then the jobs that exponentiate by them
   {
-    PdlHashArgs a{PI(o_Q), PI(o_enc), PI(o_pz), PI(o_pu1), PI(o_pu2), PI(o_pu3), nn, nl, PX(x_epdl), P};
+    PdlHashArgs a{PI(pl.o_Q), PI(pl.o_enc), PI(pl.o_pz), PI(pl.o_pu1), PI(pl.o_pu2), PI(pl.o_pu3), nn, nl,
+                  PX(pl.x_epdl), P};
     c->mark("pdl_hash", true);
     rc = c->hip_check(launch_pdl_hash(a, st), "pdl_hash");
     c->mark("pdl_hash", false);
     if (rc) return rc;
   }
   {
-    BinomArgs a{(const uint64_t*)(dev + d_bs), (const uint64_t*)(dev + d_bn), pl.s1l, nl, nn, PX(x_Bpdl), P};
+    BinomArgs a{(const uint64_t*)(dev + pl.d_bs), (const uint64_t*)(dev + pl.d_bn), pl.s1l, nl, nn, PX(pl.x_Bpdl), P};
     if ((rc = c->hip_check(launch_binom(a, st), "binom"))) return rc;
-    BinomArgs a2{(const uint64_t*)(dev + d_bs) + P, (const uint64_t*)(dev + d_bn) + P, pl.s1l, nl, nn, PX(x_gs1), P};
+    BinomArgs a2{(const uint64_t*)(dev + pl.d_bs) + P, (const uint64_t*)(dev + pl.d_bn) + P, pl.s1l, nl, nn,
+                 PX(pl.x_gs1), P};
     if ((rc = c->hip_check(launch_binom(a2, st), "binom"))) return rc;
   }
   hipEvent_t ready;
@@ -804,9 +1168,9 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
     if (ga_first & 2) (void)hipStreamWaitEvent(ss, ga_done, 0);
-    if ((rc = launch_group(2, ss, 0, 8))) return rc;
-    InverseArgs a{(const uint64_t*)(dev + d_iynn), (const uint64_t*)(dev + d_imnn), PX(x_invc), PX(x_unn),
-                  nullptr, pl.n_inv_nn};
+    if ((rc = launch_group(2, ss, 0, 8, cons_nn))) return rc;
+    InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
+                  PX(pl.x_unn), nullptr, pl.n_inv_nn};
     c->mark("inverse", true, ss);
     rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
     c->mark("inverse", false, ss);
@@ -815,7 +1179,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
     hipStream_t ss = c->side_stream(5);
     (void)hipStreamWaitEvent(ss, ready, 0);
-    PdlU1Args u{PI(o_ps1), PX(x_epdl), PI(o_Q), PI(o_pu1), pl.s1l, (uint8_t*)(out_base + x_pdlv), P};
+    PdlU1Args u{PI(pl.o_ps1), PX(pl.x_epdl), PI(pl.o_Q), PI(pl.o_pu1), pl.s1l, (uint8_t*)(out_base + pl.x_pdlv), P};
     c->mark("ec", true, ss);
     rc = c->hip_check(launch_pdl_u1(u, ss), "pdl_u1");
     c->mark("ec", false, ss);
@@ -824,8 +1188,7 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   }
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
-  {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses; a side stream when CUs are
-     // reserved (the main stream is unmasked), else the main stream
+  {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses
     hipStream_t js = st;
     if (c->reserve_cus) {
       js = c->side_stream(7);
@@ -835,15 +1198,15 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
       (void)hipEventDestroy(r2);
     }
     if (ga_first & 4) (void)hipStreamWaitEvent(js, ga_done, 0);
-    if ((rc = launch_group(3, js, prio[3], 8))) return rc;
-    InverseArgs b1{(const uint64_t*)(dev + d_iynl), (const uint64_t*)(dev + d_imnl), PX(x_invz), PX(x_uzA),
-                   nullptr, P};
+    if ((rc = launch_group(3, js, prio[3], 8, cons_nl))) return rc;
+    InverseArgs b1{(const uint64_t*)(dev + pl.d_iynl), (const uint64_t*)(dev + pl.d_imnl), PX(pl.x_invz),
+                   PX(pl.x_uzA), nullptr, P};
     c->mark("inverse", true, js);
     rc = c->hip_check(launch_inverse(nl, b1, js), "inverse nl");
     c->mark("inverse", false, js);
     if (rc) return rc;
-    InverseArgs b2{(const uint64_t*)(dev + d_iynl) + P, (const uint64_t*)(dev + d_imnl) + P, nullptr, PX(x_uzp),
-                   nullptr, P};
+    InverseArgs b2{(const uint64_t*)(dev + pl.d_iynl) + P, (const uint64_t*)(dev + pl.d_imnl) + P, nullptr,
+                   PX(pl.x_uzp), nullptr, P};
     if ((rc = c->hip_check(launch_inverse(nl, b2, js), "inverse nl 2"))) return rc;
     if (js != st && (rc = join_later(js))) return rc;
   }
@@ -854,88 +1217,128 @@ int collect_run(Ctx* c, fsdkr_verdicts* v) {
   }
   // equality checks and exact products
   {
-    EqCheckArgs a{(const EqOperand*)(dev + d_eqnn), PI(d_eqnnm), cons_nn, PX(x_pbits), DI(o_one), PX(x_eq2),
-                  pl.n_eq_nn};
+    EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqnn), PI(pl.d_eqnnm), cons_nn, PX(pl.x_pbits), DI(pl.o_one),
+                  PX(pl.x_eq2), pl.n_eq_nn};
     c->mark("eq_check", true);
     rc = c->hip_check(launch_eq_check(nn, a, st), "eq_check nn");
     c->mark("eq_check", false);
     if (rc) return rc;
-    // eq_nl outputs: [u3 P | RP Mt*M | CK Mt*11 | DLog 2J] contiguous from x_eq3
-    EqCheckArgs b1{(const EqOperand*)(dev + d_eqnl), PI(d_eqnlm), cons_nl, PX(x_pbits), DI(o_one), PX(x_eq3),
-                   pl.n_eq_nl};
+    // eq_nl outputs: [u3 P | RP Mt*M | DLog 2J] contiguous from x_eq3
+    EqCheckArgs b1{(const EqOperand*)(dev + pl.d_eqnl), PI(pl.d_eqnlm), cons_nl, PX(pl.x_pbits), DI(pl.o_one),
+                   PX(pl.x_eq3), pl.n_eq_nl};
     c->mark("eq_check", true);
     rc = c->hip_check(launch_eq_check(nl, b1, st), "eq_check nl");
     c->mark("eq_check", false);
     if (rc) return rc;
-    Prod3Args pa{(const Prod3Operand*)(dev + d_p3nn), PI(d_p3m), cons_nn, PX(x_u), P};
+    Prod3Args pa{(const Prod3Operand*)(dev + pl.d_p3nn), PI(pl.d_p3m), cons_nn, PX(pl.x_u), P};
     if ((rc = c->hip_check(launch_prod3(nn, pa, st), "prod3 nn"))) return rc;
-    Prod3Args pb{(const Prod3Operand*)(dev + d_p3nl), PI(d_p3m), cons_nl, PX(x_w), P};
+    Prod3Args pb{(const Prod3Operand*)(dev + pl.d_p3nl), PI(pl.d_p3m), cons_nl, PX(pl.x_w), P};
     if ((rc = c->hip_check(launch_prod3(nl, pb, st), "prod3 nl"))) return rc;
   }
   {
-    AliceHashArgs a{(const uint64_t*)(dev + d_ahn), (const uint64_t*)(dev + d_ahc), PI(o_az), PX(x_u), PX(x_w),
-                    PI(o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + x_rng), P};
+    AliceHashArgs a{(const uint64_t*)(dev + pl.d_ahn), (const uint64_t*)(dev + pl.d_ahc), PI(pl.o_az), PX(pl.x_u),
+                    PX(pl.x_w), PI(pl.o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + pl.x_rng), P};
     c->mark("alice_hash", true);
     rc = c->hip_check(launch_alice_hash(a, st), "alice_hash");
     c->mark("alice_hash", false);
     if (rc) return rc;
   }
-  // ---------------- results
-  std::vector<uint32_t> e_pdl((size_t)P * 8), ppanic(Mt), unn(2 * (size_t)P), uzA(P), uzp(P), eq2(P),
-      eq_nl_res(pl.n_eq_nl);
+  pl.launched = true;
+  return FSDKR_OK;
+}
+
+static bool caps_ok(const fsdkr_verdicts& v, const Sess& x) {
+  return v.feldman && v.pdl && v.range && v.ped && v.ck && (x.J == 0 || v.dlog) && v.cap_pairs >= x.P &&
+         v.cap_msgs >= x.Mt && v.cap_joins >= x.J;
+}
+
+// Wait for the launched pipeline, read the verdict words back, assemble per session.
+static int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
+  CollectPlan* plan = reinterpret_cast<CollectPlan*>(c->plan);
+  if (!plan || !plan->launched) {
+    c->fail("fsdkr_collect_finish: no launched batch");
+    return FSDKR_E_ARG;
+  }
+  CollectPlan& pl = *plan;
+  if (!out || count != pl.S) {
+    c->fail("fsdkr_collect_finish: %u verdict blocks for %u sessions", count, pl.S);
+    return FSDKR_E_ARG;
+  }
+  for (uint32_t s = 0; s < count; ++s)
+    if (!caps_ok(out[s], pl.ss[s])) {
+      c->fail("fsdkr_collect_finish: session %u: verdict arrays missing or too small", s);
+      return FSDKR_E_ARG;
+    }
+  pl.launched = false;
+  const uint32_t P = pl.P, Mt = pl.Mt, M = pl.M;
+  uint8_t* const out_base = pl.dev + pl.out_off;
+  hipStream_t st = c->stream;
+  std::vector<uint32_t> e_pdl((size_t)P * 8), ppanic(Mt), unn(pl.n_inv_nn), uzA(P), uzp(P), eq2(P), eq3(pl.n_eq_nl),
+      eqck(pl.n_eq_ck), p2(pl.n_p2);
   std::vector<uint8_t> fel(P), pdlv(P), rng(P);
+  int rc;
   auto D2H = [&](void* dst, size_t off, size_t bytes) {
+    if (!bytes) return (int)FSDKR_OK;
     return c->hip_check(hipMemcpyAsync(dst, out_base + off, bytes, hipMemcpyDeviceToHost, st), "D2H verdicts");
   };
-  if ((rc = D2H(e_pdl.data(), x_epdl, e_pdl.size() * 4)) || (rc = D2H(ppanic.data(), x_ppanic, Mt * 4)) ||
-      (rc = D2H(unn.data(), x_unn, (size_t)pl.n_inv_nn * 4)) || (rc = D2H(uzA.data(), x_uzA, P * 4)) ||
-      (rc = D2H(uzp.data(), x_uzp, P * 4)) || (rc = D2H(eq2.data(), x_eq2, P * 4)) ||
-      (rc = D2H(eq_nl_res.data(), x_eq3, eq_nl_res.size() * 4)) || (rc = D2H(fel.data(), x_fel, P)) ||
-      (rc = D2H(pdlv.data(), x_pdlv, P)) || (rc = D2H(rng.data(), x_rng, P)))
+  if ((rc = D2H(e_pdl.data(), pl.x_epdl, e_pdl.size() * 4)) || (rc = D2H(ppanic.data(), pl.x_ppanic, Mt * 4)) ||
+      (rc = D2H(unn.data(), pl.x_unn, unn.size() * 4)) || (rc = D2H(uzA.data(), pl.x_uzA, P * 4)) ||
+      (rc = D2H(uzp.data(), pl.x_uzp, P * 4)) || (rc = D2H(eq2.data(), pl.x_eq2, P * 4)) ||
+      (rc = D2H(eq3.data(), pl.x_eq3, eq3.size() * 4)) || (rc = D2H(eqck.data(), pl.x_eqck, eqck.size() * 4)) ||
+      (rc = D2H(p2.data(), pl.x_p2, p2.size() * 4)) || (rc = D2H(fel.data(), pl.x_fel, P)) ||
+      (rc = D2H(pdlv.data(), pl.x_pdlv, P)) || (rc = D2H(rng.data(), pl.x_rng, P)))
     return rc;
   if ((rc = c->sync())) return rc;
   // PDL unit test of c: c^eA witnesses it unless eA == 0 / the Alice proof was rejected early
   std::vector<uint32_t> unit_c_pdl(unn.begin(), unn.begin() + P);
-  for (size_t k = 0; k < cpdl_extra.size(); ++k) unit_c_pdl[cpdl_extra[k]] = unn[P + k];
-  const uint32_t* u_cA = unn.data();
-  const uint32_t* u_zA = uzA.data();
-  const uint32_t* u_zp = uzp.data();
-  for (uint32_t p = 0; p < P; ++p) {
-    bool ez = true;
-    for (int k = 0; k < 8; ++k) ez = ez && e_pdl[(size_t)p * 8 + k] == 0;
-    // reference panics (mod_inv(..).unwrap(), zk_pdl_with_slack.rs:180) when e != 0 and c or z is not a unit
-    const bool cunit = unit_c_pdl[p] != 0;
-    const bool panic = !ez && (!cunit || !u_zp[p]);
-    uint8_t bits = (uint8_t)(pdlv[p] & 1u);
-    if (eq2[p]) bits |= 2;
-    if (eq_nl_res[p]) bits |= 4;
-    if (panic) bits |= 8;
-    v->pdl[p] = bits;
-    v->feldman[p] = fel[p] ? 1 : 0;
-    // Alice: pre-checks, invertibility of z^e and c^e, transcript hash (range_proofs.rs:125-163)
-    v->range[p] = (rng[p] && u_cA[p] && u_zA[p]) ? 1 : 0;
-  }
-  for (uint32_t m = 0; m < Mt; ++m) {
-    v->ped[m] = ped_verdict(&eq_nl_res[P + (size_t)m * M], M, ppanic[m]);
-    bool ck = ck_pre[m];
-    for (uint32_t k = 0; k < CK_M2; ++k) ck = ck && eq_nl_res[P + (size_t)Mt * M + (size_t)m * CK_M2 + k];
-    v->ck[m] = ck ? 1 : 0;
-  }
-  for (uint32_t j = 0; j < J; ++j) {
-    const size_t base = P + (size_t)Mt * M + (size_t)Mt * CK_M2 + 2 * j;
-    uint8_t d = 0;
-    if (dlog_pre[j] && eq_nl_res[base]) d |= 1;
-    if (dlog_pre[j] && eq_nl_res[base + 1]) d |= 2;
-    v->dlog[j] = d;
+  for (size_t k = 0; k < pl.cpdl_extra.size(); ++k) unit_c_pdl[pl.cpdl_extra[k]] = unn[P + k];
+  for (uint32_t s = 0; s < count; ++s) {
+    const Sess& x = pl.ss[s];
+    fsdkr_verdicts& v = out[s];
+    for (uint32_t lp = 0; lp < x.P; ++lp) {
+      const uint32_t p = x.pbase + lp;
+      bool ez = true;
+      for (int k = 0; k < 8; ++k) ez = ez && e_pdl[(size_t)p * 8 + k] == 0;
+      // reference panics (mod_inv(..).unwrap(), zk_pdl_with_slack.rs:180) when e != 0 and c or z is not a unit
+      const bool panic = !ez && (!unit_c_pdl[p] || !uzp[p]);
+      uint8_t bits = (uint8_t)(pdlv[p] & 1u);
+      if (eq2[p]) bits |= 2;
+      if (eq3[p]) bits |= 4;
+      if (panic) bits |= 8;
+      v.pdl[lp] = bits;
+      v.feldman[lp] = fel[p];
+      // Alice: pre-checks, invertibility of z^e and c^e, transcript hash (range_proofs.rs:125-163)
+      v.range[lp] = (rng[p] && unn[p] && uzA[p]) ? 1 : 0;
+    }
+    for (uint32_t lm = 0; lm < x.Mt; ++lm) {
+      const uint32_t m = x.mbase + lm;
+      uint32_t* eqm = &eq3[P + (size_t)m * M];
+      if (pl.ped_mode[m] == 1)
+        for (uint32_t k = 0; k < M; ++k) eqm[k] = 1;   // odd part 1
+      if (pl.ped_p2_first[m] != ~0u)
+        for (uint32_t k = 0; k < M; ++k) eqm[k] = eqm[k] && p2[pl.ped_p2_first[m] + k];
+      // panic index: challenge shorter than M bits (BitVec) or Z shorter than M, whichever first
+      uint32_t pw = ppanic[m];
+      if (pl.ped_zlen[m] < M) pw = pw ? std::min(pw, pl.ped_zlen[m] + 1) : pl.ped_zlen[m] + 1;
+      v.ped[lm] = pl.ped_mode[m] == 2 ? 2 : ped_verdict(eqm, M, pw);   // A short / modulus 0: panic
+      bool ck = pl.ck_pre[m];
+      for (uint32_t k = 0; k < CK_M2; ++k) ck = ck && eqck[(size_t)m * CK_M2 + k];
+      v.ck[lm] = pl.ck_short[m] ? 2 : ((ck || pl.ck_one[m]) ? 1 : 0);
+    }
+    for (uint32_t lj = 0; lj < x.J; ++lj) {
+      const uint32_t j = x.jbase + lj;
+      const size_t base = P + (size_t)Mt * M + 2 * (size_t)j;
+      uint8_t d = 0;
+      for (int which = 0; which < 2; ++which) {
+        bool ok = (pl.dlog_pre[j] >> which) & 1u;
+        ok = ok && (pl.dlog_trivial[j] || eq3[base + which]);
+        if (pl.dlog_p2_first[j] != ~0u) ok = ok && p2[pl.dlog_p2_first[j] + which];
+        if (ok) d |= (uint8_t)(1u << which);
+      }
+      v.dlog[lj] = d;
+    }
   }
   return FSDKR_OK;
-}
-
-
-int verify_collect_impl(Ctx* c, const fsdkr_collect_batch* b, fsdkr_verdicts* v) {
-  int rc = collect_prepare(c, b);
-  if (rc) return rc;
-  return collect_run(c, v);
 }
 
 int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdkr_error* e) {
@@ -961,22 +1364,36 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
         return FSDKR_OK;
       }
     }
-    if (ref < n) {  // points_committed_vec[i] indexed past its end (:182)
+    if (ref < n) {  // points_committed_vec[i] indexed past its end (:182); the host
+                    // layer checks message 0's first `ref` shares before this panic
       e->panic = 1;
       e->variant = FSDKR_ERR_PUBLIC_SHARE_VALIDATION;
       return FSDKR_OK;
     }
   }
   if (!v) return FSDKR_E_ARG;
+  if (v->cap_pairs < R * n || v->cap_msgs < R + J || (J && (!v->dlog || v->cap_joins < J))) return FSDKR_E_ARG;
   for (uint32_t k = 0; k < R; ++k)
-    for (uint32_t i = 0; i < n; ++i)
-      if (!v->feldman[(size_t)k * n + i]) {
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint8_t f = v->feldman[(size_t)k * n + i];
+      if (f & 2) {   // empty commitment vector: curv's unwrap panics
+        e->panic = 1;
         e->variant = FSDKR_ERR_PUBLIC_SHARE_VALIDATION;
         return FSDKR_OK;
       }
+      if (!(f & 1)) {
+        e->variant = FSDKR_ERR_PUBLIC_SHARE_VALIDATION;
+        return FSDKR_OK;
+      }
+    }
   // PDL then range, per (k, i)  (:330-350)
   for (uint32_t k = 0; k < R; ++k)
     for (uint32_t i = 0; i < n; ++i) {
+      if (b->recv_avail && i >= b->recv_avail) {   // local_key.paillier_key_vec[i] out of bounds (:334)
+        e->panic = 1;
+        e->variant = FSDKR_ERR_PDL_W_SLACK_PROOF;
+        return FSDKR_OK;
+      }
       const uint8_t d = v->pdl[(size_t)k * n + i];
       if (d & 8) {
         e->panic = 1;
@@ -988,6 +1405,12 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
         e->f[0] = d & 1;
         e->f[1] = (d >> 1) & 1;
         e->f[2] = (d >> 2) & 1;
+        return FSDKR_OK;
+      }
+      if (b->range_lens && i >= b->range_lens[k]) {   // range_proofs[i] out of bounds (:342)
+        e->panic = 1;
+        e->variant = FSDKR_ERR_RANGE_PROOF;
+        e->f[0] = i;
         return FSDKR_OK;
       }
       if (!v->range[(size_t)k * n + i]) {
@@ -1008,15 +1431,22 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
       return FSDKR_OK;
     }
   }
+  const uint32_t ckl = b->ckl ? b->ckl : b->nl;
   // correct key + modulus size per refresh message (:375-396)
   for (uint32_t m = 0; m < R; ++m) {
     const uint32_t pi = b->party_index[m];
-    if (!v->ck[m]) {
+    if (v->ck[m] & 2) {   // sigma_vec[i] out of bounds in zk-paillier's verify
+      e->panic = 1;
       e->variant = FSDKR_ERR_PAILLIER_VERIFICATION;
       e->f[0] = pi;
       return FSDKR_OK;
     }
-    const uint32_t bits = hbn::bitlen(b->ck_n + (size_t)m * b->nl, b->nl);
+    if (!(v->ck[m] & 1)) {
+      e->variant = FSDKR_ERR_PAILLIER_VERIFICATION;
+      e->f[0] = pi;
+      return FSDKR_OK;
+    }
+    const uint32_t bits = hbn::bitlen(b->ck_n + (size_t)m * ckl, ckl);
     if (bits > b->key_bits || bits < b->key_bits - 1) {
       e->variant = FSDKR_ERR_MODULI_TOO_SMALL;
       e->f[0] = pi;
@@ -1032,7 +1462,13 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
       e->variant = FSDKR_ERR_NEW_PARTY_UNASSIGNED_INDEX;
       return FSDKR_OK;
     }
-    if (!v->ck[R + j]) {
+    if (v->ck[R + j] & 2) {
+      e->panic = 1;
+      e->variant = FSDKR_ERR_PAILLIER_VERIFICATION;
+      e->f[0] = pi;
+      return FSDKR_OK;
+    }
+    if (!(v->ck[R + j] & 1)) {
       e->variant = FSDKR_ERR_PAILLIER_VERIFICATION;
       e->f[0] = pi;
       return FSDKR_OK;
@@ -1042,7 +1478,7 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
       e->f[0] = pi;
       return FSDKR_OK;
     }
-    const uint32_t bits = hbn::bitlen(b->ck_n + (size_t)(R + j) * b->nl, b->nl);
+    const uint32_t bits = hbn::bitlen(b->ck_n + (size_t)(R + j) * ckl, ckl);
     if (bits > b->key_bits || bits < b->key_bits - 1) {
       e->variant = FSDKR_ERR_MODULI_TOO_SMALL;
       e->f[0] = pi;
@@ -1059,24 +1495,46 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
 
 extern "C" {
 
-int fsdkr_verify_collect(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch, fsdkr_verdicts* out) {
+int fsdkr_collect_prepare_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count) {
   fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
-  if (!c || !batch || !out || !out->feldman || !out->pdl || !out->range || !out->ped || !out->ck ||
-      (batch->n_join && !out->dlog))
-    return FSDKR_E_ARG;
-  return fsdkr::verify_collect_impl(c, batch, out);
+  if (!c) return FSDKR_E_ARG;
+  return fsdkr::collect_prepare_impl(c, batches, count);
 }
 
 int fsdkr_collect_prepare(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
-  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
-  if (!c || !batch) return FSDKR_E_ARG;
-  return fsdkr::collect_prepare(c, batch);
+  return fsdkr_collect_prepare_multi(ctx, batch, 1);
 }
 
-int fsdkr_collect_run(fsdkr_ctx* ctx, fsdkr_verdicts* out) {
+int fsdkr_collect_launch(fsdkr_ctx* ctx) {
   fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
-  if (!c || !out || !out->feldman || !out->pdl || !out->range || !out->ped || !out->ck) return FSDKR_E_ARG;
-  return fsdkr::collect_run(c, out);
+  if (!c) return FSDKR_E_ARG;
+  return fsdkr::collect_launch_impl(c);
+}
+
+int fsdkr_collect_finish_multi(fsdkr_ctx* ctx, fsdkr_verdicts* out, uint32_t count) {
+  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  return fsdkr::collect_finish_impl(c, out, count);
+}
+
+int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out) { return fsdkr_collect_finish_multi(ctx, out, 1); }
+
+int fsdkr_collect_run(fsdkr_ctx* ctx, fsdkr_verdicts* out) {
+  int rc = fsdkr_collect_launch(ctx);
+  return rc ? rc : fsdkr_collect_finish(ctx, out);
+}
+
+int fsdkr_verify_collect_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count,
+                               fsdkr_verdicts* out) {
+  if (!ctx || !batches || !out || count == 0) return FSDKR_E_ARG;
+  int rc = fsdkr_collect_prepare_multi(ctx, batches, count);
+  if (!rc) rc = fsdkr_collect_launch(ctx);
+  if (!rc) rc = fsdkr_collect_finish_multi(ctx, out, count);
+  return rc;
+}
+
+int fsdkr_verify_collect(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch, fsdkr_verdicts* out) {
+  return fsdkr_verify_collect_multi(ctx, batch, 1, out);
 }
 
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out) {

@@ -34,9 +34,17 @@ struct Ctx {
   std::map<std::string, TimeAcc> times;
   std::vector<PendingEvent> pending;
   std::vector<uint8_t> staging;   // host staging for descriptor uploads
-  static constexpr int NSIDE = 10;
+  static constexpr int NSIDE = 11;
   hipStream_t side[NSIDE] = {};   // concurrent streams for independent jobs (lazily created)
   void* plan = nullptr;           // prepared collect() batch (collect.cpp)
+  // pinned host arena for the collect() image (grow-only; one H2D copy per prepare)
+  uint8_t* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  uint8_t* host_arena(size_t bytes);
+  // stream of the share-recovery entry points (decrypt, MSM): separate from the
+  // collect pipeline so they overlap a launched batch (fsdkr_collect_launch)
+  hipStream_t aux = nullptr;
+  hipStream_t aux_stream();
 
   void fail(const char* fmt, ...);
   int hip_check(hipError_t e, const char* what);
@@ -65,6 +73,21 @@ struct Ctx {
   // synchronise the stream and fold pending events into `times`
   int sync();
 };
+
+// Runs the calls of one C-ABI entry point on another stream (the context is
+// single-threaded per the ABI, so swapping the main stream is safe).
+struct StreamScope {
+  Ctx* c;
+  hipStream_t saved;
+  StreamScope(Ctx* cx, hipStream_t s) : c(cx), saved(cx->stream) {
+    if (s) c->stream = s;
+  }
+  ~StreamScope() { c->stream = saved; }
+};
+
+// Host worker threads for the collect() pre-pass (FSDKR_HOST_THREADS, else
+// OMP_NUM_THREADS, else min(hardware threads, 16)).
+unsigned host_threads();
 
 // A batch of modexp instances of one modulus width (k32 limbs) and one
 // exponent-length class (exp_bits = max bits; sets the window count).

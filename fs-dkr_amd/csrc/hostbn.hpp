@@ -251,5 +251,80 @@ inline void store(const Limbs& a, uint32_t* out, size_t n) {
   for (size_t k = 0; k < n; ++k) out[k] = k < a.size() ? a[k] : 0u;
 }
 
+// ---- allocation-free helpers on raw limb arrays (the per-pair / per-message
+//      scans of the collect() pre-pass run these thousands of times)
+// compare a (an limbs) with b (bn limbs)
+inline int cmp_raw(const uint32_t* a, size_t an, const uint32_t* b, size_t bn) {
+  const size_t n = std::max(an, bn);
+  for (size_t k = n; k-- > 0;) {
+    const uint32_t x = k < an ? a[k] : 0u, y = k < bn ? b[k] : 0u;
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return 0;
+}
+inline bool is_zero_raw(const uint32_t* a, size_t n) {
+  for (size_t k = 0; k < n; ++k)
+    if (a[k]) return false;
+  return true;
+}
+inline uint32_t ctz_raw(const uint32_t* a, size_t n) {
+  for (size_t k = 0; k < n; ++k)
+    if (a[k]) return 32u * (uint32_t)k + (uint32_t)__builtin_ctz(a[k]);
+  return 32u * (uint32_t)n;
+}
+// a >>= s (in place, n limbs)
+inline void shr_raw(uint32_t* a, size_t n, uint32_t s) {
+  const size_t w = s / 32;
+  const uint32_t b = s % 32;
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t lo = k + w < n ? a[k + w] : 0u;
+    const uint32_t hi = k + w + 1 < n ? a[k + w + 1] : 0u;
+    a[k] = b ? (lo >> b) | (hi << (32 - b)) : lo;
+  }
+}
+// gcd(a, b) == 1, binary gcd in place on copies (no allocation per step)
+inline bool gcd_is_one(const uint32_t* a, size_t an, const uint32_t* b, size_t bn) {
+  const size_t n = std::max(an, bn);
+  std::vector<uint32_t> u(n, 0), v(n, 0);
+  std::copy(a, a + an, u.begin());
+  std::copy(b, b + bn, v.begin());
+  const bool uz = is_zero_raw(u.data(), n), vz = is_zero_raw(v.data(), n);
+  if (uz || vz) {   // gcd(0, x) = x
+    const uint32_t* x = uz ? v.data() : u.data();
+    if (uz && vz) return false;
+    if (x[0] != 1) return false;
+    return is_zero_raw(x + 1, n - 1);
+  }
+  if (!(u[0] & 1u) && !(v[0] & 1u)) return false;   // both even: 2 | gcd
+  shr_raw(u.data(), n, ctz_raw(u.data(), n));
+  size_t len = n;
+  for (;;) {
+    while (len > 1 && u[len - 1] == 0 && v[len - 1] == 0) --len;
+    shr_raw(v.data(), len, ctz_raw(v.data(), len));
+    if (cmp_raw(u.data(), len, v.data(), len) > 0) std::swap(u, v);
+    // v -= u  (v >= u)
+    int64_t br = 0;
+    for (size_t k = 0; k < len; ++k) {
+      const int64_t d = (int64_t)v[k] - u[k] + br;
+      v[k] = (uint32_t)d;
+      br = d >> 32;
+    }
+    if (is_zero_raw(v.data(), len)) break;
+  }
+  return u[0] == 1 && is_zero_raw(u.data() + 1, len - 1);
+}
+// true iff some prime in `primes` divides a (primes < 2^13, paired into
+// products < 2^26 so one 64-bit remainder chain serves two primes)
+inline bool has_small_factor(const uint32_t* a, size_t n, const std::vector<uint32_t>& primes) {
+  for (size_t j = 0; j < primes.size(); j += 2) {
+    const uint64_t p1 = primes[j], p2 = j + 1 < primes.size() ? primes[j + 1] : 1u;
+    const uint64_t m = p1 * p2;
+    uint64_t r = 0;
+    for (size_t k = n; k-- > 0;) r = ((r << 32) | a[k]) % m;
+    if (r % p1 == 0 || (p2 > 1 && r % p2 == 0)) return true;
+  }
+  return false;
+}
+
 }  // namespace hbn
 }  // namespace fsdkr

@@ -5,7 +5,9 @@
 // arithmetic of kzen-paillier decrypt runs on the host.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
@@ -16,67 +18,129 @@
 
 using namespace fsdkr;
 
+namespace {
+// f(begin, end) over [0, n) on the host worker threads
+template <class F>
+void parallel_for_host(size_t n, size_t grain, F&& f) {
+  const size_t chunks = std::min<size_t>(host_threads(), (n + grain - 1) / grain);
+  if (chunks <= 1) {
+    f((size_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t k = 1; k < chunks; ++k) th.emplace_back([&, k] { f(n * k / chunks, n * (k + 1) / chunks); });
+  f((size_t)0, n / chunks);
+  for (auto& t : th) t.join();
+}
+}  // namespace
+
 extern "C" {
 
-int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c, const uint32_t* p,
-                           const uint32_t* q, uint32_t* m_out) {
+int fsdkr_paillier_decrypt_multi(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c,
+                                 const uint32_t* key_idx, const uint32_t* p, const uint32_t* q, uint32_t n_keys,
+                                 uint32_t* m_out) {
   Ctx* cx = reinterpret_cast<Ctx*>(ctx);
-  if (!cx || !c || !p || !q || !m_out) return FSDKR_E_ARG;
+  if (!cx || !c || !key_idx || !p || !q || !m_out || n_keys == 0) return FSDKR_E_ARG;
   if (count == 0) return FSDKR_OK;
   const uint32_t nn = 2 * nl;
   if (!shape_digits(nl)) {
     cx->fail("fsdkr_paillier_decrypt: unsupported width %u", nl);
     return FSDKR_E_UNSUPPORTED;
   }
-  const hbn::Limbs P = hbn::from(p, nl), Q = hbn::from(q, nl);
-  const hbn::Limbs N = hbn::mul(P, Q);
-  const hbn::Limbs PP = hbn::mul(P, P), QQ = hbn::mul(Q, Q);
-  if (hbn::is_even(P) || hbn::is_even(Q) || hbn::bitlen(PP) > 32 * nl || hbn::bitlen(QQ) > 32 * nl ||
-      hbn::bitlen(N) > 32 * nl) {
-    cx->fail("fsdkr_paillier_decrypt: bad key");
-    return FSDKR_E_ARG;
-  }
-  const hbn::Limbs one{1};
-  const hbn::Limbs pm1 = hbn::sub(P, one), qm1 = hbn::sub(Q, one);
-  // kzen-paillier CRT decryption: m_p = L_p(c^(p-1) mod p^2) h_p mod p, h_p = L_p(g^(p-1) mod p^2)^-1, g = N+1
-  auto hconst = [&](const hbn::Limbs& X, const hbn::Limbs& XX, const hbn::Limbs& xm1, hbn::Limbs* h) {
-    const hbn::Limbs gx = hbn::mod(hbn::add(one, hbn::mul(xm1, N)), XX);  // (1+N)^(x-1) = 1 + (x-1)N mod x^2
-    const hbn::Limbs L = hbn::div_exact(hbn::sub(gx, one), X);
-    return hbn::modinv(L, X, h);
+  for (uint32_t k = 0; k < count; ++k)
+    if (key_idx[k] >= n_keys) {
+      cx->fail("fsdkr_paillier_decrypt: key_idx[%u] out of range", k);
+      return FSDKR_E_ARG;
+    }
+  StreamScope scope(cx, cx->aux_stream());   // overlaps a launched collect batch
+  // kzen-paillier CRT decryption with g = N + 1.  Its constants have closed forms:
+  // (1+N)^(p-1) = 1 + (p-1)N mod p^2 and (p-1)N = -q p mod p^2, so
+  // h_p = L_p(g^(p-1) mod p^2)^-1 = (-q)^-1 mod p = p - q^-1 mod p (likewise h_q);
+  // the two inverses per key run on the GPU (lane-cooperative inverse kernel).
+  struct Key {
+    hbn::Limbs P, Q, PP, QQ, pm1, qm1;
+    bool ok;
   };
-  hbn::Limbs hp, hq, qinv;
-  if (!hconst(P, PP, pm1, &hp) || !hconst(Q, QQ, qm1, &hq) || !hbn::modinv(Q, P, &qinv)) {
-    cx->fail("fsdkr_paillier_decrypt: degenerate key");
-    return FSDKR_E_ARG;
+  std::vector<Key> keys(n_keys);
+  std::vector<uint32_t> invy((size_t)2 * n_keys * nl, 0u), invm((size_t)2 * n_keys * nl, 0u);
+  std::vector<uint8_t> bad(n_keys, 0);
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    Key& K = keys[k];
+    K.P = hbn::from(p + (size_t)k * nl, nl);
+    K.Q = hbn::from(q + (size_t)k * nl, nl);
+    K.PP = hbn::mul(K.P, K.P);
+    K.QQ = hbn::mul(K.Q, K.Q);
+    const hbn::Limbs N = hbn::mul(K.P, K.Q);
+    K.ok = !hbn::is_even(K.P) && !hbn::is_even(K.Q) && hbn::bitlen(K.PP) <= 32 * nl &&
+           hbn::bitlen(K.QQ) <= 32 * nl && hbn::bitlen(N) <= 32 * nl && !(K.P.size() == 1 && K.P[0] == 1) &&
+           !(K.Q.size() == 1 && K.Q[0] == 1);
+    if (!K.ok) {
+      cx->fail("fsdkr_paillier_decrypt: bad key %u", k);
+      return FSDKR_E_ARG;
+    }
+    K.pm1 = hbn::sub(K.P, hbn::Limbs{1});
+    K.qm1 = hbn::sub(K.Q, hbn::Limbs{1});
+    hbn::store(hbn::mod(K.Q, K.P), invy.data() + (size_t)(2 * k) * nl, nl);      // q^-1 mod p
+    hbn::store(K.P, invm.data() + (size_t)(2 * k) * nl, nl);
+    hbn::store(hbn::mod(K.P, K.Q), invy.data() + (size_t)(2 * k + 1) * nl, nl);  // p^-1 mod q
+    hbn::store(K.Q, invm.data() + (size_t)(2 * k + 1) * nl, nl);
   }
-  // 2*count GPU exponentiations: (c mod p^2)^(p-1) mod p^2, (c mod q^2)^(q-1) mod q^2
-  std::vector<uint32_t> base((size_t)2 * count * nl), ex((size_t)2 * count * nl), idx(2 * count), mods(2 * nl),
-      outv((size_t)2 * count * nl);
-  hbn::store(PP, mods.data(), nl);
-  hbn::store(QQ, mods.data() + nl, nl);
-  for (uint32_t k = 0; k < count; ++k) {
-    const hbn::Limbs ck = hbn::from(c + (size_t)k * nn, nn);
-    hbn::store(hbn::mod(ck, PP), base.data() + (size_t)(2 * k) * nl, nl);
-    hbn::store(hbn::mod(ck, QQ), base.data() + (size_t)(2 * k + 1) * nl, nl);
-    hbn::store(pm1, ex.data() + (size_t)(2 * k) * nl, nl);
-    hbn::store(qm1, ex.data() + (size_t)(2 * k + 1) * nl, nl);
-    idx[2 * k] = 0;
-    idx[2 * k + 1] = 1;
-  }
-  int rc = fsdkr_modexp_batch(ctx, nl, 2 * count, base.data(), ex.data(), nl, idx.data(), mods.data(), 2, outv.data());
+  std::vector<uint32_t> invo((size_t)2 * n_keys * nl), unit(2 * (size_t)n_keys);
+  int rc = fsdkr_mod_inverse(ctx, nl, 2 * n_keys, invy.data(), invm.data(), invo.data(), unit.data());
   if (rc) return rc;
-  for (uint32_t k = 0; k < count; ++k) {
-    const hbn::Limbs up = hbn::from(outv.data() + (size_t)(2 * k) * nl, nl);
-    const hbn::Limbs uq = hbn::from(outv.data() + (size_t)(2 * k + 1) * nl, nl);
-    const hbn::Limbs mp = hbn::mulmod(hbn::div_exact(hbn::sub(up.empty() ? one : up, one), P), hp, P);
-    const hbn::Limbs mq = hbn::mulmod(hbn::div_exact(hbn::sub(uq.empty() ? one : uq, one), Q), hq, Q);
-    // m = mq + q * ((mp - mq) q^-1 mod p)
-    const hbn::Limbs mqp = hbn::mod(mq, P);
-    const hbn::Limbs d = hbn::cmp(mp, mqp) >= 0 ? hbn::sub(mp, mqp) : hbn::sub(hbn::add(mp, P), mqp);
-    const hbn::Limbs m = hbn::add(mq, hbn::mul(Q, hbn::mulmod(d, qinv, P)));
-    hbn::store(m, m_out + (size_t)k * nl, nl);
+  for (uint32_t k = 0; k < n_keys; ++k)
+    if (!unit[2 * k] || !unit[2 * k + 1]) {
+      cx->fail("fsdkr_paillier_decrypt: degenerate key %u", k);
+      return FSDKR_E_ARG;
+    }
+  // 2*count GPU exponentiations: (c mod p^2)^(p-1) mod p^2, (c mod q^2)^(q-1) mod q^2
+  std::vector<uint32_t> base((size_t)2 * count * nl), ex((size_t)2 * count * nl), idx(2 * count),
+      mods((size_t)2 * n_keys * nl), outv((size_t)2 * count * nl);
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    hbn::store(keys[k].PP, mods.data() + (size_t)(2 * k) * nl, nl);
+    hbn::store(keys[k].QQ, mods.data() + (size_t)(2 * k + 1) * nl, nl);
   }
+  parallel_for_host(count, 16, [&](size_t b0, size_t b1) {
+    for (size_t i = b0; i < b1; ++i) {
+      const Key& K = keys[key_idx[i]];
+      const hbn::Limbs ck = hbn::from(c + i * nn, nn);
+      hbn::store(hbn::mod(ck, K.PP), base.data() + (2 * i) * nl, nl);
+      hbn::store(hbn::mod(ck, K.QQ), base.data() + (2 * i + 1) * nl, nl);
+      hbn::store(K.pm1, ex.data() + (2 * i) * nl, nl);
+      hbn::store(K.qm1, ex.data() + (2 * i + 1) * nl, nl);
+      idx[2 * i] = 2 * key_idx[i];
+      idx[2 * i + 1] = 2 * key_idx[i] + 1;
+    }
+  });
+  rc = fsdkr_modexp_batch(ctx, nl, 2 * count, base.data(), ex.data(), nl, idx.data(), mods.data(), 2 * n_keys,
+                          outv.data());
+  if (rc) return rc;
+  const hbn::Limbs one{1};
+  parallel_for_host(count, 16, [&](size_t b0, size_t b1) {
+    for (size_t i = b0; i < b1; ++i) {
+      const uint32_t k = key_idx[i];
+      const Key& K = keys[k];
+      const hbn::Limbs qinv = hbn::from(invo.data() + (size_t)(2 * k) * nl, nl);
+      const hbn::Limbs pinv = hbn::from(invo.data() + (size_t)(2 * k + 1) * nl, nl);
+      const hbn::Limbs hp = hbn::sub(K.P, qinv), hq = hbn::sub(K.Q, pinv);
+      const hbn::Limbs up = hbn::from(outv.data() + (2 * i) * nl, nl);
+      const hbn::Limbs uq = hbn::from(outv.data() + (2 * i + 1) * nl, nl);
+      const hbn::Limbs mp = hbn::mulmod(hbn::div_exact(hbn::sub(up.empty() ? one : up, one), K.P), hp, K.P);
+      const hbn::Limbs mq = hbn::mulmod(hbn::div_exact(hbn::sub(uq.empty() ? one : uq, one), K.Q), hq, K.Q);
+      // m = mq + q * ((mp - mq) q^-1 mod p)
+      const hbn::Limbs mqp = hbn::mod(mq, K.P);
+      const hbn::Limbs d = hbn::cmp(mp, mqp) >= 0 ? hbn::sub(mp, mqp) : hbn::sub(hbn::add(mp, K.P), mqp);
+      const hbn::Limbs m = hbn::add(mq, hbn::mul(K.Q, hbn::mulmod(d, qinv, K.P)));
+      hbn::store(m, m_out + i * nl, nl);
+    }
+  });
   return FSDKR_OK;
+}
+
+int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c, const uint32_t* p,
+                           const uint32_t* q, uint32_t* m_out) {
+  std::vector<uint32_t> key_idx(count, 0u);
+  return fsdkr_paillier_decrypt_multi(ctx, nl, count, c, key_idx.data(), p, q, 1, m_out);
 }
 
 // Job 1 (refresh_message.rs:72-84): c_k = (1 + m_k N) * r_k^N mod N^2 for the
@@ -161,13 +225,15 @@ int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t*
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || !points || !scalars || !out || terms == 0) return FSDKR_E_ARG;
   if (count == 0) return FSDKR_OK;
+  StreamScope scope(c, c->aux_stream());   // overlaps a launched collect batch
   const size_t np = (size_t)count * terms;
-  uint8_t* d = (uint8_t*)c->buf("msm", np * 16 * 4 + np * 8 * 4 + np * 8 + (size_t)count * 16 * 4 + 1024);
+  uint8_t* d = (uint8_t*)c->buf("msm", np * 16 * 4 + np * 8 * 4 + np * 8 + (size_t)count * 16 * 4 + np * 96 + 1024);
   if (!d) return FSDKR_E_OOM;
   uint32_t* d_pts = (uint32_t*)d;
   uint32_t* d_sc = d_pts + np * 16;
   uint64_t* d_ptr = (uint64_t*)(d_sc + np * 8);
   uint32_t* d_out = (uint32_t*)(d_ptr + np);
+  uint32_t* d_scr = d_out + (size_t)count * 16;
   std::vector<uint64_t> ptrs(np);
   for (size_t k = 0; k < np; ++k) ptrs[k] = (uint64_t)(uintptr_t)(d_pts + k * 16);
   int rc;
@@ -175,7 +241,7 @@ int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t*
       (rc = c->hip_check(hipMemcpyAsync(d_sc, scalars, np * 32, hipMemcpyHostToDevice, c->stream), "H2D sc")) ||
       (rc = c->hip_check(hipMemcpyAsync(d_ptr, ptrs.data(), np * 8, hipMemcpyHostToDevice, c->stream), "H2D ptr")))
     return rc;
-  EcMsmArgs a{d_ptr, d_sc, terms, d_out, count};
+  EcMsmArgs a{d_ptr, d_sc, terms, d_out, count, d_scr};
   c->mark("ec", true);
   rc = c->hip_check(launch_ec_msm(a, c->stream), "ec_msm");
   c->mark("ec", false);

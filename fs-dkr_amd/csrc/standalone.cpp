@@ -14,6 +14,7 @@
 #include "ctx.hpp"
 #include "fbjob.hpp"
 #include "fsdkr/fsdkr.h"
+#include "hostbn.hpp"
 #include "kernels.h"
 #include "verify.h"
 
@@ -43,20 +44,24 @@ int fsdkr_feldman_check(fsdkr_ctx* ctx, uint32_t n_msgs, uint32_t n, uint32_t t,
     c->fail("fsdkr_feldman_check: null pointer");
     return FSDKR_E_ARG;
   }
-  const size_t vb = (size_t)n_msgs * (t + 1) * 16 * 4, cb = P * 16 * 4;
-  uint8_t* d = (uint8_t*)c->buf("fel_io", al256(vb) + al256(cb) + P);
+  const size_t vb = (size_t)n_msgs * (t + 1) * 16 * 4, cb = P * 16 * 4, ib = P * sizeof(FeldmanInfo);
+  uint8_t* d = (uint8_t*)c->buf("fel_io", al256(vb) + al256(cb) + al256(ib) + P);
   if (!d) {
     c->fail("fsdkr_feldman_check: device allocation failed");
     return FSDKR_E_OOM;
   }
   uint32_t* d_vss = (uint32_t*)d;
   uint32_t* d_com = (uint32_t*)(d + al256(vb));
-  uint8_t* d_out = d + al256(vb) + al256(cb);
+  FeldmanInfo* d_info = (FeldmanInfo*)(d + al256(vb) + al256(cb));
+  uint8_t* d_out = d + al256(vb) + al256(cb) + al256(ib);
+  std::vector<FeldmanInfo> info(P);
+  for (size_t p = 0; p < P; ++p) info[p] = {(uint32_t)((p / n) * (t + 1)), t + 1, (uint32_t)(p % n) + 1, 0};
   int rc;
   if ((rc = c->hip_check(hipMemcpyAsync(d_vss, vss, vb, hipMemcpyHostToDevice, c->stream), "H2D vss")) ||
-      (rc = c->hip_check(hipMemcpyAsync(d_com, commit, cb, hipMemcpyHostToDevice, c->stream), "H2D commit")))
+      (rc = c->hip_check(hipMemcpyAsync(d_com, commit, cb, hipMemcpyHostToDevice, c->stream), "H2D commit")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_info, info.data(), ib, hipMemcpyHostToDevice, c->stream), "H2D info")))
     return rc;
-  FeldmanArgs f{d_vss, d_com, n, t, d_out, (uint32_t)P};
+  FeldmanArgs f{d_vss, d_com, d_info, d_out, (uint32_t)P};
   c->mark("ec", true);
   rc = c->hip_check(launch_feldman(f, c->stream), "feldman");
   c->mark("ec", false);
@@ -81,20 +86,47 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
     c->fail("fsdkr_ring_pedersen_verify: unsupported modulus width %u limbs", nl);
     return FSDKR_E_UNSUPPORTED;
   }
-  for (uint32_t m = 0; m < count; ++m)
-    if (!(N[(size_t)m * nl] & 1u)) {
-      c->fail("fsdkr_ring_pedersen_verify: proof %u has an even modulus (unsupported)", m);
-      return FSDKR_E_UNSUPPORTED;
+  // N = 2^tz * odd: the Montgomery kernels run modulo the odd part, pow2.hip
+  // checks the congruence modulo 2^tz (CRT).  N = 0: GMP aborts at the first
+  // check (reported as the reference's panic); odd part 1: congruence mod 1 holds.
+  std::vector<uint32_t> Nodd((size_t)count * nl), Sred((size_t)count * nl), tz(count, 0u);
+  std::vector<uint8_t> mode(count, 0);   // 0 regular, 1 odd part 1, 2 modulus 0
+  for (uint32_t m = 0; m < count; ++m) {
+    uint32_t* on = Nodd.data() + (size_t)m * nl;
+    memcpy(on, N + (size_t)m * nl, nl * 4);
+    memcpy(Sred.data() + (size_t)m * nl, S + (size_t)m * nl, nl * 4);
+    if (hbn::is_zero_raw(on, nl)) {
+      mode[m] = 2;
+      on[0] = 3;
+      continue;
     }
+    tz[m] = hbn::ctz_raw(on, nl);
+    if (tz[m]) hbn::shr_raw(on, nl, tz[m]);
+    if (on[0] == 1 && hbn::is_zero_raw(on + 1, nl - 1)) {
+      mode[m] = 1;
+      on[0] = 3;
+      continue;
+    }
+    uint32_t* sd = Sred.data() + (size_t)m * nl;
+    if (hbn::cmp_raw(sd, nl, on, nl) >= 0) hbn::store(hbn::mod(hbn::from(sd, nl), hbn::from(on, nl)), sd, nl);
+  }
   const size_t MW = (M + 31) / 32;           // challenge-bit words per proof
   const size_t I = (size_t)count * M;        // T^Z instances
   const size_t bN = (size_t)count * nl * 4, bA = I * nl * 4, bZ = I * zl * 4;
   // device image: N | S | T | A | Z | one | bits | panic | TZ | eq | eq ops | eq mod idx
   size_t off = 0;
   auto take = [&](size_t bytes) { const size_t o = off; off = al256(off + (bytes ? bytes : 1)); return o; };
+  size_t n_p2 = 0;
+  std::vector<uint32_t> p2_first(count, ~0u);
+  for (uint32_t m = 0; m < count; ++m)
+    if (tz[m] && mode[m] != 2) {
+      p2_first[m] = (uint32_t)n_p2;
+      n_p2 += M;
+    }
   const size_t oN = take(bN), oS = take(bN), oT = take(bN), oA = take(bA), oZ = take(bZ), oOne = take(nl * 4);
   const size_t oBits = take((size_t)count * MW * 4), oPanic = take((size_t)count * 4), oTZ = take(bA);
   const size_t oEq = take(I * 4), oOps = take(I * sizeof(EqOperand)), oMod = take(I * 4);
+  const size_t oSraw = take(bN), oP2 = take(n_p2 * sizeof(Pow2Op)), oP2o = take(n_p2 * 4);
   uint8_t* d = (uint8_t*)c->buf("rp_io", off);
   if (!d) {
     c->fail("fsdkr_ring_pedersen_verify: device allocation failed");
@@ -126,10 +158,32 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
       e.flags = 0;
       mod_idx[q] = m;
     }
+  std::vector<Pow2Op> p2(n_p2);
+  for (uint32_t m = 0; m < count; ++m) {
+    if (p2_first[m] == ~0u) continue;
+    for (uint32_t k = 0; k < M; ++k) {   // T^Z_k == A_k * S^e_k  (mod 2^tz)
+      Pow2Op& o = p2[p2_first[m] + k];
+      o = Pow2Op{};
+      const size_t q = (size_t)m * M + k;
+      o.a = DA(oT + (size_t)m * nl * 4);
+      o.a_len = nl;
+      o.ea = DA(oZ + q * zl * 4);
+      o.ea_len = zl;
+      o.c = DA(oA + q * nl * 4);
+      o.c_len = nl;
+      o.d = DA(oSraw + (size_t)m * nl * 4);
+      o.d_len = nl;
+      o.sel = (uint32_t)((size_t)m * MW * 32 + k);
+      o.kbits = tz[m];
+    }
+  }
   hipStream_t st = c->stream;
   int rc;
-  if ((rc = c->hip_check(hipMemcpyAsync(d + oN, N, bN, hipMemcpyHostToDevice, st), "H2D N")) ||
-      (rc = c->hip_check(hipMemcpyAsync(d + oS, S, bN, hipMemcpyHostToDevice, st), "H2D S")) ||
+  if ((rc = c->hip_check(hipMemcpyAsync(d + oN, Nodd.data(), bN, hipMemcpyHostToDevice, st), "H2D N")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d + oS, Sred.data(), bN, hipMemcpyHostToDevice, st), "H2D S")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d + oSraw, S, bN, hipMemcpyHostToDevice, st), "H2D S raw")) ||
+      (n_p2 && (rc = c->hip_check(hipMemcpyAsync(d + oP2, p2.data(), n_p2 * sizeof(Pow2Op), hipMemcpyHostToDevice, st),
+                                  "H2D pow2"))) ||
       (rc = c->hip_check(hipMemcpyAsync(d + oT, T, bN, hipMemcpyHostToDevice, st), "H2D T")) ||
       (rc = c->hip_check(hipMemcpyAsync(d + oA, A, bA, hipMemcpyHostToDevice, st), "H2D A")) ||
       (rc = c->hip_check(hipMemcpyAsync(d + oZ, Z, bZ, hipMemcpyHostToDevice, st), "H2D Z")) ||
@@ -151,6 +205,10 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
   c->mark("ped_hash", true, hs);
   rc = c->hip_check(launch_ped_hash(h, hs), "ped_hash");
   c->mark("ped_hash", false, hs);
+  if (!rc && n_p2) {
+    Pow2Args pa{(const Pow2Op*)(d + oP2), (const uint32_t*)(d + oBits), (uint32_t*)(d + oP2o), (uint32_t)n_p2};
+    rc = c->hip_check(launch_pow2_check(pa, hs), "pow2_check");
+  }
   (void)hipEventRecord(hashed, hs);
   job.finalize();
   if (!rc) rc = fb_run(c, job, cons, "rp");
@@ -164,14 +222,21 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
   rc = c->hip_check(launch_eq_check(nl, ea, st), "eq_check");
   c->mark("eq_check", false);
   if (rc) return rc;
-  std::vector<uint32_t> eq(I), panic(count);
+  std::vector<uint32_t> eq(I), panic(count), p2o(n_p2);
   if ((rc = c->hip_check(hipMemcpyAsync(eq.data(), d + oEq, I * 4, hipMemcpyDeviceToHost, st), "D2H eq")) ||
       (rc = c->hip_check(hipMemcpyAsync(panic.data(), d + oPanic, (size_t)count * 4, hipMemcpyDeviceToHost, st),
-                         "D2H panic")))
+                         "D2H panic")) ||
+      (n_p2 && (rc = c->hip_check(hipMemcpyAsync(p2o.data(), d + oP2o, n_p2 * 4, hipMemcpyDeviceToHost, st),
+                                  "D2H pow2"))))
     return rc;
   if ((rc = c->sync())) return rc;
   for (uint32_t m = 0; m < count; ++m) {
-    verdict[m] = ped_verdict(&eq[(size_t)m * M], M, panic[m]);
+    uint32_t* e = &eq[(size_t)m * M];
+    if (mode[m] == 1)
+      for (uint32_t k = 0; k < M; ++k) e[k] = 1;
+    if (p2_first[m] != ~0u)
+      for (uint32_t k = 0; k < M; ++k) e[k] = e[k] && p2o[p2_first[m] + k];
+    verdict[m] = mode[m] == 2 ? 2 : ped_verdict(e, M, panic[m]);
   }
   return FSDKR_OK;
 }

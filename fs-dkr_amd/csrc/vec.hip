@@ -76,24 +76,29 @@ __global__ void pdl_u1_kernel(const PdlU1Args a) {
   a.verdict[p] = (uint8_t)((a.verdict[p] & ~1u) | (eq ? 1u : 0u));
 }
 
-// S_{k,i} == Horner(A_k, i+1)
+// S_{k,i} == Horner(A_k, i+1) over the message's own commitment vector
+// (curv get_point_commitment: fold from the top coefficient; empty -> unwrap panic)
 __global__ void feldman_kernel(const FeldmanArgs a) {
   using namespace ec;
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.count) return;
-  const uint32_t k = p / a.n, i = p % a.n;
-  const uint32_t* A = a.vss + (size_t)k * (a.t + 1) * 16;
-  const uint32_t idx = i + 1;
+  const FeldmanInfo in = a.info[p];
+  if (in.ncoef == 0) {
+    a.verdict[p] = 2u;
+    return;
+  }
+  const uint32_t* A = a.vss + (size_t)in.off * 16;
+  const uint32_t idx = in.idx;
   Jac acc;
   Fe x, y;
-  if (aff_load(x, y, A + (size_t)a.t * 16)) {
+  if (aff_load(x, y, A + (size_t)(in.ncoef - 1) * 16)) {
     jac_set_inf(acc);
   } else {
     acc.X = x;
     acc.Y = y;
     fe_set_u32(acc.Z, 1);
   }
-  for (int j = (int)a.t - 1; j >= 0; --j) {
+  for (int j = (int)in.ncoef - 2; j >= 0; --j) {
     // acc = acc * idx
     Jac r;
     jac_set_inf(r);
@@ -108,24 +113,50 @@ __global__ void feldman_kernel(const FeldmanArgs a) {
   a.verdict[p] = jac_eq_aff(acc, x, y, sinf) ? 1u : 0u;
 }
 
-// out[o] = sum_j s[o][j] * P[o][j]   (affine out, terms affine points)
-__global__ void ec_msm_kernel(const EcMsmArgs a) {
+// out[o] = sum_j s[o][j] * P[o][j]: one thread per term (a full 256-bit scalar
+// multiplication each), then one thread per output sums its terms.  The terms
+// of one output are independent, so spreading them over threads turns the
+// pk_vec rebuild (n outputs x (t+1) terms, refresh_message.rs:455-464) from
+// t+1 serial ladders per thread into one ladder per thread.
+__global__ void ec_msm_term_kernel(const EcMsmArgs a) {
+  using namespace ec;
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= a.count * a.terms) return;
+  uint32_t* J = a.scratch + (size_t)q * 24;
+  const uint32_t* pt = P32(a.pt_ptr[q]);
+  const uint32_t* sc = a.scalars + (size_t)q * 8;
+  Fe x, y;
+  Jac r;
+  if (aff_load(x, y, pt)) {
+    jac_set_inf(r);
+  } else {
+    uint32_t k[8];
+    for (int i = 0; i < 8; ++i) k[i] = sc[i];
+    scalar_reduce(k);
+    scalar_mul_aff(r, k, x, y);
+  }
+  for (int i = 0; i < 8; ++i) {
+    J[i] = r.X.v[i];
+    J[8 + i] = r.Y.v[i];
+    J[16 + i] = r.Z.v[i];
+  }
+}
+
+__global__ void ec_msm_sum_kernel(const EcMsmArgs a) {
   using namespace ec;
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= a.count) return;
   Jac acc;
   jac_set_inf(acc);
   for (uint32_t j = 0; j < a.terms; ++j) {
-    const uint32_t* pt = P32(a.pt_ptr[(size_t)o * a.terms + j]);
-    const uint32_t* sc = a.scalars + ((size_t)o * a.terms + j) * 8;
-    Fe x, y;
-    if (aff_load(x, y, pt)) continue;
-    uint32_t k[8];
-    for (int i = 0; i < 8; ++i) k[i] = sc[i];
-    scalar_reduce(k);
-    Jac r;
-    scalar_mul_aff(r, k, x, y);
-    jac_add(acc, acc, r);
+    const uint32_t* J = a.scratch + ((size_t)o * a.terms + j) * 24;
+    Jac t;
+    for (int i = 0; i < 8; ++i) {
+      t.X.v[i] = J[i];
+      t.Y.v[i] = J[8 + i];
+      t.Z.v[i] = J[16 + i];
+    }
+    jac_add(acc, acc, t);
   }
   jac_to_aff(a.out + (size_t)o * 16, acc);
 }
@@ -142,8 +173,9 @@ hipError_t launch_feldman(const FeldmanArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_ec_msm(const EcMsmArgs& a, hipStream_t st) {
-  if (!a.count) return hipSuccess;
-  hipLaunchKernelGGL(ec_msm_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
+  if (!a.count || !a.terms) return hipSuccess;
+  hipLaunchKernelGGL(ec_msm_term_kernel, dim3(blocks_for(a.count * a.terms, 64)), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(ec_msm_sum_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

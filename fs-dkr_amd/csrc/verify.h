@@ -87,11 +87,39 @@ struct PdlU1Args {          // G*(s1 mod q) + Q*(q - e) == u1
   uint32_t count;
 };
 
+// One Feldman share check: S == sum_j A[off + j] * idx^j over ncoef commitments.
+struct FeldmanInfo {
+  uint32_t off;             // first commitment point (index into vss)
+  uint32_t ncoef;           // commitments of the message (0: curv's unwrap panics)
+  uint32_t idx;             // evaluation point i + 1
+  uint32_t pad;
+};
+
 struct FeldmanArgs {
-  const uint32_t* vss;      // [R][t+1][16]
-  const uint32_t* S;        // [R*n][16]
-  uint32_t n, t;
-  uint8_t* verdict;         // [R*n]
+  const uint32_t* vss;      // [points][16]
+  const uint32_t* S;        // [count][16]
+  const FeldmanInfo* info;  // [count]
+  uint8_t* verdict;         // [count] bit0 ok, bit1 panic
+  uint32_t count;
+};
+
+// 2-adic half of a check modulo an even modulus N = 2^k * m (m odd):
+//   a^ea * b^eb == c * d^[bit]   (mod 2^k)
+// (the odd half runs in the Montgomery kernels modulo m).  Used for even
+// ring-Pedersen and composite-DLog moduli, which the reference exponentiates
+// with GMP like any other (ring_pedersen_proof.rs:144-148, zk-paillier
+// CompositeDLogProof::verify).  Null addresses stand for the value 1.
+struct Pow2Op {
+  uint64_t a, ea, b, eb, c, d;
+  uint32_t a_len, ea_len, b_len, eb_len, c_len, d_len;
+  uint32_t sel;             // ~0: d always; else challenge bit index (d used iff set)
+  uint32_t kbits;           // k (1 .. 32 * 96)
+};
+
+struct Pow2Args {
+  const Pow2Op* ops;
+  const uint32_t* sel_bits;
+  uint32_t* out;            // [count] 1/0
   uint32_t count;
 };
 
@@ -101,6 +129,7 @@ struct EcMsmArgs {          // out[o] = sum_j scalars[o][j] * P[o][j]
   uint32_t terms;
   uint32_t* out;            // [count][16] affine
   uint32_t count;
+  uint32_t* scratch;        // [count][terms][24] Jacobian terms
 };
 
 hipError_t launch_binom(const BinomArgs& a, hipStream_t st);
@@ -115,5 +144,6 @@ hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st);
 hipError_t launch_pdl_u1(const PdlU1Args& a, hipStream_t st);
 hipError_t launch_feldman(const FeldmanArgs& a, hipStream_t st);
 hipError_t launch_ec_msm(const EcMsmArgs& a, hipStream_t st);
+hipError_t launch_pow2_check(const Pow2Args& a, hipStream_t st);
 
 }  // namespace fsdkr

@@ -39,14 +39,17 @@ class CollectBatchC(ctypes.Structure):
                                     "enc", "commit", "pdl_z", "pdl_u3", "pdl_s2", "pdl_u1", "pdl_u2", "pdl_s1",
                                     "pdl_s3", "rp_z", "rp_s", "rp_e", "rp_s1", "rp_s2", "vss", "ped_S", "ped_T",
                                     "ped_N", "ped_A", "ped_Z", "ck_n", "ck_sigma", "dlog_N", "dlog_g", "dlog_ni",
-                                    "dlog_x1", "dlog_x2", "dlog_y1", "dlog_y2")] + [("n_recv", ctypes.c_uint32)]
+                                    "dlog_x1", "dlog_x2", "dlog_y1", "dlog_y2")] + [("n_recv", ctypes.c_uint32)] + \
+               [("vss_len", u32p), ("range_lens", u32p), ("ckl", ctypes.c_uint32), ("recv_avail", ctypes.c_uint32),
+                ("ped_lens", u32p), ("ck_lens", u32p)]
 
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 
 
 class VerdictsC(ctypes.Structure):
-    _fields_ = [(f, u8p) for f in ("feldman", "pdl", "range", "ped", "ck", "dlog")]
+    _fields_ = [(f, u8p) for f in ("feldman", "pdl", "range", "ped", "ck", "dlog")] + \
+               [(f, ctypes.c_uint32) for f in ("cap_pairs", "cap_msgs", "cap_joins")]
 
 
 class ErrorC(ctypes.Structure):
@@ -91,6 +94,20 @@ def lib():
     L.fsdkr_collect_prepare.restype = ctypes.c_int
     L.fsdkr_collect_run.argtypes = [vp, ctypes.POINTER(VerdictsC)]
     L.fsdkr_collect_run.restype = ctypes.c_int
+    L.fsdkr_collect_launch.argtypes = [vp]
+    L.fsdkr_collect_launch.restype = ctypes.c_int
+    L.fsdkr_collect_finish.argtypes = [vp, ctypes.POINTER(VerdictsC)]
+    L.fsdkr_collect_finish.restype = ctypes.c_int
+    L.fsdkr_collect_prepare_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
+    L.fsdkr_collect_prepare_multi.restype = ctypes.c_int
+    L.fsdkr_collect_finish_multi.argtypes = [vp, ctypes.POINTER(VerdictsC), ctypes.c_uint32]
+    L.fsdkr_collect_finish_multi.restype = ctypes.c_int
+    L.fsdkr_verify_collect_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32,
+                                             ctypes.POINTER(VerdictsC)]
+    L.fsdkr_verify_collect_multi.restype = ctypes.c_int
+    L.fsdkr_paillier_decrypt_multi.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p,
+                                               ctypes.c_uint32, u32p]
+    L.fsdkr_paillier_decrypt_multi.restype = ctypes.c_int
     L.fsdkr_collect_first_error.argtypes = [ctypes.POINTER(CollectBatchC), ctypes.POINTER(VerdictsC),
                                             ctypes.POINTER(ErrorC)]
     L.fsdkr_collect_first_error.restype = ctypes.c_int
@@ -255,6 +272,31 @@ class Context:
         self.check(self._lib.fsdkr_collect_run(self._h, ctypes.byref(v.c)))
         return v
 
+    def collect_launch(self):
+        """Enqueue the kernel pipeline of the prepared batch (returns at once)."""
+        self.check(self._lib.fsdkr_collect_launch(self._h))
+
+    def collect_finish(self, batch):
+        """Wait for the launched pipeline; returns Verdicts."""
+        from .batch import Verdicts
+        v = Verdicts(batch.R, batch.J, batch.n)
+        self.check(self._lib.fsdkr_collect_finish(self._h, ctypes.byref(v.c)))
+        return v
+
+    def collect_prepare_many(self, batches):
+        """Prepare many sessions (fsdkr.batch.CollectBatch each) as ONE device image."""
+        arr = (CollectBatchC * len(batches))(*[b.c for b in batches])
+        self._many = arr   # keep the array alive until finish
+        self.check(self._lib.fsdkr_collect_prepare_multi(self._h, arr, len(batches)))
+
+    def collect_finish_many(self, batches):
+        """Wait for the launched multi-session pipeline; one Verdicts per session."""
+        from .batch import Verdicts
+        vs = [Verdicts(b.R, b.J, b.n) for b in batches]
+        arr = (VerdictsC * len(vs))(*[v.c for v in vs])
+        self.check(self._lib.fsdkr_collect_finish_multi(self._h, arr, len(vs)))
+        return vs
+
     def paillier_decrypt(self, cts, p, q, nl):
         """Decrypt ciphertexts under dk = (p, q) on the GPU (CRT form)."""
         C = ints_to_limbs(cts, 2 * nl)
@@ -262,6 +304,19 @@ class Context:
         Qq = ints_to_limbs([q], nl)
         O = np.zeros((len(cts), nl), dtype=np.uint32)
         self.check(self._lib.fsdkr_paillier_decrypt(self._h, nl, len(cts), _ptr(C), _ptr(Pp), _ptr(Qq), _ptr(O)))
+        return limbs_to_ints(O)
+
+    def paillier_decrypt_many(self, cts, key_idx, ps, qs, nl):
+        """Decrypt cts[k] under key (ps[key_idx[k]], qs[key_idx[k]]) on the GPU."""
+        if not cts:
+            return []
+        C = ints_to_limbs(cts, 2 * nl)
+        I = np.ascontiguousarray(np.asarray(key_idx, dtype=np.uint32))
+        Pp = ints_to_limbs(ps, nl)
+        Qq = ints_to_limbs(qs, nl)
+        O = np.zeros((len(cts), nl), dtype=np.uint32)
+        self.check(self._lib.fsdkr_paillier_decrypt_multi(self._h, nl, len(cts), _ptr(C), _ptr(I), _ptr(Pp),
+                                                          _ptr(Qq), len(ps), _ptr(O)))
         return limbs_to_ints(O)
 
     def paillier_encrypt(self, ms, rs, ns, n_idx, nl):

@@ -6,7 +6,17 @@ North star job (4) places this layer in the Rust crate; with no Rust
 toolchain in this image it is restated here and reads the reference's message
 structures by field name (refresh_message.rs:31-48, add_party_message.rs:36-45,
 zk_pdl_with_slack.rs:41-50, range_proofs.rs:101-108,
-ring_pedersen_proof.rs:30-38,79-84).  Any object with those attributes works."""
+ring_pedersen_proof.rs:30-38,79-84).  Any object with those attributes works.
+
+Shapes the reference accepts and the kernels represent per instance (instead
+of rejecting the whole batch): commitment vectors of any length (Horner over
+each message's own vector, refresh_message.rs:180-182), range_proofs / A / Z /
+sigma_vec shorter than the loops index (the reference's index panic at that
+check), a LocalKey with fewer keys than receivers (panic at the first pair
+past them, :334-339), an ek.n wider than the batch's moduli (its correct-key
+proof runs at its own width before ModuliTooSmall, :376-391).  Still outside
+the representable set (UnsupportedInput): negative BigInts and values wider
+than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
 import ctypes
 
 import numpy as np
@@ -14,10 +24,11 @@ import numpy as np
 from ._native import CollectBatchC, ErrorC, VerdictsC, lib
 
 M2 = 11   # zk-paillier NiCorrectKeyProof sigma_vec length
+_CK_WIDTHS = (64, 96, 128, 192)
 
 
 class UnsupportedInput(ValueError):
-    """Input outside what the C ABI represents (negative BigInts, oversize moduli)."""
+    """Input outside what the C ABI represents (negative BigInts, oversize values)."""
 
 
 def _limbs_for(bits):
@@ -27,29 +38,30 @@ def _limbs_for(bits):
 def pack(values, limbs):
     """ints -> (len, limbs) uint32, little-endian; raises on negatives / overflow."""
     nbytes = 4 * limbs
-    parts = []
-    for v in values:
-        if v < 0:
-            raise UnsupportedInput("negative big integer in a proof field")
-        if v.bit_length() > 8 * nbytes:
-            raise UnsupportedInput(f"value of {v.bit_length()} bits exceeds the {8 * nbytes}-bit slot")
-        parts.append(v.to_bytes(nbytes, "little"))
-    return np.frombuffer(b"".join(parts), dtype=np.uint32).reshape(len(values), limbs).copy()
+    try:
+        raw = b"".join([v.to_bytes(nbytes, "little") for v in values])
+    except OverflowError:
+        bad = next(v for v in values if v < 0 or v.bit_length() > 8 * nbytes)
+        if bad < 0:
+            raise UnsupportedInput("negative big integer in a proof field") from None
+        raise UnsupportedInput(f"value of {bad.bit_length()} bits exceeds the {8 * nbytes}-bit slot") from None
+    return np.frombuffer(raw, dtype=np.uint32).reshape(len(values), limbs)
 
 
 def pack_points(points):
     """affine (x, y) or None -> (len, 16) uint32, (0,0) = infinity."""
-    parts = []
-    for pt in points:
-        if pt is None:
-            parts.append(b"\x00" * 64)
-        else:
-            parts.append(pt[0].to_bytes(32, "little") + pt[1].to_bytes(32, "little"))
-    return np.frombuffer(b"".join(parts), dtype=np.uint32).reshape(len(points), 16).copy()
+    z = b"\x00" * 64
+    raw = b"".join([z if pt is None else pt[0].to_bytes(32, "little") + pt[1].to_bytes(32, "little")
+                    for pt in points])
+    return np.frombuffer(raw, dtype=np.uint32).reshape(len(points), 16)
 
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+def _bits(values):
+    return max([v.bit_length() for v in values] + [1])
 
 
 class Verdicts:
@@ -61,21 +73,27 @@ class Verdicts:
         self.ped = np.zeros(R + J, np.uint8)
         self.ck = np.zeros(R + J, np.uint8)
         self.dlog = np.zeros(max(J, 1), np.uint8)
+        self._bind(P, R + J, J)
+
+    def _bind(self, P, Mt, J):
         u8 = ctypes.POINTER(ctypes.c_uint8)
-        self.c = VerdictsC(*(a.ctypes.data_as(u8) for a in (self.feldman, self.pdl, self.range, self.ped, self.ck,
-                                                            self.dlog)))
+        arrs = [np.ascontiguousarray(a) for a in (self.feldman, self.pdl, self.range, self.ped, self.ck, self.dlog)]
+        self._keep = arrs
+        self.c = VerdictsC(*(a.ctypes.data_as(u8) for a in arrs), P, Mt, J)
 
 
 class CollectBatch:
     """SoA view of (refresh_messages, local_key, join_messages) for one collect().
 
     `header_only` is set when validate_collect's threshold / size checks fail
-    (refresh_message.rs:149-175): then only the counts are filled and the
-    first error is decided without the GPU."""
+    (refresh_message.rs:149-175), or when the caller asks for it (the rank that
+    maps all-reduced shard verdicts): then only what fsdkr_collect_first_error
+    reads is packed (counts, party indices, lengths, ek.n)."""
 
-    def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048, n_recv=None):
-        """n_recv: receivers (default R + J); a multi-GPU shard passes its slice of
-        the messages together with the full receiver count."""
+    def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048, n_recv=None,
+                 header_only=False):
+        """n_recv: receivers (default R + J); a multi-GPU shard passes its slice of the
+        messages together with the full receiver count."""
         msgs, joins = list(refresh_messages), list(join_messages)
         R, J = len(msgs), len(joins)
         n = n_recv if n_recv else R + J
@@ -89,42 +107,61 @@ class CollectBatch:
         c.party_index, c.msg_lens = self._k(pidx), self._k(lens)
         c.n_recv = n if n_recv else 0
         self.c = c
-        ref = lens[0][0] if R else 0
+        ref = int(lens[0][0]) if R else 0
+        self.ref_len = ref
         # the threshold check (refresh_message.rs:149) is about the whole message set: a
         # multi-GPU shard (n_recv given) holds a slice that may be <= t messages
         below_threshold = R <= local_key.t and not n_recv
-        self.header_only = (below_threshold or R == 0 or any(tuple(l) != (ref, ref, ref) for l in lens[:R])
-                            or ref < n or any(len(m.range_proofs) < n for m in msgs))
-        if self.header_only:
-            return
-        recv_keys = local_key.paillier_key_vec[:n]
-        recv_dlog = local_key.h1_h2_n_tilde_vec[:n]
-        mod_bits = max([k.n.bit_length() for k in recv_keys] + [s.N.bit_length() for s in recv_dlog] +
-                       [m.ring_pedersen_statement.N.bit_length() for m in msgs + joins] +
-                       [m.ek.n.bit_length() for m in msgs + joins] +
-                       [j.dlog_statement.N.bit_length() for j in joins])
-        nl = 64 if mod_bits <= 2048 else 96 if mod_bits <= 3072 else None
-        if nl is None:
-            raise UnsupportedInput(f"{mod_bits}-bit modulus")
-        c.nl = nl
-        pdl = [m.pdl_proof_vec[i] for m in msgs for i in range(n)]
-        rng = [m.range_proofs[i] for m in msgs for i in range(n)]
-        c.s1l = _limbs_for(max([p.s1.bit_length() for p in pdl] + [a.s1.bit_length() for a in rng]))
-        c.s3l = _limbs_for(max([p.s3.bit_length() for p in pdl] + [a.s2.bit_length() for a in rng]))
-        c.el = _limbs_for(max(a.e.bit_length() for a in rng))
+        self.size_fail = below_threshold or R == 0 or any(tuple(l) != (ref, ref, ref) for l in lens[:R]) or ref < n
+        self.header_only = header_only or self.size_fail
+        all_m = msgs + joins
         M = m_security
-        for m in msgs + joins:
-            if len(m.ring_pedersen_proof.A) < M or len(m.ring_pedersen_proof.Z) < M or \
-                    len(m.dk_correctness_proof.sigma_vec) < M2:
-                raise UnsupportedInput("short ring-Pedersen / correct-key vectors (the reference panics)")
-        c.zl = _limbs_for(max(z.bit_length() for m in msgs + joins for z in m.ring_pedersen_proof.Z[:M]))
-        c.yl = _limbs_for(max([j.composite_dlog_proof_base_h1.y.bit_length() for j in joins] +
-                              [j.composite_dlog_proof_base_h2.y.bit_length() for j in joins] + [1]))
+        # ---- widths: nl covers every value of the nl / 2nl slots; ek.n and sigma get ckl
+        ck_bits = _bits([m.ek.n for m in all_m] + [s for m in all_m for s in m.dk_correctness_proof.sigma_vec[:M2]])
+        ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
+        if ckl is None:
+            raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
+        if self.header_only:
+            c.nl = 64 if ck_bits <= 2048 else 96
+            c.ckl = max(ckl, c.nl)
+            c.ck_n = self._k(pack([m.ek.n for m in all_m] or [0], c.ckl))
+            self.nl = c.nl
+            return
+        keys, sts = local_key.paillier_key_vec, local_key.h1_h2_n_tilde_vec
+        avail = min(len(keys), len(sts), n)
+        c.recv_avail = avail if avail < n else 0
+        pdl = [m.pdl_proof_vec[i] for m in msgs for i in range(n)]
+        short_rng = any(len(m.range_proofs) < n for m in msgs)
+        rng = [m.range_proofs[i] if i < len(m.range_proofs) else None for m in msgs for i in range(n)]
+        rng_ok = [a for a in rng if a is not None]
+        recv_vals = [k.n for k in keys[:avail]] + [v for s in sts[:avail] for v in (s.N, s.g, s.ni)]
+        rp_vals = [v for m in all_m for v in (m.ring_pedersen_statement.N, m.ring_pedersen_statement.S,
+                                             m.ring_pedersen_statement.T)] + \
+                  [a for m in all_m for a in m.ring_pedersen_proof.A[:M]]
+        dl_vals = [v for j in joins for v in (j.dlog_statement.N, j.dlog_statement.g, j.dlog_statement.ni,
+                                             j.composite_dlog_proof_base_h1.x, j.composite_dlog_proof_base_h2.x)]
+        one_vals = [v for p in pdl for v in (p.z, p.u3, p.s2)] + [v for a in rng_ok for v in (a.z, a.s)]
+        two_vals = [m.points_encrypted_vec[i] for m in msgs for i in range(n)] + [p.u2 for p in pdl]
+        nl_bits = max(_bits(recv_vals), _bits(rp_vals), _bits(dl_vals), _bits(one_vals), (_bits(two_vals) + 1) // 2)
+        nl = 64 if nl_bits <= 2048 else 96 if nl_bits <= 3072 else None
+        if nl is None:
+            raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
+        c.nl = nl
+        c.ckl = max(ckl, nl)
+        c.s1l = _limbs_for(max(_bits([p.s1 for p in pdl]), _bits([a.s1 for a in rng_ok])))
+        c.s3l = _limbs_for(max(_bits([p.s3 for p in pdl]), _bits([a.s2 for a in rng_ok])))
+        c.el = _limbs_for(_bits([a.e for a in rng_ok]))
+        c.zl = _limbs_for(_bits([z for m in all_m for z in m.ring_pedersen_proof.Z[:M]]))
+        c.yl = _limbs_for(_bits([j.composite_dlog_proof_base_h1.y for j in joins] +
+                                [j.composite_dlog_proof_base_h2.y for j in joins]))
         k = self._k
-        c.recv_n = k(pack([x.n for x in recv_keys], nl))
-        c.recv_ntilde = k(pack([s.N for s in recv_dlog], nl))
-        c.recv_h1 = k(pack([s.g for s in recv_dlog], nl))
-        c.recv_h2 = k(pack([s.ni for s in recv_dlog], nl))
+        # receivers (placeholders past the keys the LocalKey holds: odd modulus 3)
+        rn = [x.n for x in keys[:avail]] + [3] * (n - avail)
+        rst = list(sts[:avail]) + [None] * (n - avail)
+        c.recv_n = k(pack(rn, nl))
+        c.recv_ntilde = k(pack([s.N if s else 3 for s in rst], nl))
+        c.recv_h1 = k(pack([s.g if s else 1 for s in rst], nl))
+        c.recv_h2 = k(pack([s.ni if s else 1 for s in rst], nl))
         c.enc = k(pack([m.points_encrypted_vec[i] for m in msgs for i in range(n)], 2 * nl))
         c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
         c.pdl_z = k(pack([p.z for p in pdl], nl))
@@ -134,27 +171,36 @@ class CollectBatch:
         c.pdl_s1 = k(pack([p.s1 for p in pdl], c.s1l))
         c.pdl_s2 = k(pack([p.s2 for p in pdl], nl))
         c.pdl_s3 = k(pack([p.s3 for p in pdl], c.s3l))
+        if short_rng:   # range_proofs[i] past the vector: placeholder rows, the reference panics there
+            c.range_lens = k(np.array([len(m.range_proofs) for m in msgs], dtype=np.uint32))
+            rng = [a if a is not None else _ZERO_ALICE for a in rng]
         c.rp_z = k(pack([a.z for a in rng], nl))
         c.rp_e = k(pack([a.e for a in rng], c.el))
         c.rp_s = k(pack([a.s for a in rng], nl))
         c.rp_s1 = k(pack([a.s1 for a in rng], c.s1l))
         c.rp_s2 = k(pack([a.s2 for a in rng], c.s3l))
         t = local_key.t
-        vss = []
-        for m in msgs:
-            com = list(m.coefficients_committed_vec.commitments)
-            if len(com) != t + 1:
-                raise UnsupportedInput("commitment vector length != t+1")
-            vss += com
-        c.vss = k(pack_points(vss))
-        all_m = msgs + joins
+        com = [list(m.coefficients_committed_vec.commitments) for m in msgs]
+        if any(len(x) != t + 1 for x in com):   # Horner over each message's own vector
+            c.vss_len = k(np.array([len(x) for x in com], dtype=np.uint32))
+        c.vss = k(pack_points([p for x in com for p in x] or [None]))
         c.ped_S = k(pack([m.ring_pedersen_statement.S for m in all_m], nl))
         c.ped_T = k(pack([m.ring_pedersen_statement.T for m in all_m], nl))
         c.ped_N = k(pack([m.ring_pedersen_statement.N for m in all_m], nl))
-        c.ped_A = k(pack([a for m in all_m for a in m.ring_pedersen_proof.A[:M]], nl))
-        c.ped_Z = k(pack([z for m in all_m for z in m.ring_pedersen_proof.Z[:M]], c.zl))
-        c.ck_n = k(pack([m.ek.n for m in all_m], nl))
-        c.ck_sigma = k(pack([s for m in all_m for s in m.dk_correctness_proof.sigma_vec[:M2]], nl))
+        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
+        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
+        if any(len(a) < M for a in A) or any(len(z) < M for z in Z):
+            c.ped_lens = k(np.array([[len(a), len(z)] for a, z in zip(A, Z)], dtype=np.uint32))
+            A = [a + [0] * (M - len(a)) for a in A]
+            Z = [z + [0] * (M - len(z)) for z in Z]
+        c.ped_A = k(pack([a for row in A for a in row], nl))
+        c.ped_Z = k(pack([z for row in Z for z in row], c.zl))
+        c.ck_n = k(pack([m.ek.n for m in all_m], c.ckl))
+        sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
+        if any(len(x) < M2 for x in sig):
+            c.ck_lens = k(np.array([len(x) for x in sig], dtype=np.uint32))
+            sig = [x + [0] * (M2 - len(x)) for x in sig]
+        c.ck_sigma = k(pack([s for row in sig for s in row], c.ckl))
         if J:
             c.dlog_N = k(pack([j.dlog_statement.N for j in joins], nl))
             c.dlog_g = k(pack([j.dlog_statement.g for j in joins], nl))
@@ -178,3 +224,10 @@ class CollectBatch:
         if rc != 0:
             raise RuntimeError(f"fsdkr_collect_first_error failed ({rc})")
         return err
+
+
+class _ZeroAlice:
+    z = e = s = s1 = s2 = 0
+
+
+_ZERO_ALICE = _ZeroAlice()

@@ -19,7 +19,7 @@ LIB = os.path.join(PKG, "libfsdkr.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["modexp.hip", "fixedbase.hip", "inverse.hip", "vhash.hip", "vmont.hip", "vec.hip",
+SOURCES = ["modexp.hip", "fixedbase.hip", "inverse.hip", "vhash.hip", "vmont.hip", "vec.hip", "pow2.hip",
            "capi.cpp", "collect.cpp", "recover.cpp", "standalone.cpp", "fixedbase_host.cpp"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
           "-Wno-unused-result"]

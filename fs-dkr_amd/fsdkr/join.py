@@ -34,17 +34,29 @@ def validate_collect(ctx, refresh_messages, t, n):
         if not (a == ref and b == ref and c == ref):
             raise FsDkrError("SizeMismatchError", refresh_message_index=k, pdl_proof_len=a,
                              points_commited_len=b, points_encrypted_len=c)
-    # validate_share_public reads points_committed_vec[i] for i < n (index panic past the end)
-    if ref < n:
-        raise FsDkrPanic("validate_collect: points_committed_vec[i] out of bounds")
-    degs = {len(m.coefficients_committed_vec.commitments) for m in msgs}
-    if len(degs) != 1 or min(degs) == 0:
-        raise UnsupportedInput("refresh messages commit to polynomials of different degrees")
-    deg = degs.pop() - 1
-    ok = ctx.feldman_check([list(m.coefficients_committed_vec.commitments) for m in msgs],
-                           [m.points_committed_vec[i] for m in msgs for i in range(n)], n, deg)
-    if not ok.all():
-        raise FsDkrError("PublicShareValidationError")
+    # validate_share_public reads points_committed_vec[i] for i < n: message 0's first
+    # `ref` shares are checked, then the index past the end panics
+    rows = min(ref, n)
+    groups = {}
+    for k, m in enumerate(msgs):
+        groups.setdefault(len(m.coefficients_committed_vec.commitments), []).append(k)
+    ok = {}
+    for ncoef, ks in groups.items():
+        if ncoef == 0:       # curv get_point_commitment: head.unwrap() on an empty vector panics
+            continue
+        v = ctx.feldman_check([list(msgs[k].coefficients_committed_vec.commitments) for k in ks],
+                              [msgs[k].points_committed_vec[i] for k in ks for i in range(rows)], rows, ncoef - 1)
+        for q, k in enumerate(ks):
+            ok[k] = v[q * rows:(q + 1) * rows]
+    for k, m in enumerate(msgs):   # reference order: message by message, share by share
+        if rows == 0 and ref < n:
+            raise FsDkrPanic("validate_collect: points_committed_vec[i] out of bounds")
+        if k not in ok:
+            raise FsDkrPanic("validate_share_public: empty commitment vector (unwrap)")
+        if not ok[k].all():
+            raise FsDkrError("PublicShareValidationError")
+        if ref < n:
+            raise FsDkrPanic("validate_collect: points_committed_vec[i] out of bounds")
 
 
 def verify_ring_pedersen(ctx, messages, m_security=256):

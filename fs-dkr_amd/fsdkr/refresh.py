@@ -5,8 +5,12 @@ Same argument meaning and error behaviour as the reference: returns None on
 success after mutating `local_key` exactly as collect() does, raises
 FsDkrError with the reference's variant name and payload for the FIRST failing
 check (or FsDkrPanic where the reference panics).  All proof verification runs
-in one batched GPU pass (fsdkr_verify_collect); share recovery uses the GPU
-decryption and MSM entry points.  There is no CPU fallback."""
+in one batched GPU pass (fsdkr_collect_launch/finish); the share recovery
+(decryption + pk_vec MSM) runs speculatively on the context's recovery stream
+WHILE the proofs are verified and is discarded if a check fails (its result
+is deterministic, so running it early changes nothing but the latency).
+collect_many() verifies many independent sessions in one device pass
+(BASELINE configs[4]).  There is no CPU fallback."""
 from ._native import Context
 from .batch import CollectBatch
 
@@ -55,6 +59,8 @@ def _lagrange(index, s):
             continue
         num = num * (j + 1) % Q
         den = den * ((j + 1) - xi) % Q
+    if den == 0:
+        raise FsDkrPanic("map_share_to_new_params: repeated party index (zero inverse)")
     return num * pow(den, -1, Q) % Q
 
 
@@ -70,62 +76,236 @@ def _ctx(ctx):
     return _default_ctx
 
 
-def verify(refresh_messages, local_key, join_messages, ctx=None, m_security=256, key_bits=2048):
-    """Verification half of collect(): (error or None, keys_applied, batch)."""
-    batch = CollectBatch(refresh_messages, local_key, join_messages, m_security, key_bits)
-    verdicts = None if batch.header_only else _ctx(ctx).verify_collect(batch)
-    err = batch.first_error(verdicts)
+def _error_of(err):
+    """fsdkr_error -> None | FsDkrError | FsDkrPanic."""
     if err.variant == 0:
-        return None, err.keys_applied, batch
+        return None
     name, fields = _VARIANTS[err.variant]
     vals = {f: (bool(err.f[k]) if f in _BOOL_FIELDS else int(err.f[k])) for k, f in enumerate(fields)}
     if err.panic:
-        return FsDkrPanic(f"reference panics at {name}"), err.keys_applied, batch
-    return FsDkrError(name, **vals), err.keys_applied, batch
+        return FsDkrPanic(f"reference panics at {name}")
+    return FsDkrError(name, **vals)
+
+
+def _short_share_check(ctx, batch, msgs):
+    """validate_collect with points_committed_vec shorter than new_n (:177-188):
+    message 0's first `ref` shares are checked, then index `ref` panics."""
+    m = msgs[0]
+    com = list(m.coefficients_committed_vec.commitments)
+    ref = batch.ref_len
+    if ref and com:
+        ok = ctx.feldman_check([com], list(m.points_committed_vec[:ref]), ref, len(com) - 1)
+        if not ok.all():
+            return FsDkrError("PublicShareValidationError")
+    return FsDkrPanic("validate_collect: points_committed_vec[i] out of bounds")
+
+
+def _mapped(ctx, batch, msgs, verdicts):
+    """(error or None, keys_applied) of one session."""
+    err = batch.first_error(verdicts)
+    e = _error_of(err)
+    if isinstance(e, FsDkrPanic) and err.variant == 2 and batch.size_fail and not batch.c.n_recv and \
+            batch.R > batch.c.t and batch.ref_len < batch.n:
+        e = _short_share_check(ctx, batch, msgs)
+    return e, err.keys_applied
+
+
+def verify(refresh_messages, local_key, join_messages, ctx=None, m_security=256, key_bits=2048):
+    """Verification half of collect(): (error or None, keys_applied, batch)."""
+    ctx = _ctx(ctx)
+    msgs = list(refresh_messages)
+    batch = CollectBatch(msgs, local_key, join_messages, m_security, key_bits)
+    verdicts = None if batch.header_only else ctx.verify_collect(batch)
+    err, applied = _mapped(ctx, batch, msgs, verdicts)
+    return err, applied, batch
+
+
+def _apply_keys(local_key, msgs, joins, applied):
+    # paillier_key_vec is written message by message before a later check fails (:394, :436)
+    for k, m in enumerate(msgs + joins):
+        if k >= applied:
+            break
+        local_key.paillier_key_vec[m.party_index - 1] = m.ek
+
+
+def _apply_share(local_key, new_dk, rec):
+    new_share, y, pk, t_ok = rec
+    local_key.paillier_dk = new_dk
+    local_key.x_i = new_share
+    local_key.y = y
+    for i in range(len(pk)):
+        local_key.pk_vec.insert(i, pk[i])
+    if not t_ok:   # li_vec[j] for j <= local_key.t past the vss threshold (:460-462)
+        raise FsDkrPanic("collect: li_vec index out of bounds (local_key.t > vss threshold)")
 
 
 def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_security=256, key_bits=2048):
     """RefreshMessage::collect (refresh_message.rs:321-467)."""
     ctx = _ctx(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
-    err, applied, batch = verify(msgs, local_key, joins, ctx, m_security, key_bits)
-    # paillier_key_vec is written message by message before a later check fails (:394, :436)
-    for k, m in enumerate(msgs + joins):
-        if k >= applied:
-            break
-        local_key.paillier_key_vec[m.party_index - 1] = m.ek
+    batch = CollectBatch(msgs, local_key, joins, m_security, key_bits)
+    spec = None
+    if batch.header_only:
+        verdicts = None
+    else:
+        ctx.collect_prepare(batch)
+        ctx.collect_launch()
+        spec = _speculative(ctx, [(msgs, local_key, len(msgs) + len(joins))])[0]
+        verdicts = ctx.collect_finish(batch)
+    err, applied = _mapped(ctx, batch, msgs, verdicts)
+    _apply_keys(local_key, msgs, joins, applied)
     if err is not None:
         raise err
-    # ---- share recovery (:367-373, :439-464)
-    t = local_key.vss_scheme.threshold
-    n_new = len(msgs) + len(joins)
-    new_share, y, pk = recover_share(ctx, msgs, local_key.i, t, local_key.paillier_dk, batch.nl, n_new)
-    local_key.paillier_dk = new_dk
-    local_key.x_i = new_share
-    local_key.y = y
-    for i in range(n_new):
-        local_key.pk_vec.insert(i, pk[i])
+    if isinstance(spec, Exception):
+        raise spec
+    _apply_share(local_key, new_dk, spec)
+
+
+def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
+    """Many independent RefreshMessage::collect calls verified in ONE device pass
+    (fsdkr_collect_prepare_multi; BASELINE configs[4]).  `sessions`: list of
+    (refresh_messages, local_key, new_dk, join_messages).  Each session gets the
+    reference's outcome on its own: returns a list with None (local_key
+    updated as collect() does) or the FsDkrError / FsDkrPanic collect() would
+    raise (local_key partially updated as collect() leaves it)."""
+    ctx = _ctx(ctx)
+    sess = [(list(r), lk, dk, list(j)) for r, lk, dk, j in sessions]
+    batches = [CollectBatch(r, lk, j, m_security, key_bits) for r, lk, dk, j in sess]
+    live = [i for i, b in enumerate(batches) if not b.header_only]
+    verdicts = [None] * len(sess)
+    specs = [None] * len(sess)
+    if live:
+        ctx.collect_prepare_many([batches[i] for i in live])
+        ctx.collect_launch()
+        res = _speculative(ctx, [(sess[i][0], sess[i][1], len(sess[i][0]) + len(sess[i][3])) for i in live])
+        for i, r in zip(live, res):
+            specs[i] = r
+        vs = ctx.collect_finish_many([batches[i] for i in live])
+        for i, v in zip(live, vs):
+            verdicts[i] = v
+    out = []
+    for i, (msgs, lk, dk, joins) in enumerate(sess):
+        err, applied = _mapped(ctx, batches[i], msgs, verdicts[i])
+        _apply_keys(lk, msgs, joins, applied)
+        if err is None and isinstance(specs[i], Exception):
+            err = specs[i]
+        if err is None:
+            try:
+                _apply_share(lk, dk, specs[i])
+            except FsDkrPanic as e:
+                err = e
+        out.append(err)
+    return out
+
+
+def _dk_limbs(dk):
+    """Limb width holding N = p q of a decryption key (and p^2, q^2)."""
+    bits = max((dk.p * dk.q).bit_length(), 2 * dk.p.bit_length(), 2 * dk.q.bit_length())
+    for w in (64, 96, 128, 192):
+        if bits <= 32 * w:
+            return w
+    return None
+
+
+def _speculative(ctx, jobs):
+    """Share recovery of every job (msgs, local_key, n_new) on the recovery stream:
+    one batched decryption per key width + one MSM launch for all of them.  Per
+    job: the 4-tuple of recover_share or the exception the reference raises there."""
+    plans = []
+    for msgs, lk, n_new in jobs:
+        try:
+            plans.append(_recovery_plan(msgs, lk, n_new))
+            if _dk_limbs(lk.paillier_dk) is None:
+                plans[-1] = FsDkrPanic("share recovery: decryption key wider than 6144 bits")
+        except (FsDkrPanic, IndexError, AttributeError, TypeError) as e:
+            plans.append(e if isinstance(e, FsDkrPanic) else FsDkrPanic(f"share recovery: {e!r}"))
+    sig_of = {}
+    for w in (64, 96, 128, 192):
+        cts, kidx, ps, qs, owners = [], [], [], [], []
+        for j, (p, (msgs, lk, n_new)) in enumerate(zip(plans, jobs)):
+            if isinstance(p, Exception) or _dk_limbs(lk.paillier_dk) != w:
+                continue
+            owners.append((j, len(cts), len(p["cts"])))
+            for c in p["cts"]:
+                cts.append(c)
+                kidx.append(len(ps))
+            ps.append(lk.paillier_dk.p)
+            qs.append(lk.paillier_dk.q)
+        if not cts:
+            continue
+        try:
+            sig = ctx.paillier_decrypt_many(cts, kidx, ps, qs, w)
+        except ValueError as e:   # a ciphertext wider than N^2 (ints_to_limbs)
+            for j, _, _ in owners:
+                plans[j] = FsDkrPanic(f"share recovery: {e}")
+            continue
+        for j, at, cnt in owners:
+            sig_of[j] = sig[at:at + cnt]
+    return _finish_recovery(ctx, plans, sig_of)
+
+
+def _finish_recovery(ctx, plans, sig_of):
+    """new share = sum_j l_j Dec(c_j) mod N mod q; y and pk_vec by one MSM launch."""
+    rows, scs = [], []
+    width = 1
+    for j, p in enumerate(plans):
+        if isinstance(p, Exception):
+            continue
+        m = sig_of[j]
+        new_share = sum(l * s for l, s in zip(p["li"], m)) % p["N"] % Q
+        p["share"] = new_share
+        rows.append([(GX, GY)])
+        scs.append([new_share])
+        for i in range(p["n_new"]):
+            rows.append(p["pts"][i])
+            scs.append(p["li"][:len(p["pts"][i])])
+        width = max([width] + [len(r) for r in p["pts"]])
+    rows = [r + [None] * (width - len(r)) for r in rows]
+    scs = [r + [0] * (width - len(r)) for r in scs]
+    res = ctx.ec_msm(rows, scs) if rows else []
+    out, pos = [], 0
+    for p in plans:
+        if isinstance(p, Exception):
+            out.append(p)
+            continue
+        y = res[pos]
+        pk = res[pos + 1:pos + 1 + p["n_new"]]
+        pos += 1 + p["n_new"]
+        out.append((p["share"], y, pk, p["t_ok"]))
+    return out
+
+
+def _recovery_plan(msgs, local_key, n_new):
+    """get_ciphertext_sum (:193-237) + the pk_vec loop inputs (:455-464).
+
+    Lagrange weights use the first t+1 messages in slice order, t = the vss
+    threshold (local_key.vss_scheme.parameters); the pk_vec sum runs j over
+    0..=local_key.t (:460).  The GPU decrypts each c_j and the host combines
+    sum_j l_j * Dec(c_j) mod N: decryption is a homomorphism on units of
+    Z_{N^2}, so this equals the reference's decryption of prod_j c_j^l_j *
+    Enc(0) (the Enc(0) factor only re-randomises)."""
+    t_vss = local_key.vss_scheme.threshold
+    indices = [msgs[j].old_party_index - 1 for j in range(t_vss + 1)]
+    li = [_lagrange(indices[j], indices) for j in range(t_vss + 1)]
+    cts = [msgs[j].points_encrypted_vec[local_key.i - 1] for j in range(t_vss + 1)]
+    t_key = local_key.t
+    terms = min(t_key, t_vss) + 1
+    pts = [[msgs[j].points_committed_vec[i] for j in range(terms)] for i in range(n_new)]
+    dk = local_key.paillier_dk
+    return {"li": li, "cts": cts, "pts": pts, "n_new": n_new, "N": dk.p * dk.q, "t_ok": t_key <= t_vss}
 
 
 def recover_share(ctx, msgs, party_index, t, dk, nl, n_new):
     """get_ciphertext_sum + Paillier::decrypt + the pk_vec loop
     (refresh_message.rs:193-237, :439-464; add_party_message.rs:186-213):
-    (new share, G * share, [pk_vec entry for each of the n_new parties]).
-
-    Lagrange weights use the first t+1 messages in slice order.  The GPU
-    decrypts each c_j and combines sum_j l_j * Dec(c_j) mod N: decryption is a
-    homomorphism on units of Z_{N^2}, so this equals the reference's decryption
-    of prod_j c_j^l_j * Enc(0) (the Enc(0) factor only re-randomises)."""
-    indices = [msgs[j].old_party_index - 1 for j in range(t + 1)]
-    li = [_lagrange(indices[j], indices) for j in range(t + 1)]
-    cts = [msgs[j].points_encrypted_vec[party_index - 1] for j in range(t + 1)]
-    sig = ctx.paillier_decrypt(cts, dk.p, dk.q, nl)
-    new_share = sum(l * s for l, s in zip(li, sig)) % (dk.p * dk.q) % Q
-    pts = [[(GX, GY)]] + [[msgs[j].points_committed_vec[i] for j in range(t + 1)] for i in range(n_new)]
-    scs = [[new_share]] + [li[:] for _ in range(n_new)]
-    # one MSM launch: y = G*x, then pk_vec[i] = sum_j P_j,i * l_j  (rows padded to t+1 terms)
-    width = t + 1
-    pts = [row + [None] * (width - len(row)) for row in pts]
-    scs = [row + [0] * (width - len(row)) for row in scs]
-    res = ctx.ec_msm(pts, scs)
-    return new_share, res[0], res[1:]
+    (new share, G * share, [pk_vec entry for each of the n_new parties]),
+    t = the threshold of both the Lagrange set and the pk_vec sum."""
+    class _K:
+        pass
+    lk = _K()
+    lk.vss_scheme = type("V", (), {"threshold": t})()
+    lk.t, lk.i, lk.paillier_dk = t, party_index, dk
+    r = _speculative(ctx, [(msgs, lk, n_new)])[0]
+    if isinstance(r, Exception):
+        raise r
+    return r[0], r[1], r[2]

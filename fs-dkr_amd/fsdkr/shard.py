@@ -1,4 +1,4 @@
-"""Multi-GPU sharding of one collect() verification.
+"""Multi-GPU sharding of one collect().
 
 Rank r of W verifies a contiguous slice of the refresh messages and of the
 join messages' proofs against the FULL receiver set (fsdkr_collect_batch
@@ -7,8 +7,13 @@ zero-filled byte vector laid out as
 
     [feldman R*n | pdl R*n | range R*n | ped R+J | ck R+J | dlog J]
 
-No other data crosses the interconnect."""
+No other data crosses the interconnect.  collect() then maps the merged
+verdicts to the reference's first error on a header-only batch of the whole
+message set (threshold, sizes, party indices, ek.n) and applies collect()'s
+side effects and share recovery (refresh_message.rs:330-464) on every rank."""
 import numpy as np
+
+from .batch import CollectBatch, Verdicts
 
 
 def shard_range(count, world, rank):
@@ -26,33 +31,37 @@ def scatter(v, R, J, n, world, rank):
     j0, j1 = shard_range(J, world, rank)
     P = R * n
     out = np.zeros(global_len(R, J, n), np.uint8)
+    if v is None:
+        return out
     lo, cnt = r0 * n, (r1 - r0) * n
     out[lo:lo + cnt] = v.feldman[:cnt]
     out[P + lo:P + lo + cnt] = v.pdl[:cnt]
     out[2 * P + lo:2 * P + lo + cnt] = v.range[:cnt]
     base_ped, base_ck, base_dl = 3 * P, 3 * P + (R + J), 3 * P + 2 * (R + J)
     nr = r1 - r0
-    for q in range(nr):
-        out[base_ped + r0 + q] = v.ped[q]
-        out[base_ck + r0 + q] = v.ck[q]
-    for q in range(j1 - j0):
-        out[base_ped + R + j0 + q] = v.ped[nr + q]
-        out[base_ck + R + j0 + q] = v.ck[nr + q]
-        out[base_dl + j0 + q] = v.dlog[q]
+    out[base_ped + r0:base_ped + r1] = v.ped[:nr]
+    out[base_ck + r0:base_ck + r1] = v.ck[:nr]
+    nj = j1 - j0
+    out[base_ped + R + j0:base_ped + R + j1] = v.ped[nr:nr + nj]
+    out[base_ck + R + j0:base_ck + R + j1] = v.ck[nr:nr + nj]
+    out[base_dl + j0:base_dl + j1] = v.dlog[:nj]
     return out
 
 
-class MergedVerdicts:
-    """Global verdicts rebuilt from the all-reduced vector (same fields as batch.Verdicts)."""
+class MergedVerdicts(Verdicts):
+    """Global verdicts rebuilt from the all-reduced vector (same fields and C view as batch.Verdicts)."""
 
     def __init__(self, vec, R, J, n):
         P = R * n
+        vec = np.ascontiguousarray(vec, dtype=np.uint8)
         self.feldman = vec[:P]
         self.pdl = vec[P:2 * P]
         self.range = vec[2 * P:3 * P]
         self.ped = vec[3 * P:3 * P + R + J]
         self.ck = vec[3 * P + R + J:3 * P + 2 * (R + J)]
-        self.dlog = vec[3 * P + 2 * (R + J):3 * P + 2 * (R + J) + J]
+        self.dlog = vec[3 * P + 2 * (R + J):3 * P + 2 * (R + J) + J] if J else np.zeros(1, np.uint8)
+        self._vec = vec
+        self._bind(P, R + J, J)
 
 
 def merge(dist, local_vec, device=None):
@@ -64,3 +73,56 @@ def merge(dist, local_vec, device=None):
         t = t.to(device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.cpu().numpy()
+
+
+def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=2048, launch_only=False):
+    """This rank's slice as a CollectBatch (n_recv = n); launched on the GPU.
+    Returns (batch or None, verdicts or None); with launch_only the caller
+    finishes it (ctx.collect_finish) after overlapping host work."""
+    R, J = len(msgs), len(joins)
+    n = R + J
+    r0, r1 = shard_range(R, world, rank)
+    j0, j1 = shard_range(J, world, rank)
+    if r1 == r0 and j1 == j0:
+        return None, None
+    b = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], m_security, key_bits, n_recv=n)
+    if b.header_only:   # an empty refresh slice (joins only) or a size failure the header batch reports
+        return None, None
+    ctx.collect_prepare(b)
+    ctx.collect_launch()
+    if launch_only:
+        return b, None
+    return b, ctx.collect_finish(b)
+
+
+def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, device=None, m_security=256,
+            key_bits=2048):
+    """RefreshMessage::collect (refresh_message.rs:321-467) sharded over the ranks of
+    `dist` (torch.distributed, initialised): every rank holds every message (the
+    broadcast channel of README.md:19) and the same LocalKey; each verifies its
+    slice, the verdict bytes are all-reduced once, and every rank returns the
+    reference's outcome: None after updating `local_key` as collect() does, or
+    raises the FsDkrError / FsDkrPanic collect() raises (with its partial
+    paillier_key_vec updates)."""
+    from .refresh import _apply_keys, _apply_share, _mapped, _speculative
+    world, rank = dist.get_world_size(), dist.get_rank()
+    msgs, joins = list(refresh_messages), list(join_messages)
+    R, J = len(msgs), len(joins)
+    n = R + J
+    header = CollectBatch(msgs, local_key, joins, m_security, key_bits, header_only=True)
+    spec = None
+    if header.size_fail:
+        merged = None
+    else:
+        b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True)
+        # share recovery on the recovery stream while the slice is verified
+        spec = _speculative(ctx, [(msgs, local_key, n)])[0]
+        v = ctx.collect_finish(b) if b is not None else None
+        merged = MergedVerdicts(merge(dist, scatter(v, R, J, n, world, rank), device), R, J, n)
+    err, applied = _mapped(ctx, header, msgs, merged)
+    _apply_keys(local_key, msgs, joins, applied)
+    if err is not None:
+        raise err
+    if isinstance(spec, Exception):
+        raise spec
+    _apply_share(local_key, new_dk, spec)

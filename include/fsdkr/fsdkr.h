@@ -136,25 +136,70 @@ typedef struct fsdkr_collect_batch {
   /* receivers; 0 means R + J.  A multi-GPU shard passes a slice of the refresh
    * messages (and of the joins' proofs) with the full receiver set n. */
   uint32_t n_recv;
+  /* Optional (NULL / 0 = the regular shape):
+   *  vss_len    [R] number of commitments of each coefficients_committed_vec; vss is
+   *             then ragged (sum vss_len points).  curv validate_share_public runs
+   *             Horner over each message's own vector (refresh_message.rs:180-182);
+   *             an empty vector panics (unwrap).  NULL: t+1 each.
+   *  range_lens [R] range_proofs lengths; range_proofs[i] with i >= len panics
+   *             (refresh_message.rs:342).  rp_* rows past the length are placeholders.
+   *  ckl        limbs of ck_n / ck_sigma (64, 96, 128, 192); 0 = nl.  Lets a batch of
+   *             2048-bit receivers carry an oversize ek.n whose correct-key proof the
+   *             reference verifies before it reports ModuliTooSmall (:376-391).
+   *  recv_avail receivers that local_key holds keys for (0 = all n); the reference
+   *             indexes paillier_key_vec[i] / h1_h2_n_tilde_vec[i] (:334-339) and panics
+   *             at the first pair with i >= recv_avail (rows past it are placeholders).
+   *  ped_lens   [R+J][2] lengths of ring_pedersen_proof.A and .Z: A shorter than M
+   *             panics in the challenge hash, Z shorter at check len(Z)
+   *             (ring_pedersen_proof.rs:131-144); missing rows are placeholders.
+   *  ck_lens    [R+J] lengths of dk_correctness_proof.sigma_vec (< 11 panics in
+   *             zk-paillier's verify); missing rows are placeholders. */
+  const uint32_t* vss_len;
+  const uint32_t* range_lens;
+  uint32_t ckl;
+  uint32_t recv_avail;
+  const uint32_t* ped_lens;
+  const uint32_t* ck_lens;
 } fsdkr_collect_batch;
 
-/* Verdicts (caller-allocated). 1 bits mean "check passed". */
+/* Verdicts (caller-allocated). 1 bits mean "check passed".  cap_* are the
+ * element capacities of the arrays; a call fails with FSDKR_E_ARG if the
+ * prepared batch needs more (R*n pairs, R+J messages, J joins). */
 typedef struct fsdkr_verdicts {
-  uint8_t* feldman;  /* [R*n]  validate_share_public                                  */
+  uint8_t* feldman;  /* [R*n]  bit0 validate_share_public ok; bit1: reference panics  */
   uint8_t* pdl;      /* [R*n]  bit0 u1, bit1 u2, bit2 u3 equal; bit3: reference panics */
   uint8_t* range;    /* [R*n]  AliceProof::verify                                      */
   uint8_t* ped;      /* [R+J]  bit0 RingPedersenProof::verify ok; bit1: panics         */
-  uint8_t* ck;       /* [R+J]  NiCorrectKeyProof::verify ok                            */
-  uint8_t* dlog;     /* [J]    bit0 base-h1 proof ok, bit1 base-h2 proof ok           */
+  uint8_t* ck;       /* [R+J]  bit0 NiCorrectKeyProof::verify ok; bit1: reference panics */
+  uint8_t* dlog;     /* [J]    bit0 base-h1 proof ok, bit1 base-h2 proof ok (may be NULL if J = 0) */
+  uint32_t cap_pairs, cap_msgs, cap_joins;
 } fsdkr_verdicts;
 
 int fsdkr_verify_collect(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch, fsdkr_verdicts* out);
 
-/* The same as two phases: prepare = host pre-pass + ONE host->device copy of
- * the batch image (kept in the context); run = the kernel pipeline on the
- * device-resident batch + verdict readback.  run may be repeated. */
+/* The same as phases: prepare = host pre-pass + ONE host->device copy of the
+ * batch image (kept in the context); run = the kernel pipeline on the
+ * device-resident batch + verdict readback (= launch + finish: launch only
+ * enqueues the kernels and returns, so the caller can overlap host work or the
+ * share-recovery calls, which run on their own stream).  run may be repeated;
+ * a failed prepare leaves no batch (run then returns FSDKR_E_ARG). */
 int fsdkr_collect_prepare(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
 int fsdkr_collect_run(fsdkr_ctx* ctx, fsdkr_verdicts* out);
+int fsdkr_collect_launch(fsdkr_ctx* ctx);
+int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
+
+/* ---- Many independent collect() calls in ONE device pass -------------------
+ * `count` sessions (e.g. BASELINE configs[4]: 1024 custody wallets, t=1 n=3,
+ * 3072-bit keys), each the batch its own RefreshMessage::collect
+ * (refresh_message.rs:321-326) would verify; out[s] receives session s's
+ * verdicts.  Sessions may differ in R, J, n, t and limb widths (the device
+ * image uses the widest); m_security must agree.  The reference has no such
+ * entry point: it verifies one session per call.  fsdkr_collect_first_error
+ * then maps each session's verdicts on its own. */
+int fsdkr_verify_collect_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count,
+                               fsdkr_verdicts* out);
+int fsdkr_collect_prepare_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count);
+int fsdkr_collect_finish_multi(fsdkr_ctx* ctx, fsdkr_verdicts* out, uint32_t count);
 
 /* FsDkrError variants, in error.rs declaration order (error.rs:6-60). */
 #define FSDKR_ERR_NONE 0
@@ -180,7 +225,7 @@ typedef struct fsdkr_error {
 } fsdkr_error;
 
 /* Map verdicts to the FIRST failing check in collect() order:
- * threshold, sizes, Feldman (k, i), [PDL then range] (k, i), ring-Pedersen
+ * threshold, sizes, Feldman (k, i), [PDL then range (or its index panic)] (k, i), ring-Pedersen
  * (refresh, then join), per refresh message correct-key then modulus size,
  * per join message index, correct-key, DLog, modulus size.  `verdicts` may be
  * NULL when the threshold or size check already fails.  Pure host logic. */
@@ -207,8 +252,9 @@ int fsdkr_feldman_check(fsdkr_ctx* ctx, uint32_t n_msgs, uint32_t n, uint32_t t,
 /* RingPedersenProof::verify (ring_pedersen_proof.rs:126-157) for `count`
  * independent proofs: S, T, N: [count][nl]; A: [count][M][nl]; Z: [count][M][zl].
  * verdict[m] bit0 = Ok(()), bit1 = the reference panics (challenge shorter
- * than M bits and every check before the panicking index passes); 0 =
- * Err(RingPedersenProofError).  Called by JoinMessage::collect
+ * than M bits and every check before the panicking index passes, or N = 0);
+ * 0 = Err(RingPedersenProofError).  Any N: an even N = 2^k m is checked modulo
+ * m (Montgomery) and modulo 2^k (pow2.hip).  Called by JoinMessage::collect
  * (add_party_message.rs:146-167). */
 int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint32_t m_security, uint32_t zl,
                                const uint32_t* S, const uint32_t* T, const uint32_t* N, const uint32_t* A,
@@ -223,13 +269,23 @@ int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const ui
                            uint32_t* out);
 
 /* ---- share recovery building blocks (refresh_message.rs:367-373, 439-464) ---
+ * Both run on the context's recovery stream, so they overlap a batch started
+ * with fsdkr_collect_launch (collect() recovers the share speculatively while
+ * the proofs are verified and discards it if a check fails).
  * Paillier decryption of `count` ciphertexts [count][2nl] under one key
- * dk = (p, q) (each [nl], zero-padded), kzen-paillier CRT form; the
- * exponentiations run on the GPU.  m_out: [count][nl]. */
+ * dk = (p, q) (each [nl], zero-padded), kzen-paillier CRT form
+ * (Paillier::decrypt, refresh_message.rs:439); the exponentiations and the
+ * CRT constants' inverses run on the GPU.  m_out: [count][nl]. */
 int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c, const uint32_t* p,
                            const uint32_t* q, uint32_t* m_out);
+/* The same for many keys (one per session of fsdkr_verify_collect_multi):
+ * ciphertext k is decrypted under key key_idx[k] of p, q: [n_keys][nl]. */
+int fsdkr_paillier_decrypt_multi(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c,
+                                 const uint32_t* key_idx, const uint32_t* p, const uint32_t* q, uint32_t n_keys,
+                                 uint32_t* m_out);
 /* out[o] = sum_j scalars[o][j] * points[o][j] on secp256k1 (affine 16-limb
- * points, 8-limb scalars reduced mod q on device): pk_vec entries and G*x. */
+ * points, 8-limb scalars reduced mod q on device): pk_vec entries and G*x.
+ * One GPU thread per term, then one per output. */
 int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t* points, const uint32_t* scalars,
                  uint32_t* out);
 
