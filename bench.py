@@ -3,16 +3,21 @@
 n = 64 (60 refresh + 4 JoinMessage replacements, t = 32, 2048-bit Paillier N,
 M = 256) — BASELINE.json configs[2], the configuration the metric is quoted
 on; plus the metric's second half, 4096-bit modexp/s/GPU (exponent N,
-modulus N^2).
+modulus N^2), and BASELINE configs[4] (many independent t=1 n=3 sessions with
+3072-bit keys in one device pass) as an extra object on the same line.
 
-One step = one pass of the batched collect() verification over the
-device-resident batch (fsdkr_collect_run: every PDL, Alice range,
-ring-Pedersen, correct-key and composite-DLog proof and every Feldman check)
-plus verdict readback.  With --gpus N (torchrun) the refresh messages (and
-the joins' proofs) are sharded across ranks and the verdict bitmask is
-all-reduced over RCCL.  Inputs are synthetic, generated on the GPU with a
-seeded prover (fsdkr.synth)."""
+One step = ONE WHOLE collect() call (fsdkr.refresh.collect) on host-resident
+messages: packing of the n x n proof instances into the C-ABI SoA buffers,
+the host pre-pass + one upload (fsdkr_collect_prepare), the kernel pipeline
+(every PDL, Alice range, ring-Pedersen, correct-key and composite-DLog proof
+and every Feldman check), verdict readback, first-error mapping, the
+paillier_key_vec updates and the share recovery (GPU decryption + pk_vec MSM,
+overlapped with the pipeline), on a fresh copy of the LocalKey each step.
+With --gpus N (torchrun) each rank verifies a slice of the messages and the
+verdict bytes are all-reduced over RCCL (fsdkr.shard.collect).  Inputs are
+synthetic, generated on the GPU with a seeded prover (fsdkr.synth)."""
 import argparse
+import copy
 import json
 import os
 import sys
@@ -20,7 +25,7 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
-# collect() runs up to eleven concurrent streams (csrc/collect.cpp stream plan); with
+# collect() runs up to twelve concurrent streams (csrc/collect.cpp stream plan); with
 # HIP's default of 4 hardware queues per process (exported as 4 on the GPU
 # boxes) several of them would share queues and serialise.  Raise it (never
 # lower it) before the HIP runtime initialises.
@@ -41,13 +46,15 @@ def proofs_of(R, J, n):
     return 2 * R * n + (R + J) + (R + J) + 2 * J
 
 
-def collect_work(R, J, n, M=256):
-    """Algorithmic MACs of one collect (SURVEY §8d accounting)."""
-    k, kk = 64, 128
-    pair = (w_modexp(kk, 2048) * 2 + w_modexp(kk, 256) * 2 + w_modexp(k, 769) * 2 + w_modexp(k, 2816) * 2 +
+def collect_work(R, J, n, M=256, k=64):
+    """Algorithmic MACs of one collect (SURVEY §8d accounting); k = limbs of N."""
+    kk = 2 * k
+    b = 32 * k
+    s1, s3 = 769, b + 768
+    pair = (w_modexp(kk, b) * 2 + w_modexp(kk, 256) * 2 + w_modexp(k, s1) * 2 + w_modexp(k, s3) * 2 +
             w_modexp(k, 256) * 2 + 2 * (2 * kk * kk + kk))
-    return R * n * pair + (R + J) * (M * w_modexp(k, 2048) + 11 * w_modexp(k, 2048)) + \
-        J * 2 * (w_modexp(k, 2560) + w_modexp(k, 256))
+    return R * n * pair + (R + J) * (M * w_modexp(k, b) + 11 * w_modexp(k, b)) + \
+        J * 2 * (w_modexp(k, b + 512) + w_modexp(k, 256))
 
 
 def collect_issued(R, J, n, M=256, w=6):
@@ -70,19 +77,31 @@ def collect_issued(R, J, n, M=256, w=6):
     return var + fixed + tables
 
 
-def cpu_baseline(msgs, joins, lk, key_bits, n_pairs, seconds_budget=20.0):
-    """Oracle restatement (bigint via GMP, the reference's own engine), ONE thread,
-    on a bounded sample of the same workload; extrapolated to the n=64 proof mix."""
+def cpu_baseline(batch, verdict_ref, proofs, threads, seconds_budget=12.0):
+    """The C++ restatement of collect()'s verification over GMP (oracle/cpu_baseline.cpp,
+    dlopen libgmp.so.10: the reference's own bignum engine) on this host, on a
+    bounded sample of the SAME packed workload (pairs from the start of the
+    batch, whole ring-Pedersen / correct-key / DLog proofs), on 1 thread and on
+    `threads` threads; extrapolated to the full proof mix.  Its verdicts on the
+    sample are checked against the GPU's."""
+    from oracle import cpu_baseline as cb
+    out = cb.measure(batch, verdict_ref, threads=threads, budget_s=seconds_budget)
+    out["value"] = proofs / out["collect_s"]
+    out["unit"] = "proofs/s"
+    out["kind"] = "port"
+    return out
+
+
+def cpu_baseline_python(msgs, joins, lk, n_pairs):
+    """Fallback when the C++ baseline is not built: the Python oracle, 1 thread."""
     from oracle import range_proofs, ring_pedersen
     from oracle import secp256k1 as ec
     from oracle import zk_pdl_with_slack as pdl
-    from oracle.vss import VerifiableSS
-    from oracle.zk_paillier import CompositeDLogProof, DLogStatement, NiCorrectKeyProof
+    from oracle.zk_paillier import NiCorrectKeyProof
     R, J = len(msgs), len(joins)
     n = R + J
-    t_pair = t_rp = t_ck = t_dl = t_fel = 0.0
-    done_pairs = 0
-    t0 = time.perf_counter()
+    t_pair = 0.0
+    done = 0
     for k in range(R):
         for i in range(n):
             m = msgs[k]
@@ -91,13 +110,12 @@ def cpu_baseline(msgs, joins, lk, key_bits, n_pairs, seconds_budget=20.0):
                                         lk.h1_h2_n_tilde_vec[i].N)
             a = time.perf_counter()
             pdl.verify(m.pdl_proof_vec[i], st)
-            ok = range_proofs.verify(m.range_proofs[i], st.ciphertext, st.ek, lk.h1_h2_n_tilde_vec[i])
+            assert range_proofs.verify(m.range_proofs[i], st.ciphertext, st.ek, lk.h1_h2_n_tilde_vec[i])
             t_pair += time.perf_counter() - a
-            assert ok
-            done_pairs += 1
-            if done_pairs >= n_pairs:
+            done += 1
+            if done >= n_pairs:
                 break
-        if done_pairs >= n_pairs:
+        if done >= n_pairs:
             break
     m = msgs[0]
     a = time.perf_counter()
@@ -106,26 +124,10 @@ def cpu_baseline(msgs, joins, lk, key_bits, n_pairs, seconds_budget=20.0):
     a = time.perf_counter()
     assert NiCorrectKeyProof(m.dk_correctness_proof.sigma_vec).verify(m.ek.n)
     t_ck = time.perf_counter() - a
-    vss = VerifiableSS(lk.t, n, list(m.coefficients_committed_vec.commitments))
-    a = time.perf_counter()
-    for i in range(min(n, 8)):
-        assert vss.validate_share_public(m.points_committed_vec[i], i + 1)
-    t_fel = (time.perf_counter() - a) / min(n, 8)
-    if J:
-        j = joins[0]
-        st = DLogStatement(j.dlog_statement.N, j.dlog_statement.g, j.dlog_statement.ni)
-        a = time.perf_counter()
-        assert CompositeDLogProof(j.composite_dlog_proof_base_h1.x, j.composite_dlog_proof_base_h1.y).verify(st)
-        t_dl = time.perf_counter() - a
-    total = time.perf_counter() - t0
-    per_pair = t_pair / done_pairs
-    t_collect = R * n * (per_pair + t_fel) + (R + J) * (t_rp + t_ck) + 2 * J * t_dl
+    t_collect = R * n * t_pair / done + (R + J) * (t_rp + t_ck)
     return {"value": proofs_of(R, J, n) / t_collect, "unit": "proofs/s", "cores": 1, "kind": "port",
-            "sample": f"oracle (GMP mpz_powm via ctypes), 1 thread: {done_pairs} PDL+Alice pairs, 1 ring-Pedersen,"
-                      f" 1 correct-key, {1 if J else 0} composite-DLog, {min(n, 8)} Feldman checks of the bench"
-                      f" workload ({total:.1f} s); extrapolated to the n={n} proof mix",
-            "per_pair_ms": per_pair * 1e3, "per_ring_pedersen_ms": t_rp * 1e3, "per_correct_key_ms": t_ck * 1e3,
-            "collect_s": t_collect}
+            "sample": f"Python oracle (GMP mpz_powm via ctypes), 1 thread: {done} PDL+Alice pairs, 1 ring-Pedersen, "
+                      f"1 correct-key; extrapolated to the n={n} proof mix (C++ baseline not built)"}
 
 
 def modexp_roofline(ctx, count, reps, seed=1234):
@@ -156,12 +158,14 @@ def modexp_roofline(ctx, count, reps, seed=1234):
         ctx.check(L.fsdkr_modexp_batch_device(ctx.handle, 128, count, d_b.data_ptr(), d_e.data_ptr(), 64, 2048,
                                               d_i.data_ptr(), d_m.data_ptr(), nmod, d_o.data_ptr()))
     once()
+    ctx.set_timing(True)
     ctx.kernel_time_reset()
     t0 = time.perf_counter()
     for _ in range(reps):
         once()
     wall = (time.perf_counter() - t0) / reps
     ms, nl = ctx.kernel_time("modexp")
+    ctx.set_timing(False)
     ms /= max(nl, 1)
     out = d_o.cpu().numpy().view(np.uint32)
     for i in range(0, count, count // 4):
@@ -186,6 +190,61 @@ def pmc_traffic(count):
     return d["hbm_traffic_bytes"] * count / inst, os.path.relpath(files[-1], REPO)
 
 
+def phases(ctx, msgs, lk, joins, key_bits):
+    """One instrumented collect: where the host time of a step goes."""
+    from fsdkr.batch import CollectBatch
+    from fsdkr.refresh import _speculative
+    t0 = time.perf_counter()
+    b = CollectBatch(msgs, lk, joins, 256, key_bits)
+    t1 = time.perf_counter()
+    ctx.collect_prepare(b)
+    t2 = time.perf_counter()
+    ctx.collect_launch()
+    _speculative(ctx, [(msgs, lk, len(msgs) + len(joins))])
+    t3 = time.perf_counter()
+    v = ctx.collect_finish(b)
+    t4 = time.perf_counter()
+    b.first_error(v)
+    t5 = time.perf_counter()
+    # the device pipeline alone on the prepared batch (no host work)
+    ctx.collect_prepare(b)
+    runs = []
+    for _ in range(3):
+        a = time.perf_counter()
+        ctx.collect_run(b)
+        runs.append((time.perf_counter() - a) * 1e3)
+    return b, v, {"pack_ms": (t1 - t0) * 1e3, "prepare_ms": (t2 - t1) * 1e3,
+                  "launch_and_overlapped_recovery_ms": (t3 - t2) * 1e3, "finish_wait_ms": (t4 - t3) * 1e3,
+                  "first_error_ms": (t5 - t4) * 1e3, "device_pipeline_ms": min(runs)}
+
+
+def sessions_bench(ctx, count, steps, seed):
+    """BASELINE configs[4]: `count` independent t=1 n=3 collect() sessions with
+    3072-bit keys, verified in ONE device pass per step (refresh.collect_many:
+    packing, one multi-session image, pipeline, per-session first error, key
+    updates and share recovery)."""
+    from fsdkr import refresh, synth
+    tg = time.perf_counter()
+    sess = synth.synth_sessions(ctx, count, n=3, t=1, seed=seed, key_bits=3072)
+    gen_s = time.perf_counter() - tg
+    work = [[(m, copy.deepcopy(lk), dk, j) for (m, j, lk, dk) in sess] for _ in range(steps + 1)]
+    res = refresh.collect_many(work[0], ctx=ctx, key_bits=3072)
+    assert all(r is None for r in res), "synthetic sessions failed verification"
+    import torch
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        refresh.collect_many(work[s + 1], ctx=ctx, key_bits=3072)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    proofs = count * proofs_of(3, 0, 3)
+    return {"workload": f"{count} independent RefreshMessage::collect sessions, t=1 n=3, 3072-bit Paillier "
+                        f"(BASELINE configs[4]), one device pass per step", "sessions": count,
+            "proofs_per_step": proofs, "steps": steps, "ms_per_step": el * 1e3, "value": proofs / el,
+            "unit": "proofs/s", "sessions_per_s": count / el, "workload_gen_s": gen_s,
+            "data": "synthetic (seeded GPU prover; keys are distinct products of pairs from a shared prime pool)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,8 +256,10 @@ def main():
     ap.add_argument("--key-bits", type=int, default=2048)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--modexp-count", type=int, default=65536)
-    ap.add_argument("--cpu-pairs", type=int, default=400)
+    ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sessions", type=int, default=1024, help="configs[4] sessions (0: skip)")
+    ap.add_argument("--session-steps", type=int, default=2)
     ap.add_argument("--unique-msgs", type=int, default=0,
                     help="generate U distinct refresh messages and tile them to n (n = 256 run; the verifier "
                          "still checks every pair)")
@@ -215,9 +276,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from fsdkr import Context, synth
-    from fsdkr.batch import CollectBatch
-    ctx = Context(device=local, timing=True)
+    from fsdkr import Context, refresh, shard, synth
+    ctx = Context(device=local)
     R, J, t, n = a.n - a.joins, a.joins, a.t, a.n
     tg = time.perf_counter()
     if a.unique_msgs and a.unique_msgs < R:
@@ -226,46 +286,43 @@ def main():
     else:
         msgs, joins, lk = synth.synth_collect(ctx, R, J, t, a.seed, key_bits=a.key_bits)
     gen_s = time.perf_counter() - tg
-    # shard: contiguous slices of the refresh messages and of the joins (fsdkr.shard)
-    from fsdkr import shard
-    sw = a.emulate_shard if (a.emulate_shard and world == 1) else world
-    r0, r1 = shard.shard_range(R, sw, rank)
-    j0, j1 = shard.shard_range(J, sw, rank)
-    batch = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], 256, a.key_bits, n_recv=n)
-    ctx.collect_prepare(batch)
-    P = R * n
+    new_dk = lk.paillier_dk
     dev = torch.device("cuda", local)
-
-    def step():
-        v = ctx.collect_run(batch)
-        if dist is not None:
-            return shard.MergedVerdicts(shard.merge(dist, shard.scatter(v, R, J, n, world, rank), dev), R, J, n)
-        return v
-
-    # per-kernel HIP events cost ~9 ms per collect (tools/ab_collect.py --timing):
-    # the timed region runs without them; one extra step afterwards is timed per kernel
-    ctx.set_timing(False)
-    for _ in range(a.warmup):
-        res = step()
-    if sw != world:       # emulated shard: verdicts cover only this slice; report its step time
+    if a.emulate_shard and world == 1:
+        # analysis only: rank 0's slice of a W-way shard (verification of the slice)
+        from fsdkr.batch import CollectBatch
+        r0, r1 = shard.shard_range(R, a.emulate_shard, 0)
+        j0, j1 = shard.shard_range(J, a.emulate_shard, 0)
+        b = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], 256, a.key_bits, n_recv=n)
+        ctx.collect_prepare(b)
+        for _ in range(a.warmup):
+            ctx.collect_run(b)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            step()
+            ctx.collect_run(b)
         torch.cuda.synchronize()
-        print(json.dumps({"emulated_shard": sw, "refresh_slice": [r0, r1], "join_slice": [j0, j1],
-                          "ms_per_step": (time.perf_counter() - t0) / a.steps * 1e3}), flush=True)
+        print(json.dumps({"emulated_shard": a.emulate_shard, "refresh_slice": [r0, r1], "join_slice": [j0, j1],
+                          "device_ms_per_step": (time.perf_counter() - t0) / a.steps * 1e3}), flush=True)
         return
-    # correctness gate: every synthetic proof verifies
-    assert res.feldman[:P].all() and (res.pdl[:P] == 7).all() and res.range[:P].all() and \
-        (res.ped[:R + J] == 1).all() and res.ck[:R + J].all() and (res.dlog[:J] == 3).all(), \
-        "synthetic workload failed verification"
+    keys = [copy.deepcopy(lk) for _ in range(a.warmup + a.steps)]   # a fresh LocalKey per collect()
+
+    def step(k):
+        if dist is not None:
+            shard.collect(dist, msgs, keys[k], new_dk, joins, ctx, device=dev, key_bits=a.key_bits)
+        else:
+            refresh.collect(msgs, keys[k], new_dk, joins, ctx=ctx, key_bits=a.key_bits)
+
+    # correctness gate: every synthetic proof verifies (collect() raises otherwise)
+    for k in range(a.warmup):
+        step(k)
+    assert keys[0].x_i != lk.x_i and len(keys[0].pk_vec) == n, "collect() did not update the LocalKey"
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for k in range(a.steps):
+        step(a.warmup + k)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -274,25 +331,23 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    ctx.set_timing(True)
-    ctx.kernel_time_reset()
-    step()
-    torch.cuda.synchronize()
-    mx_ms, mx_n = ctx.kernel_time("modexp")
     ms_per_step = elapsed / a.steps * 1e3
     proofs = proofs_of(R, J, n)
     value = proofs * a.steps / elapsed
-    # full-call (PCIe-inclusive) rate: prepare + run, single measurement
-    tp = time.perf_counter()
-    ctx.collect_prepare(batch)
-    ctx.collect_run(batch)
-    full_ms = (time.perf_counter() - tp) * 1e3
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
+    batch, verd, ph = phases(ctx, msgs, lk, joins, a.key_bits)
     roof = modexp_roofline(ctx, a.modexp_count, 3)
-    cpu = None if a.no_cpu_baseline or world > 1 else cpu_baseline(msgs, joins, lk, a.key_bits, a.cpu_pairs)
+    cpu = None
+    if not a.no_cpu_baseline and world == 1:
+        try:
+            cpu = cpu_baseline(batch, verd, proofs, a.cpu_threads)
+        except (ImportError, OSError) as e:
+            cpu = cpu_baseline_python(msgs, joins, lk, 200)
+            cpu["cpp_unavailable"] = str(e)
+    s4 = sessions_bench(ctx, a.sessions, a.session_steps, a.seed + 4) if a.sessions and world == 1 else None
     W_collect = collect_work(R, J, n)
     traffic, traffic_src = pmc_traffic(roof["count"])
     out = {
@@ -303,24 +358,30 @@ def main():
                 (f"; {a.unique_msgs} distinct refresh messages tiled to {R}" if a.unique_msgs and a.unique_msgs < R
                  else ""),
         "config": {"workload": f"RefreshMessage::collect n={n} t={t}: {R} refresh + {J} JoinMessage, M=256, "
-                               f"{a.key_bits}-bit N (BASELINE configs[{3 if n >= 256 else 2}])",
+                               f"{a.key_bits}-bit N (BASELINE configs[{3 if n >= 256 else 2}]); one step = the whole "
+                               f"collect() call (pack, pre-pass + upload, pipeline, first error, key updates, "
+                               f"share recovery)",
                    "n": n, "t": t, "refresh": R, "joins": J,
                    "proofs_per_step": proofs, "parallelism": f"refresh messages sharded over {world} GPU(s)"},
+        "phases_ms": ph,
+        "device_pipeline_proofs_per_s": proofs / (ph["device_pipeline_ms"] * 1e-3),
         "modexp_4096_per_s": roof["modexp_per_s"],
         "roofline": {"bound": "valu-int", "achieved": roof["achieved_mac_per_s"] / 1e12, "peak": PEAK_MAC / 1e12,
                      "unit": "T u32-MAC/s", "frac": roof["achieved_mac_per_s"] / PEAK_MAC, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                      "algorithmic_bytes": roof["count"] * (512 + 256 + 512),
-                     "kernel": "modexp_kernel<144,8,128> (4096-bit modulus N^2, 2048-bit exponent N)",
+                     "kernel": "modexp_kernel (4096-bit modulus N^2, 2048-bit exponent N)",
                      "per_launch": f"{roof['count']} instances x {w_modexp(128, 2048) / 1e6:.2f} M MACs in "
                                    f"{roof['kernel_ms']:.2f} ms (HIP events)"},
         "collect_efficiency": {"algorithmic_mac_per_step": W_collect,
                                "frac_of_peak": W_collect / (ms_per_step * 1e-3) / PEAK_MAC / world,
                                "issued_mac_per_step": collect_issued(R, J, n),
                                "issued_frac_of_peak": collect_issued(R, J, n) / (ms_per_step * 1e-3) / PEAK_MAC
-                               / world},
-        "modexp_kernel_ms_per_step": mx_ms,   # summed over streams, one extra step with HIP events on
-        "full_call_pcie_inclusive_ms": full_ms, "workload_gen_s": gen_s,
+                               / world,
+                               "device_pipeline_frac_of_peak": W_collect / (ph["device_pipeline_ms"] * 1e-3) /
+                               PEAK_MAC},
+        "config4_sessions": s4,
+        "workload_gen_s": gen_s,
         "cpu_baseline": cpu,
     }
     print(json.dumps(out), flush=True)

@@ -157,6 +157,30 @@ def synth_collect_tiled(ctx, R, t, seed, unique, key_bits=2048, M=256):
     return tiled, joins, lk
 
 
+def _drive(B, gens):
+    """Run session generators in lockstep: each yields when it needs the shared
+    Batch run; one GPU pass serves every session's requests."""
+    outs = [None] * len(gens)
+    alive = {}
+    for k, g in enumerate(gens):
+        try:
+            next(g)
+            alive[k] = g
+        except StopIteration as e:
+            outs[k] = e.value
+    while alive:
+        res = B.run()
+        nxt = {}
+        for k, g in alive.items():
+            try:
+                g.send(res)
+                nxt[k] = g
+            except StopIteration as e:
+                outs[k] = e.value
+        alive = nxt
+    return outs
+
+
 def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
     """Messages for one collect() with R refresh and J join messages (n = R+J
     receivers, or n_recv when J = 0): returns (refresh_messages,
@@ -169,9 +193,45 @@ def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
     Mt = R + J
     nk = 2 * n + 2 * Mt                     # receivers: Paillier + N~; messages: new ek + RP key
     kp = _keypairs(gen_primes(ctx, 2 * nk, key_bits // 2, rnd))
+    B = Batch(ctx)
+    return _drive(B, [_session(ctx, B, R, J, t, rnd, n, kp, M)])[0][:3]
+
+
+def synth_sessions(ctx, count, n=3, t=1, seed=0, key_bits=3072, M=256):
+    """`count` independent collect() sessions (BASELINE configs[4]: custody
+    wallets, t=1 n=3, 3072-bit keys), generated in lockstep so each GPU pass
+    serves all sessions.  Keys are products of distinct prime PAIRS drawn from a
+    shared pool (every modulus distinct; the verifier's work is that of
+    independent keys).  Returns [(refresh_messages, join_messages, local_key of
+    party 1, a fresh DecryptionKey for collect's new_dk)]."""
+    rnd = random.Random(seed)
+    per = 2 * n + 2 * n                     # keys per session
+    need = per * count
+    pool = 16
+    while pool * (pool - 1) // 2 < need + need // 4:
+        pool += 16
+    primes = gen_primes(ctx, pool, key_bits // 2, rnd)
+    pairs = set()
+    keys = []
+    while len(keys) < need:
+        a, b = rnd.sample(range(pool), 2)
+        if (min(a, b), max(a, b)) in pairs:
+            continue
+        pairs.add((min(a, b), max(a, b)))
+        p, q = primes[a], primes[b]
+        keys.append((p, q, p * q))
+    B = Batch(ctx)
+    gens = [_session(ctx, B, n, 0, t, random.Random(rnd.getrandbits(64)), n, keys[s * per:(s + 1) * per], M)
+            for s in range(count)]
+    out = _drive(B, gens)
+    return [(m, j, lk, dk) for (m, j, lk, dk) in out]
+
+
+def _session(ctx, B, R, J, t, rnd, n, kp, M):
+    """Generator body of one session (yields where the shared Batch must run)."""
+    Mt = R + J
     recv_kp, nt_kp = kp[:n], kp[n:2 * n]
     ek_kp, rp_kp = kp[2 * n:2 * n + Mt], kp[2 * n + Mt:2 * n + 2 * Mt]
-    B = Batch(ctx)
     # ---- receivers' DLog statements (generate_h1_h2_n_tilde, add_party_message.rs:50-66)
     h1s, xhis, xinvs = [], [], []
     for (p, q, Nt) in nt_kp:
@@ -231,7 +291,7 @@ def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
         dinv = pow(N, -1, phi)
         rho = [_mask(N.bit_length(), H(N, int.from_bytes(SALT, "big"), j)) % N for j in range(M2)]
         ck.append([B.add(r_, dinv, N) for r_ in rho])
-    res = B.run()
+    res = yield
     # h2 depends on round-1 results; second batch: h2^rho, h2^gamma etc.
     h2s = [res[h] for h in h2_h]
     for (k, i), d in pr.items():
@@ -240,7 +300,7 @@ def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
         d["h2g"] = B.add(h2s[i], d["gamma"], Nt)
         d["ah2r"] = B.add(h2s[i], d["arho"], Nt)
         d["ah2g"] = B.add(h2s[i], d["agamma"], Nt)
-    res2 = B.run()
+    res2 = yield
     # ---- EC: committed points, commitments, u1 = G*alpha
     pts_sc = []
     for k in range(R):
@@ -303,7 +363,7 @@ def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
         r2 = rnd.randrange((1 << 512) * Nt)
         jd.append(dict(st1=st1, st2=st2, sec1=xs, sec2=xi, r1=r1, r2=r2, x1=B.add(st1.g, r1, Nt),
                        x2=B.add(st2.g, r2, Nt)))
-    res3 = B.run()
+    res3 = yield
     # ---- build messages
     msgs = []
     for k in range(R):
@@ -350,4 +410,4 @@ def synth_collect(ctx, R, J, t, seed, key_bits=2048, M=256, n_recv=None):
                   paillier_key_vec=[EncryptionKey(kk[2], kk[2] ** 2) for kk in recv_kp], y_sum_s=None,
                   h1_h2_n_tilde_vec=[DLogStatement(nt_kp[i][2], h1s[i], h2s[i]) for i in range(n)],
                   vss_scheme=VerifiableSS(t, n, []), i=1, t=t, n=n)
-    return msgs, joins, lk
+    return msgs, joins, lk, DecryptionKey(ek_kp[0][0], ek_kp[0][1])

@@ -60,15 +60,21 @@ def prove(wit: RingPedersenWitness, st: RingPedersenStatement, M: int, rng) -> R
 
 
 def verify(pf: RingPedersenProof, st: RingPedersenStatement, M: int) -> bool:
-    """:126-157 (returns False for FsDkrError::RingPedersenProofError)."""
+    """:126-157 (returns False for FsDkrError::RingPedersenProofError).  The hash
+    loop indexes A[0..M) first; inside the check loop, bit i of the challenge
+    (BitVec index) and Z[i] are read at iteration i, so a failing check before
+    either index is reached returns the error, not the panic."""
     if len(pf.A) < M:
         raise bigint.PanicError("RingPedersenProof: A shorter than M")
-    bits = challenge_bits(pf.A, M)
-    if len(pf.Z) < M:
-        raise bigint.PanicError("RingPedersenProof: Z shorter than M")
+    eb = bigint.to_bytes(chain_bigint(*pf.A[:M]))
     for i in range(M):
+        if i >= 8 * len(eb):
+            raise bigint.PanicError("RingPedersenProof: challenge shorter than M bits (BitVec index)")
+        bit = (eb[i >> 3] >> (i & 7)) & 1
+        if i >= len(pf.Z):
+            raise bigint.PanicError("RingPedersenProof: Z shorter than M")
         lhs = bigint.mod_pow(st.T, pf.Z[i], st.N)
-        rhs = bigint.mod_mul(pf.A[i], bigint.mod_pow(st.S, bits[i], st.N), st.N)
+        rhs = bigint.mod_mul(pf.A[i], bigint.mod_pow(st.S, bit, st.N), st.N)
         if lhs != rhs:
             return False
     return True

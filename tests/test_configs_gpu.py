@@ -1,0 +1,172 @@
+"""GPU parity at the BASELINE.json configs (VERDICT r1 "do this" 1-2):
+
+  configs[1]  n=16, t=8, 2048-bit: full collect() against the oracle run on the
+              same messages (outcome + updated LocalKey), one tamper per
+              verdict kind, and the frozen n=16 sampled-pairs golden fixture;
+  configs[2]  n=64, t=32, 60 refresh + 4 JoinMessage, 2048-bit: synthetic
+              workload, 64 randomly sampled pairs + 2 ring-Pedersen + the
+              joins' DLog proofs cross-checked with the oracle, 8 injected
+              tampers -> verdict vector == the injected set, first error ==
+              the oracle's;
+  configs[3]  n=256, t=128, 2048-bit (16 distinct messages tiled to 256, every
+              pair verified independently): the same injected-tamper check;
+  configs[4]  many independent t=1 n=3 sessions with 3072-bit keys in ONE
+              device pass (fsdkr_verify_collect_multi / refresh.collect_many):
+              per-session outcome == the oracle's, with tampers in a few
+              sessions.
+"""
+import copy
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import tamper  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _verdicts(ctx, msgs, lk, joins, key_bits=2048):
+    from fsdkr.batch import CollectBatch
+    b = CollectBatch(msgs, lk, joins, 256, key_bits)
+    v = ctx.verify_collect(b)
+    return b, v
+
+
+def _first(b, v):
+    from fsdkr.refresh import _error_of
+    e = _error_of(b.first_error(v))
+    return None if e is None else (e.variant, e.fields)
+
+
+def _sample_pairs_with_oracle(msgs, lk, n, count, seed):
+    rnd = random.Random(seed)
+    R = len(msgs)
+    for _ in range(count):
+        k, i = rnd.randrange(R), rnd.randrange(n)
+        bits, ok = tamper.oracle_pair(msgs[k], lk, i)
+        assert bits == 7 and ok, (k, i, bits, ok)
+
+
+def _tamper_check(ctx, msgs, joins, lk, spec, key_bits=2048):
+    R, J = len(msgs), len(joins)
+    n = R + J
+    m2, j2 = tamper.inject(msgs, joins, spec)
+    pairs, mres, jres, first = tamper.expected(m2, j2, lk, spec, key_bits)
+    b, v = _verdicts(ctx, m2, lk, j2, key_bits)
+    tamper.check_verdicts(v, R, J, n, pairs, mres, jres)
+    assert _first(b, v) == first, (_first(b, v), first)
+    return first
+
+
+# ------------------------------------------------------------------ configs[1]
+def test_config1_n16_t8_full_collect_vs_oracle(gpu_ctx):
+    """configs[1] at full size through the oracle's own prover and collect."""
+    from fsdkr import refresh
+    from oracle import protocol
+    from oracle.rng import Rng
+    rng = Rng("config1-n16")
+    t, n, kb = 8, 16, 2048
+    keys = protocol.simulate_keygen(t, n, rng, kb)
+    msgs, dks = [], []
+    for key in keys:
+        m, dk = protocol.distribute(key.i, key, n, rng, kb)
+        msgs.append(m)
+        dks.append(dk)
+    ko, kg = keys[5].clone(), keys[5].clone()
+    protocol.collect(copy.deepcopy(msgs), ko, dks[5], [], Rng("a8"), kb)
+    refresh.collect(copy.deepcopy(msgs), kg, dks[5], [], ctx=gpu_ctx, key_bits=kb)
+    assert (ko.x_i, ko.y, ko.pk_vec) == (kg.x_i, kg.y, kg.pk_vec)
+    assert [k.n for k in ko.paillier_key_vec] == [k.n for k in kg.paillier_key_vec]
+    # one tamper per verdict kind at configs[1] size: verdicts and first error vs the oracle
+    spec = [("pdl_s3", 3, 11), ("range_s2", 9, 2), ("rp_Z", 12, 200), ("ck", 14, 0)]
+    for sub in ([spec[0]], [spec[1]], [spec[2]], [spec[3]], spec):
+        first = _tamper_check(gpu_ctx, msgs, [], keys[5], sub)
+        assert first is not None
+
+
+# ------------------------------------------------------------------ configs[2]
+@pytest.fixture(scope="module")
+def config2(gpu_ctx):
+    from fsdkr import synth
+    return synth.synth_collect(gpu_ctx, 60, 4, 32, 4242, key_bits=2048)
+
+
+def test_config2_n64_joins_valid_and_sampled(gpu_ctx, config2):
+    msgs, joins, lk = config2
+    b, v = _verdicts(gpu_ctx, msgs, lk, joins)
+    tamper.check_verdicts(v, 60, 4, 64, {}, {}, {})
+    assert _first(b, v) is None
+    _sample_pairs_with_oracle(msgs, lk, 64, 64, seed=2)
+    for m in (msgs[7], joins[2]):
+        assert tamper.oracle_message(m) == (True, True)
+    for j in joins:
+        assert tamper.oracle_dlog(j) == 3
+
+
+def test_config2_n64_injected_tampers(gpu_ctx, config2):
+    msgs, joins, lk = config2
+    spec = [("pdl_s1", 5, 17), ("pdl_u2", 9, 63), ("pdl_s3", 22, 0), ("range_s2", 30, 40), ("range_e", 41, 8),
+            ("rp_Z", 44, 13), ("rp_Z", 61, 250), ("ck", 50, 0), ("dlog", 3, 0)]
+    first = _tamper_check(gpu_ctx, msgs, joins, lk, spec)
+    assert first[0] == "PDLwSlackProof"
+    # only the later kinds: the first error moves down the reference order
+    first = _tamper_check(gpu_ctx, msgs, joins, lk, [("rp_Z", 61, 250), ("ck", 50, 0), ("dlog", 3, 0)])
+    assert first == ("RingPedersenProofError", {})
+    first = _tamper_check(gpu_ctx, msgs, joins, lk, [("ck", 50, 0), ("dlog", 3, 0)])
+    assert first == ("PaillierVerificationError", {"party_index": 51})
+    first = _tamper_check(gpu_ctx, msgs, joins, lk, [("dlog", 3, 0)])
+    assert first == ("DLogProofValidation", {"party_index": 64})
+    first = _tamper_check(gpu_ctx, msgs, joins, lk, [("feldman", 33, 7), ("pdl_s3", 2, 2)])
+    assert first == ("PublicShareValidationError", {})
+
+
+# ------------------------------------------------------------------ configs[3]
+def test_config3_n256_injected_tampers(gpu_ctx):
+    from fsdkr import synth
+    msgs, joins, lk = synth.synth_collect_tiled(gpu_ctx, 256, 128, 77, 16, key_bits=2048)
+    spec = [("pdl_s3", 17, 200), ("range_e", 100, 255), ("pdl_u2", 250, 3), ("rp_Z", 128, 77), ("ck", 255, 0)]
+    first = _tamper_check(gpu_ctx, msgs, joins, lk, spec)
+    assert first[0] == "PDLwSlackProof"
+    _sample_pairs_with_oracle(msgs, lk, 256, 8, seed=3)
+
+
+# ------------------------------------------------------------------ configs[4]
+def test_config4_multi_session_3072(gpu_ctx):
+    """Independent t=1 n=3 sessions with 3072-bit keys in ONE device pass:
+    each session's outcome (and updated LocalKey) equals its own collect() by
+    the oracle (sampled sessions) and by the single-session GPU path; tampered
+    sessions fail with the oracle's error while their neighbours succeed."""
+    from fsdkr import refresh, synth
+    S = 24
+    sessions = synth.synth_sessions(gpu_ctx, S, n=3, t=1, seed=99, key_bits=3072)
+    tampered = {3: [("pdl_s3", 1, 2)], 10: [("rp_Z", 0, 5)], 17: [("ck", 2, 0)], 20: [("range_s2", 2, 0)]}
+    work, expect = [], {}
+    for s, (msgs, joins, lk, dk) in enumerate(sessions):
+        if s in tampered:
+            msgs, joins = tamper.inject(msgs, joins, tampered[s])
+            expect[s] = tamper.expected(msgs, joins, lk, tampered[s], 3072)[3]
+        work.append((msgs, copy.deepcopy(lk), dk, joins))
+    res = refresh.collect_many([(m, lk, dk, j) for m, lk, dk, j in work], ctx=gpu_ctx, key_bits=3072)
+    for s, r in enumerate(res):
+        got = None if r is None else (r.variant, r.fields)
+        assert got == expect.get(s), (s, got, expect.get(s))
+    # untampered sessions: the LocalKey equals the single-session GPU collect and,
+    # for two sampled sessions, the oracle's collect
+    from oracle import protocol
+    from oracle.rng import Rng
+    for s in (0, 7, 23):
+        msgs, joins, lk, dk = sessions[s]
+        single = copy.deepcopy(lk)
+        refresh.collect(msgs, single, dk, joins, ctx=gpu_ctx, key_bits=3072)
+        many = work[s][1]
+        assert (single.x_i, single.y, single.pk_vec) == (many.x_i, many.y, many.pk_vec)
+        if s != 23:
+            ko = copy.deepcopy(lk)
+            protocol.collect(tamper.to_oracle(msgs), ko, dk, [], Rng("a8"), 3072)
+            assert (ko.x_i, ko.y, ko.pk_vec) == (many.x_i, many.y, many.pk_vec)

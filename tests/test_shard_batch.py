@@ -7,6 +7,7 @@ CPU part: packing of every slice.  GPU part: the verdicts of all slices,
 scattered and max-merged exactly as shard.merge's all-reduce does, equal the
 single-batch verdicts (valid and tampered inputs)."""
 import copy
+import dataclasses
 import os
 import sys
 
@@ -79,3 +80,96 @@ def test_sharded_verdicts_equal_single_batch(gpu_ctx, world):
         for f in ("feldman", "pdl", "range", "ped", "ck"):
             assert np.array_equal(getattr(whole, f), getattr(merged, f)), f
     assert merged.pdl[3 * 5 + 1] != 7 and merged.range[1 * 5 + 4] == 0
+
+
+class _Shared:
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.buf = [None] * world
+
+
+class _RankDist:
+    """torch.distributed stand-in for ranks emulated as threads of one process
+    (each with its own HIP context on the one GPU): all_reduce(MAX) over a barrier."""
+
+    class ReduceOp:
+        MAX = "max"
+
+    def __init__(self, shared, rank):
+        self.s, self.rank = shared, rank
+
+    def get_rank(self):
+        return self.rank
+
+    def get_world_size(self):
+        return self.s.world
+
+    def all_reduce(self, t, op):
+        import torch
+        assert op == "max"
+        self.s.buf[self.rank] = t.clone()
+        self.s.bar.wait()
+        m = self.s.buf[0]
+        for x in self.s.buf[1:]:
+            m = torch.maximum(m, x)
+        t.copy_(m)
+        self.s.bar.wait()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tamper", [None, "pdl", "ck"])
+def test_sharded_collect_two_emulated_ranks(gpu_ctx, tamper):
+    """fsdkr.shard.collect with two ranks emulated as threads (one HIP context
+    each, one GPU): every rank's outcome and LocalKey equal the single-process
+    GPU collect() and the oracle's."""
+    import threading
+    from fsdkr import Context, refresh, shard
+    from oracle import protocol
+    from oracle.rng import Rng
+    raw, cls, d = _fixture()
+    kb = raw["meta"]["key_bits"]
+    msgs, key, dk = copy.deepcopy(d["msgs"]), d["keys"][0], d["dks"][0]
+    if tamper == "pdl":
+        p = msgs[3].pdl_proof_vec[1]
+        msgs[3].pdl_proof_vec[1] = dataclasses.replace(p, s3=p.s3 + 1)
+    elif tamper == "ck":
+        sv = msgs[4].dk_correctness_proof.sigma_vec
+        msgs[4].dk_correctness_proof = dataclasses.replace(msgs[4].dk_correctness_proof,
+                                                           sigma_vec=(sv[0] + 1,) + tuple(sv[1:]))
+
+    def outcome(fn):
+        try:
+            fn()
+            return None
+        except Exception as e:
+            return (getattr(e, "variant", "panic"), getattr(e, "fields", {}))
+
+    def summary(k):
+        return (k.x_i, k.y, list(k.pk_vec), [e.n for e in k.paillier_key_vec])
+    single = copy.deepcopy(key)
+    want = outcome(lambda: refresh.collect(copy.deepcopy(msgs), single, dk, [], ctx=gpu_ctx, key_bits=kb))
+    ocls = codec.oracle_classes()
+    od = {k: codec.dec(raw[k], ocls) for k in ("keys", "dks")}
+    sys.path.insert(0, HERE)
+    import tamper as tp
+    ko = od["keys"][0].clone()
+    ow = outcome(lambda: protocol.collect(tp.to_oracle(copy.deepcopy(msgs)), ko, od["dks"][0], [], Rng("a8"), kb))
+    assert want == ow
+    shared = _Shared(2)
+    res = {}
+
+    def rank_main(r):
+        ctx = Context()
+        k = copy.deepcopy(key)
+        res[r] = (outcome(lambda: shard.collect(_RankDist(shared, r), msgs, k, dk, [], ctx, key_bits=kb)), summary(k))
+        ctx.close()
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=240)
+    for r in range(2):
+        assert res[r][0] == want, (r, res[r][0], want)
+        assert res[r][1] == summary(single)
