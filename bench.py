@@ -87,6 +87,7 @@ def cpu_baseline(batch, verdict_ref, proofs, threads, seconds_budget=12.0):
     from oracle import cpu_baseline as cb
     out = cb.measure(batch, verdict_ref, threads=threads, budget_s=seconds_budget)
     out["value"] = proofs / out["collect_s"]
+    out["single_thread_value"] = proofs / out["single_thread_collect_s"]
     out["unit"] = "proofs/s"
     out["kind"] = "port"
     return out

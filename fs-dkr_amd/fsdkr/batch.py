@@ -21,6 +21,7 @@ import ctypes
 
 import numpy as np
 
+from . import _pack
 from ._native import CollectBatchC, ErrorC, VerdictsC, lib
 
 M2 = 11   # zk-paillier NiCorrectKeyProof sigma_vec length
@@ -35,17 +36,23 @@ def _limbs_for(bits):
     return max(1, (bits + 31) // 32)
 
 
+def pack_attr(objs, attr, limbs):
+    """getattr(o, attr) (attr None: o) of every object -> (len, limbs) uint32,
+    little-endian, written in place by the C extension; raises UnsupportedInput
+    on negatives / overflow."""
+    arr = np.empty((len(objs), limbs), dtype=np.uint32)
+    try:
+        _pack.pack(objs, attr, arr, limbs)
+    except ValueError as e:
+        raise UnsupportedInput(str(e)) from None
+    except OverflowError:
+        raise UnsupportedInput(f"value exceeds the {32 * limbs}-bit slot") from None
+    return arr
+
+
 def pack(values, limbs):
     """ints -> (len, limbs) uint32, little-endian; raises on negatives / overflow."""
-    nbytes = 4 * limbs
-    try:
-        raw = b"".join([v.to_bytes(nbytes, "little") for v in values])
-    except OverflowError:
-        bad = next(v for v in values if v < 0 or v.bit_length() > 8 * nbytes)
-        if bad < 0:
-            raise UnsupportedInput("negative big integer in a proof field") from None
-        raise UnsupportedInput(f"value of {bad.bit_length()} bits exceeds the {8 * nbytes}-bit slot") from None
-    return np.frombuffer(raw, dtype=np.uint32).reshape(len(values), limbs)
+    return pack_attr(values, None, limbs)
 
 
 def pack_points(points):
@@ -60,8 +67,12 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
 
 
-def _bits(values):
-    return max([v.bit_length() for v in values] + [1])
+def _bits(values, attr=None):
+    """max bit length (>= 1) of the values (or of their `attr`); negatives -> UnsupportedInput."""
+    try:
+        return max(1, _pack.maxbits(values, attr))
+    except ValueError as e:
+        raise UnsupportedInput(str(e)) from None
 
 
 class Verdicts:
@@ -140,17 +151,18 @@ class CollectBatch:
                   [a for m in all_m for a in m.ring_pedersen_proof.A[:M]]
         dl_vals = [v for j in joins for v in (j.dlog_statement.N, j.dlog_statement.g, j.dlog_statement.ni,
                                              j.composite_dlog_proof_base_h1.x, j.composite_dlog_proof_base_h2.x)]
-        one_vals = [v for p in pdl for v in (p.z, p.u3, p.s2)] + [v for a in rng_ok for v in (a.z, a.s)]
-        two_vals = [m.points_encrypted_vec[i] for m in msgs for i in range(n)] + [p.u2 for p in pdl]
-        nl_bits = max(_bits(recv_vals), _bits(rp_vals), _bits(dl_vals), _bits(one_vals), (_bits(two_vals) + 1) // 2)
+        enc = [m.points_encrypted_vec[i] for m in msgs for i in range(n)]
+        one_bits = max(_bits(pdl, "z"), _bits(pdl, "u3"), _bits(pdl, "s2"), _bits(rng_ok, "z"), _bits(rng_ok, "s"))
+        two_bits = max(_bits(enc), _bits(pdl, "u2"))
+        nl_bits = max(_bits(recv_vals), _bits(rp_vals), _bits(dl_vals), one_bits, (two_bits + 1) // 2)
         nl = 64 if nl_bits <= 2048 else 96 if nl_bits <= 3072 else None
         if nl is None:
             raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
         c.nl = nl
         c.ckl = max(ckl, nl)
-        c.s1l = _limbs_for(max(_bits([p.s1 for p in pdl]), _bits([a.s1 for a in rng_ok])))
-        c.s3l = _limbs_for(max(_bits([p.s3 for p in pdl]), _bits([a.s2 for a in rng_ok])))
-        c.el = _limbs_for(_bits([a.e for a in rng_ok]))
+        c.s1l = _limbs_for(max(_bits(pdl, "s1"), _bits(rng_ok, "s1")))
+        c.s3l = _limbs_for(max(_bits(pdl, "s3"), _bits(rng_ok, "s2")))
+        c.el = _limbs_for(_bits(rng_ok, "e"))
         c.zl = _limbs_for(_bits([z for m in all_m for z in m.ring_pedersen_proof.Z[:M]]))
         c.yl = _limbs_for(_bits([j.composite_dlog_proof_base_h1.y for j in joins] +
                                 [j.composite_dlog_proof_base_h2.y for j in joins]))
@@ -162,23 +174,23 @@ class CollectBatch:
         c.recv_ntilde = k(pack([s.N if s else 3 for s in rst], nl))
         c.recv_h1 = k(pack([s.g if s else 1 for s in rst], nl))
         c.recv_h2 = k(pack([s.ni if s else 1 for s in rst], nl))
-        c.enc = k(pack([m.points_encrypted_vec[i] for m in msgs for i in range(n)], 2 * nl))
+        c.enc = k(pack(enc, 2 * nl))
         c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
-        c.pdl_z = k(pack([p.z for p in pdl], nl))
+        c.pdl_z = k(pack_attr(pdl, "z", nl))
         c.pdl_u1 = k(pack_points([p.u1 for p in pdl]))
-        c.pdl_u2 = k(pack([p.u2 for p in pdl], 2 * nl))
-        c.pdl_u3 = k(pack([p.u3 for p in pdl], nl))
-        c.pdl_s1 = k(pack([p.s1 for p in pdl], c.s1l))
-        c.pdl_s2 = k(pack([p.s2 for p in pdl], nl))
-        c.pdl_s3 = k(pack([p.s3 for p in pdl], c.s3l))
+        c.pdl_u2 = k(pack_attr(pdl, "u2", 2 * nl))
+        c.pdl_u3 = k(pack_attr(pdl, "u3", nl))
+        c.pdl_s1 = k(pack_attr(pdl, "s1", c.s1l))
+        c.pdl_s2 = k(pack_attr(pdl, "s2", nl))
+        c.pdl_s3 = k(pack_attr(pdl, "s3", c.s3l))
         if short_rng:   # range_proofs[i] past the vector: placeholder rows, the reference panics there
             c.range_lens = k(np.array([len(m.range_proofs) for m in msgs], dtype=np.uint32))
             rng = [a if a is not None else _ZERO_ALICE for a in rng]
-        c.rp_z = k(pack([a.z for a in rng], nl))
-        c.rp_e = k(pack([a.e for a in rng], c.el))
-        c.rp_s = k(pack([a.s for a in rng], nl))
-        c.rp_s1 = k(pack([a.s1 for a in rng], c.s1l))
-        c.rp_s2 = k(pack([a.s2 for a in rng], c.s3l))
+        c.rp_z = k(pack_attr(rng, "z", nl))
+        c.rp_e = k(pack_attr(rng, "e", c.el))
+        c.rp_s = k(pack_attr(rng, "s", nl))
+        c.rp_s1 = k(pack_attr(rng, "s1", c.s1l))
+        c.rp_s2 = k(pack_attr(rng, "s2", c.s3l))
         t = local_key.t
         com = [list(m.coefficients_committed_vec.commitments) for m in msgs]
         if any(len(x) != t + 1 for x in com):   # Horner over each message's own vector

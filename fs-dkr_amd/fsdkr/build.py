@@ -61,8 +61,25 @@ def _compile(src, verbose):
     return obj
 
 
+def _build_pack(verbose):
+    """The CPython extension of the batching layer (csrc/pack.c -> fsdkr/_pack*.so)."""
+    import sysconfig
+    src = os.path.join(CSRC, "pack.c")
+    out = os.path.join(PKG, "_pack" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-I", sysconfig.get_paths()["include"], src, "-o", out]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"pack extension build failed:\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def build(verbose=False, force=False):
     os.makedirs(BUILD, exist_ok=True)
+    _build_pack(verbose)
     todo = [s for s in SOURCES if _stale(s, force)]
     objs = [_obj(s) for s in SOURCES]
     if todo:
