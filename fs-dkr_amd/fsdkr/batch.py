@@ -18,6 +18,7 @@ proof runs at its own width before ModuliTooSmall, :376-391).  Still outside
 the representable set (UnsupportedInput): negative BigInts and values wider
 than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
 import ctypes
+import os
 
 import numpy as np
 
@@ -36,17 +37,41 @@ def _limbs_for(bits):
     return max(1, (bits + 31) // 32)
 
 
+def host_threads():
+    """Worker threads of the host gather (FSDKR_HOST_THREADS, else OMP_NUM_THREADS,
+    else the visible cores, at most 16 -- the GPU box's CPU share)."""
+    for k in ("FSDKR_HOST_THREADS", "OMP_NUM_THREADS"):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return min(int(v), 64)
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cores = os.cpu_count() or 1
+    return max(1, min(cores, 16))
+
+
+def _gather(objs, attr=None):
+    try:
+        return _pack.gather(objs, attr)
+    except ValueError as e:
+        raise UnsupportedInput(str(e)) from None
+
+
+def _convert(jobs, threads=1):
+    try:
+        _pack.convert(jobs, threads)
+    except OverflowError as e:
+        raise UnsupportedInput(str(e)) from None
+
+
 def pack_attr(objs, attr, limbs):
     """getattr(o, attr) (attr None: o) of every object -> (len, limbs) uint32,
     little-endian, written in place by the C extension; raises UnsupportedInput
     on negatives / overflow."""
     arr = np.empty((len(objs), limbs), dtype=np.uint32)
-    try:
-        _pack.pack(objs, attr, arr, limbs)
-    except ValueError as e:
-        raise UnsupportedInput(str(e)) from None
-    except OverflowError:
-        raise UnsupportedInput(f"value exceeds the {32 * limbs}-bit slot") from None
+    h, _ = _gather(objs, attr)
+    _convert([(h, arr, limbs)])
     return arr
 
 
@@ -55,24 +80,37 @@ def pack(values, limbs):
     return pack_attr(values, None, limbs)
 
 
-def pack_points(points):
-    """affine (x, y) or None -> (len, 16) uint32, (0,0) = infinity."""
-    z = b"\x00" * 64
-    raw = b"".join([z if pt is None else pt[0].to_bytes(32, "little") + pt[1].to_bytes(32, "little")
-                    for pt in points])
-    return np.frombuffer(raw, dtype=np.uint32).reshape(len(points), 16)
+def pack_points(points, attr=None):
+    """affine (x, y) or None (or their `attr`) -> (len, 16) uint32, (0,0) = infinity."""
+    arr = np.empty((len(points), 16), dtype=np.uint32)
+    try:
+        _pack.points(points, attr, arr)
+    except (ValueError, OverflowError) as e:
+        raise UnsupportedInput(str(e)) from None
+    return arr
+
+
+class _Gather:
+    """Every big-integer field of one batch: gathered once (max bit lengths for the
+    slot widths), converted together on host_threads() workers."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def field(self, objs, attr=None):
+        return _gather(objs, attr) + (len(objs),)
+
+    def slot(self, f, limbs):
+        arr = np.empty((f[2], limbs), dtype=np.uint32)
+        self.jobs.append((f[0], arr, limbs))
+        return arr
+
+    def run(self):
+        _convert(self.jobs, host_threads())
 
 
 def _ptr(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
-
-
-def _bits(values, attr=None):
-    """max bit length (>= 1) of the values (or of their `attr`); negatives -> UnsupportedInput."""
-    try:
-        return max(1, _pack.maxbits(values, attr))
-    except ValueError as e:
-        raise UnsupportedInput(str(e)) from None
 
 
 class Verdicts:
@@ -127,100 +165,96 @@ class CollectBatch:
         self.header_only = header_only or self.size_fail
         all_m = msgs + joins
         M = m_security
+        G = _Gather()
+        k = self._k
         # ---- widths: nl covers every value of the nl / 2nl slots; ek.n and sigma get ckl
-        ck_bits = _bits([m.ek.n for m in all_m] + [s for m in all_m for s in m.dk_correctness_proof.sigma_vec[:M2]])
+        sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
+        f_ckn = G.field([m.ek.n for m in all_m] or [0])
+        ck_bits = max(1, f_ckn[1])
+        if not self.header_only:
+            ck_short = any(len(x) < M2 for x in sig)
+            f_sig = G.field([s for row in sig for s in row + [0] * (M2 - len(row))])
+            ck_bits = max(ck_bits, f_sig[1])
         ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
         if ckl is None:
             raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
         if self.header_only:
             c.nl = 64 if ck_bits <= 2048 else 96
             c.ckl = max(ckl, c.nl)
-            c.ck_n = self._k(pack([m.ek.n for m in all_m] or [0], c.ckl))
+            c.ck_n = k(G.slot(f_ckn, c.ckl))
+            G.run()
             self.nl = c.nl
             return
         keys, sts = local_key.paillier_key_vec, local_key.h1_h2_n_tilde_vec
         avail = min(len(keys), len(sts), n)
         c.recv_avail = avail if avail < n else 0
         pdl = [m.pdl_proof_vec[i] for m in msgs for i in range(n)]
-        short_rng = any(len(m.range_proofs) < n for m in msgs)
-        rng = [m.range_proofs[i] if i < len(m.range_proofs) else None for m in msgs for i in range(n)]
-        rng_ok = [a for a in rng if a is not None]
-        recv_vals = [k.n for k in keys[:avail]] + [v for s in sts[:avail] for v in (s.N, s.g, s.ni)]
-        rp_vals = [v for m in all_m for v in (m.ring_pedersen_statement.N, m.ring_pedersen_statement.S,
-                                             m.ring_pedersen_statement.T)] + \
-                  [a for m in all_m for a in m.ring_pedersen_proof.A[:M]]
-        dl_vals = [v for j in joins for v in (j.dlog_statement.N, j.dlog_statement.g, j.dlog_statement.ni,
-                                             j.composite_dlog_proof_base_h1.x, j.composite_dlog_proof_base_h2.x)]
-        enc = [m.points_encrypted_vec[i] for m in msgs for i in range(n)]
-        one_bits = max(_bits(pdl, "z"), _bits(pdl, "u3"), _bits(pdl, "s2"), _bits(rng_ok, "z"), _bits(rng_ok, "s"))
-        two_bits = max(_bits(enc), _bits(pdl, "u2"))
-        nl_bits = max(_bits(recv_vals), _bits(rp_vals), _bits(dl_vals), one_bits, (two_bits + 1) // 2)
+        if any(len(m.range_proofs) < n for m in msgs):
+            # range_proofs[i] past the vector: placeholder rows, the reference panics there
+            c.range_lens = k(np.array([len(m.range_proofs) for m in msgs], dtype=np.uint32))
+            rng = [m.range_proofs[i] if i < len(m.range_proofs) else _ZERO_ALICE for m in msgs for i in range(n)]
+        else:
+            rng = [m.range_proofs[i] for m in msgs for i in range(n)]
+        # receivers (placeholders past the keys the LocalKey holds: odd modulus 3)
+        rst = list(sts[:avail]) + [None] * (n - avail)
+        F = {
+            "recv_n": G.field([x.n for x in keys[:avail]] + [3] * (n - avail)),
+            "recv_ntilde": G.field([s.N if s else 3 for s in rst]),
+            "recv_h1": G.field([s.g if s else 1 for s in rst]),
+            "recv_h2": G.field([s.ni if s else 1 for s in rst]),
+            "enc": G.field([m.points_encrypted_vec[i] for m in msgs for i in range(n)]),
+        }
+        for a in ("z", "u2", "u3", "s1", "s2", "s3"):
+            F["pdl_" + a] = G.field(pdl, a)
+        for a in ("z", "e", "s", "s1", "s2"):
+            F["rp_" + a] = G.field(rng, a)
+        for a in ("S", "T", "N"):
+            F["ped_" + a] = G.field([m.ring_pedersen_statement for m in all_m], a)
+        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
+        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
+        if any(len(x) < M for x in A) or any(len(z) < M for z in Z):
+            c.ped_lens = k(np.array([[len(x), len(z)] for x, z in zip(A, Z)], dtype=np.uint32))
+        F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
+        F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
+        if J:
+            for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
+                F["dlog_" + name] = G.field([j.dlog_statement for j in joins], attr)
+            for name, which, attr in (("x1", 1, "x"), ("x2", 2, "x"), ("y1", 1, "y"), ("y2", 2, "y")):
+                F["dlog_" + name] = G.field([getattr(j, f"composite_dlog_proof_base_h{which}") for j in joins], attr)
+
+        def bits(*names):
+            return max([1] + [F[x][1] for x in names if x in F])
+
+        one_bits = bits("pdl_z", "pdl_u3", "pdl_s2", "rp_z", "rp_s")
+        two_bits = bits("enc", "pdl_u2")
+        nl_bits = max(bits("recv_n", "recv_ntilde", "recv_h1", "recv_h2"), bits("ped_N", "ped_S", "ped_T", "ped_A"),
+                      bits("dlog_N", "dlog_g", "dlog_ni", "dlog_x1", "dlog_x2"), one_bits, (two_bits + 1) // 2)
         nl = 64 if nl_bits <= 2048 else 96 if nl_bits <= 3072 else None
         if nl is None:
             raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
         c.nl = nl
         c.ckl = max(ckl, nl)
-        c.s1l = _limbs_for(max(_bits(pdl, "s1"), _bits(rng_ok, "s1")))
-        c.s3l = _limbs_for(max(_bits(pdl, "s3"), _bits(rng_ok, "s2")))
-        c.el = _limbs_for(_bits(rng_ok, "e"))
-        c.zl = _limbs_for(_bits([z for m in all_m for z in m.ring_pedersen_proof.Z[:M]]))
-        c.yl = _limbs_for(_bits([j.composite_dlog_proof_base_h1.y for j in joins] +
-                                [j.composite_dlog_proof_base_h2.y for j in joins]))
-        k = self._k
-        # receivers (placeholders past the keys the LocalKey holds: odd modulus 3)
-        rn = [x.n for x in keys[:avail]] + [3] * (n - avail)
-        rst = list(sts[:avail]) + [None] * (n - avail)
-        c.recv_n = k(pack(rn, nl))
-        c.recv_ntilde = k(pack([s.N if s else 3 for s in rst], nl))
-        c.recv_h1 = k(pack([s.g if s else 1 for s in rst], nl))
-        c.recv_h2 = k(pack([s.ni if s else 1 for s in rst], nl))
-        c.enc = k(pack(enc, 2 * nl))
+        c.s1l = _limbs_for(bits("pdl_s1", "rp_s1"))
+        c.s3l = _limbs_for(bits("pdl_s3", "rp_s2"))
+        c.el = _limbs_for(bits("rp_e"))
+        c.zl = _limbs_for(bits("ped_Z"))
+        c.yl = _limbs_for(bits("dlog_y1", "dlog_y2"))
+        width = {"enc": 2 * nl, "pdl_u2": 2 * nl, "pdl_s1": c.s1l, "rp_s1": c.s1l, "pdl_s3": c.s3l, "rp_s2": c.s3l,
+                 "rp_e": c.el, "ped_Z": c.zl, "dlog_y1": c.yl, "dlog_y2": c.yl}
+        for name, f in F.items():
+            setattr(c, name, k(G.slot(f, width.get(name, nl))))
+        c.ck_n = k(G.slot(f_ckn, c.ckl))
+        if ck_short:
+            c.ck_lens = k(np.array([len(x) for x in sig], dtype=np.uint32))
+        c.ck_sigma = k(G.slot(f_sig, c.ckl))
+        G.run()
         c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
-        c.pdl_z = k(pack_attr(pdl, "z", nl))
-        c.pdl_u1 = k(pack_points([p.u1 for p in pdl]))
-        c.pdl_u2 = k(pack_attr(pdl, "u2", 2 * nl))
-        c.pdl_u3 = k(pack_attr(pdl, "u3", nl))
-        c.pdl_s1 = k(pack_attr(pdl, "s1", c.s1l))
-        c.pdl_s2 = k(pack_attr(pdl, "s2", nl))
-        c.pdl_s3 = k(pack_attr(pdl, "s3", c.s3l))
-        if short_rng:   # range_proofs[i] past the vector: placeholder rows, the reference panics there
-            c.range_lens = k(np.array([len(m.range_proofs) for m in msgs], dtype=np.uint32))
-            rng = [a if a is not None else _ZERO_ALICE for a in rng]
-        c.rp_z = k(pack_attr(rng, "z", nl))
-        c.rp_e = k(pack_attr(rng, "e", c.el))
-        c.rp_s = k(pack_attr(rng, "s", nl))
-        c.rp_s1 = k(pack_attr(rng, "s1", c.s1l))
-        c.rp_s2 = k(pack_attr(rng, "s2", c.s3l))
+        c.pdl_u1 = k(pack_points(pdl, "u1"))
         t = local_key.t
         com = [list(m.coefficients_committed_vec.commitments) for m in msgs]
         if any(len(x) != t + 1 for x in com):   # Horner over each message's own vector
             c.vss_len = k(np.array([len(x) for x in com], dtype=np.uint32))
         c.vss = k(pack_points([p for x in com for p in x] or [None]))
-        c.ped_S = k(pack([m.ring_pedersen_statement.S for m in all_m], nl))
-        c.ped_T = k(pack([m.ring_pedersen_statement.T for m in all_m], nl))
-        c.ped_N = k(pack([m.ring_pedersen_statement.N for m in all_m], nl))
-        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
-        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
-        if any(len(a) < M for a in A) or any(len(z) < M for z in Z):
-            c.ped_lens = k(np.array([[len(a), len(z)] for a, z in zip(A, Z)], dtype=np.uint32))
-            A = [a + [0] * (M - len(a)) for a in A]
-            Z = [z + [0] * (M - len(z)) for z in Z]
-        c.ped_A = k(pack([a for row in A for a in row], nl))
-        c.ped_Z = k(pack([z for row in Z for z in row], c.zl))
-        c.ck_n = k(pack([m.ek.n for m in all_m], c.ckl))
-        sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
-        if any(len(x) < M2 for x in sig):
-            c.ck_lens = k(np.array([len(x) for x in sig], dtype=np.uint32))
-            sig = [x + [0] * (M2 - len(x)) for x in sig]
-        c.ck_sigma = k(pack([s for row in sig for s in row], c.ckl))
-        if J:
-            c.dlog_N = k(pack([j.dlog_statement.N for j in joins], nl))
-            c.dlog_g = k(pack([j.dlog_statement.g for j in joins], nl))
-            c.dlog_ni = k(pack([j.dlog_statement.ni for j in joins], nl))
-            c.dlog_x1 = k(pack([j.composite_dlog_proof_base_h1.x for j in joins], nl))
-            c.dlog_x2 = k(pack([j.composite_dlog_proof_base_h2.x for j in joins], nl))
-            c.dlog_y1 = k(pack([j.composite_dlog_proof_base_h1.y for j in joins], c.yl))
-            c.dlog_y2 = k(pack([j.composite_dlog_proof_base_h2.y for j in joins], c.yl))
         self.nl = nl
 
     def _k(self, arr):

@@ -92,13 +92,17 @@ def vss_share(ctx, t, n, secret, sample_below=None):
 
 
 def collect(self_msg, refresh_messages, paillier_key, join_messages, t, n, ctx=None, m_security=256,
-            missing_dlog_statement=None, sample_below=None):
+            missing_dlog_statement=None, sample_below=None, key_bits=2048, rng=None):
     """JoinMessage::collect (add_party_message.rs:136-294) -> LocalKey.
 
-    `missing_dlog_statement(party)` supplies the DLogStatement of a party index
-    with no message (the reference generates a fresh one there,
-    :262-263 -> generate_dlog_statement_proofs: key generation, out of scope);
-    `sample_below` injects the randomness of the new VSS polynomial (:279)."""
+    A party index with no message gets a freshly generated DLogStatement, as
+    the reference does (:257-266 -> generate_dlog_statement_proofs().0, a new
+    PAILLIER_KEY_SIZE keypair with h2 = h1^xhi, :50-66): by default on the GPU
+    (fsdkr.distribute.generate_h1_h2_n_tilde: batched prime search + modexp;
+    the two composite proofs the reference computes and discards are skipped).
+    `missing_dlog_statement(party)` overrides it (injected statements);
+    `rng` (sample_below(upper)) injects the generator's randomness and
+    `sample_below` that of the new VSS polynomial (:279)."""
     ctx = _ctx(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
     validate_collect(ctx, msgs, t, n)
@@ -144,8 +148,9 @@ def collect(self_msg, refresh_messages, paillier_key, join_messages, t, n, ctx=N
         elif missing_dlog_statement is not None:
             h1_h2.append(missing_dlog_statement(p))
         else:
-            raise UnsupportedInput(f"party {p} has no DLogStatement; pass missing_dlog_statement "
-                                   "(the reference generates a fresh one: key generation is out of scope)")
+            from .distribute import SystemRng, generate_h1_h2_n_tilde
+            n_tilde, h1, h2, _, _ = generate_h1_h2_n_tilde(ctx, rng or SystemRng(), key_bits)
+            h1_h2.append(DLogStatement(n_tilde, h1, h2))
     for m in msgs:                                                     # :271-275
         if m.public_key != msgs[0].public_key:
             raise FsDkrError("BroadcastedPublicKeyError")

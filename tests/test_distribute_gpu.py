@@ -87,3 +87,13 @@ def test_join_distribute_and_replace_match_oracle(gpu_ctx):
     assert lk.i == 4 and lk.y_sum_s == msgs[0].public_key
     # both ends of the refresh agree on the joiner's public share
     assert k1.pk_vec[3] == lk.pk_vec[3]
+    # a party with no message (party 3 here): JoinMessage::collect generates its
+    # DLogStatement (add_party_message.rs:257-266) -- on the GPU, equal to the
+    # oracle's generate_h1_h2_n_tilde under the same draws
+    lk2 = join.collect(jg, copy.deepcopy(msgs[:2]), jkg, [], t, n, ctx=gpu_ctx, key_bits=kb, rng=Rng("miss"))
+    n_tilde, h1, h2, _, _ = protocol.generate_h1_h2_n_tilde(kb, Rng("miss"))
+    st = lk2.h1_h2_n_tilde_vec[2]
+    assert (st.N, st.g, st.ni) == (n_tilde, h1, h2)
+    assert [s.N for s in lk2.h1_h2_n_tilde_vec[:2]] == [s.N for s in lk.h1_h2_n_tilde_vec[:2]]
+    assert lk2.x_i == lk.x_i and lk2.pk_vec == lk.pk_vec   # the first t+1 messages fix the share
+    assert lk2.paillier_key_vec[2].n == 0                  # EncryptionKey(0, 0) for the missing party

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Device-pipeline profile target: K collect_run calls (no host work between
+launches beyond the verdict readback, 20 ms idle gaps so tools/prof_summary.py
+--gap can cut the steps) on BASELINE configs[2] (n=64 + 4 joins) or, with
+--sessions S, on S independent t=1 n=3 3072-bit sessions (configs[4])."""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--sessions", type=int, default=0)
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--joins", type=int, default=4)
+    ap.add_argument("--t", type=int, default=32)
+    a = ap.parse_args()
+    import torch  # noqa: F401
+    from fsdkr import Context, synth
+    from fsdkr.batch import CollectBatch
+    ctx = Context()
+    if a.sessions:
+        sess = synth.synth_sessions(ctx, a.sessions, n=3, t=1, seed=5, key_bits=3072)
+        batches = [CollectBatch(m, lk, j, 256, 3072) for (m, j, lk, dk) in sess]
+        ctx.collect_prepare_many(batches)
+        for _ in range(a.steps):
+            time.sleep(0.02)
+            t0 = time.perf_counter()
+            ctx.collect_launch()
+            ctx.collect_finish_many(batches)
+            print(f"multi-session run {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+        return
+    msgs, joins, lk = synth.synth_collect(ctx, a.n - a.joins, a.joins, a.t, 2024)
+    b = CollectBatch(msgs, lk, joins, 256, 2048)
+    ctx.collect_prepare(b)
+    for _ in range(a.steps):
+        time.sleep(0.02)
+        t0 = time.perf_counter()
+        ctx.collect_run(b)
+        print(f"collect_run {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()

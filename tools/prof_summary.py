@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=2)
+    ap.add_argument("--gap", type=float, default=0.0, help="split steps at device idle gaps of this many ms")
     a = ap.parse_args()
     rows = load(a.trace)
     by = {}
@@ -43,12 +44,23 @@ def main():
     for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
         print(f"{k:44s} {len(v):6d} {sum(v):10.3f} {statistics.mean(v):9.3f} {min(v):9.3f} {max(v):9.3f} "
               f"{100 * sum(v) / tot:6.2f}")
-    idx = [i for i, r in enumerate(rows) if "pdl_hash" in r[0]]
-    if len(idx) > a.step:
-        i0 = idx[a.step]
-        i1 = idx[a.step + 1] if a.step + 1 < len(idx) else len(rows)
+    if a.gap:
+        # steps = bursts of kernels separated by >= gap ms of device idle time
+        idx, end = [], None
+        for i, r in enumerate(rows):
+            if "copyBuffer" in r[0]:
+                continue
+            if end is None or r[1] - end > a.gap * 1e6:
+                idx.append(i)
+            end = r[2] if end is None else max(end, r[2])
+    else:
+        idx = [i for i, r in enumerate(rows) if "pdl_hash" in r[0]]
+    step = a.step if a.step >= 0 else len(idx) + a.step
+    if 0 <= step < len(idx):
+        i0 = idx[step]
+        i1 = idx[step + 1] if step + 1 < len(idx) else len(rows)
         t0 = rows[i0][1]
-        print(f"\ntimeline of collect step {a.step} (ms from pdl_hash start; stream/queue ids from the trace)")
+        print(f"\ntimeline of collect step {a.step} (ms from the step's first kernel; stream/queue ids from the trace)")
         for r in rows[i0:i1]:
             if "copyBuffer" in r[0]:
                 continue
