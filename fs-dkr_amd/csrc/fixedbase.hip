@@ -69,7 +69,8 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
       for (int j = 0; j < L; ++j) stream[g * L + j] = acc[j];
     }
     __builtin_amdgcn_wave_barrier();
-    M.mul(acc, acc, stream);
+    if (st == 0) M.mul(acc, acc, stream);
+    else M.sqr(acc, acc, stream);
     if (st == 0 || (st % a.w) == 0) {
 #pragma unroll
       for (int j = 0; j < L; ++j) T[(size_t)entry * KD + g * L + j] = acc[j];

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __rest
   for (int s = 0; s < S; ++s) {
     lds_put<KD, G>(stream, y, g);
     __builtin_amdgcn_wave_barrier();
-    M.mul(y, y, stream);
+    M.sqr(y, y, stream);
     __builtin_amdgcn_wave_barrier();
   }
   M.carry_exact(y);
@@ -127,7 +127,8 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
     return (uint32_t)(mk64(v0, v1) >> sh) & (tsize - 1);
   };
   // Every Montgomery product of the exponentiation is acc <- acc * stream, issued
-  // from this ONE site so the unrolled product body exists once in the I-cache.
+  // from two sites (squaring rows for the ladder's squarings, plain rows for the
+  // rest) so each unrolled product body exists once in the I-cache.
   //   step 0                      : stream = R^2            -> acc = xm, T[1] = xm
   //   step 1 .. tsize-2           : stream = T[1]           -> T[step+1]
   //   then per window k=1..nwin-1 : w x (stream = acc), then stream = T[d_k]
@@ -164,7 +165,8 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
       for (int j = 0; j < L; ++j) stream[g * L + j] = src[g * L + j];
     }
     __builtin_amdgcn_wave_barrier();
-    M.mul(acc, acc, stream);
+    if (from_acc) M.sqr(acc, acc, stream);   // the ladder's squarings: tournament rows
+    else M.mul(acc, acc, stream);
     if (st < n_build) {
 #pragma unroll
       for (int j = 0; j < L; ++j) T[(size_t)(st + 1) * KD + g * L + j] = acc[j];

@@ -174,11 +174,38 @@ struct Mont29 {
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  // Squaring rows (SQ): of the pair products a_r a_p (p = g L + j) a row issues
+  // only the slots of a cyclic tournament over d = (j - r) mod L, uniform across
+  // the group's lanes (r mod L = R is a compile-time row of the cycle):
+  //   d = 0                        a_r   * a_p   (the diagonal, and the pairs
+  //                                               p = r mod L of other lanes,
+  //                                               issued from both rows)
+  //   1 <= d < L/2 (L odd: <= L/2)  2 a_r * a_p   (row p skips this pair)
+  //   d = L/2 (L even)             a_r   * a_p   (both rows issue it)
+  // so every unordered pair is counted twice and every a_r^2 once: (L+1)/2
+  // (L odd) or L/2 + 1 (L even) MACs per row instead of L.  A pair {r, p} is
+  // issued in a row <= r + p, so the column a row retires holds the same value
+  // as in the plain product: identical m digits, bit-identical results.  A
+  // column now gains < 2^59.6 per row (2 a_r < 2^30.01), so L <= 21 rows fit a
+  // 64-bit accumulator between normalisations (NSTEP <= 18, L <= 18 here).
+  static constexpr bool sq_raw(int d) { return d == 0 || (L % 2 == 0 && d == L / 2); }
+  static constexpr bool sq_dbl(int d) { return d > 0 && (L % 2 == 1 ? d <= L / 2 : d < L / 2); }
+
   // one CIOS row at rotation R (logical column j lives in slot (j+R)%L)
-  template <int R>
+  template <int R, bool SQ>
   __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, const uint32_t* n, uint32_t ai) const {
+    if constexpr (SQ) {
+      const uint32_t a2 = ai << 1;
 #pragma unroll
-    for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], ai, b[j]);
+      for (int j = 0; j < L; ++j) {
+        const int d = (j - R % L + L) % L;
+        if (sq_raw(d)) mac(acc[(j + R) % L], ai, b[j]);
+        else if (sq_dbl(d)) mac(acc[(j + R) % L], a2, b[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], ai, b[j]);
+    }
     constexpr int s0 = R % L, s1 = (R + 1) % L;
     const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
 #pragma unroll
@@ -192,16 +219,22 @@ struct Mont29 {
     if constexpr (ROW_FENCE) __builtin_amdgcn_sched_barrier(0);
   }
 
-  template <int... Rs>
+  template <bool SQ, int... Rs>
   __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* arow,
                                         std::integer_sequence<int, Rs...>) const {
-    (row<Rs>(acc, b, n, arow[Rs]), ...);
+    (row<Rs, SQ>(acc, b, n, arow[Rs]), ...);
   }
 
   // out = a * b / R  (almost Montgomery, < 2N), b = this lane's L digits (regs),
   // a = full KD-digit operand in LDS.  out may alias b.  (Non-const: b and n
   // pass through opaque(), which leaves their values unchanged.)
-  __device__ __forceinline__ void mul(uint32_t* out, uint32_t* b, const uint32_t* a_lds) {
+  __device__ __forceinline__ void mul(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<false>(out, b, a_lds); }
+  // out = a^2 / R where a_lds holds the same value as b (squaring rows above)
+  __device__ __forceinline__ void sqr(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<true>(out, b, a_lds); }
+
+  template <bool SQ>
+  __device__ __forceinline__ void product(uint32_t* out, uint32_t* b, const uint32_t* a_lds) {
+    static_assert(!SQ || NORM_IN_CYCLE || L <= 21, "squaring rows: column bound");
     uint64_t acc[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) acc[j] = 0;
@@ -210,7 +243,7 @@ struct Mont29 {
       // values unchanged; only the optimiser's view of them is reset (see opaque)
       opaque<L>(b);
       opaque<L>(n);
-      cycle(acc, b, n, a_lds + cyc * L, std::make_integer_sequence<int, L>{});
+      cycle<SQ>(acc, b, n, a_lds + cyc * L, std::make_integer_sequence<int, L>{});
     }
     // rotation is back to identity; two more carry steps give digits <= 2^29+127
     norm_step<0>(acc);

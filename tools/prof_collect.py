@@ -10,7 +10,10 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+# --hwq N sets the hardware queue count exactly (1 serialises every stream: each
+# kernel's standalone full-chip duration); default: at least 12 like bench.py
+_hwq = next((sys.argv[i + 1] for i, x in enumerate(sys.argv[:-1]) if x == "--hwq"), None)
+os.environ["GPU_MAX_HW_QUEUES"] = _hwq or str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
 def main():
@@ -20,6 +23,7 @@ def main():
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--joins", type=int, default=4)
     ap.add_argument("--t", type=int, default=32)
+    ap.add_argument("--hwq", type=int, default=0)
     a = ap.parse_args()
     import torch  # noqa: F401
     from fsdkr import Context, synth
