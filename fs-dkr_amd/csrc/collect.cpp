@@ -1034,6 +1034,12 @@ static int collect_launch_impl(Ctx* c) {
     const char* e = getenv("FSDKR_COLLECT_GA_G");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
+  // J2 / J5 (256-bit challenge exponents) lanes per instance: FSDKR_COLLECT_J2_G / _J5_G
+  auto env_group = [](const char* k, uint32_t dflt) -> uint32_t {
+    const char* e = getenv(k);
+    return e ? (uint32_t)atoi(e) : dflt;
+  };
+  const uint32_t j2_group = env_group("FSDKR_COLLECT_J2_G", 8), j5_group = env_group("FSDKR_COLLECT_J5_G", 8);
   uint32_t ga_group = 8;
   for (uint32_t g : {16u, kWideGroup})
     if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
@@ -1168,7 +1174,7 @@ static int collect_launch_impl(Ctx* c) {
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
     if (ga_first & 2) (void)hipStreamWaitEvent(ss, ga_done, 0);
-    if ((rc = launch_group(2, ss, 0, 8, cons_nn))) return rc;
+    if ((rc = launch_group(2, ss, 0, j2_group, cons_nn))) return rc;
     InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
                   PX(pl.x_unn), nullptr, pl.n_inv_nn};
     c->mark("inverse", true, ss);
@@ -1198,7 +1204,7 @@ static int collect_launch_impl(Ctx* c) {
       (void)hipEventDestroy(r2);
     }
     if (ga_first & 4) (void)hipStreamWaitEvent(js, ga_done, 0);
-    if ((rc = launch_group(3, js, prio[3], 8, cons_nl))) return rc;
+    if ((rc = launch_group(3, js, prio[3], j5_group, cons_nl))) return rc;
     InverseArgs b1{(const uint64_t*)(dev + pl.d_iynl), (const uint64_t*)(dev + pl.d_imnl), PX(pl.x_invz),
                    PX(pl.x_uzA), nullptr, P};
     c->mark("inverse", true, js);

@@ -240,12 +240,12 @@ hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_
   }
 }
 
-// Lanes per instance.  L = KD/G = 18 digits per lane is the most efficient per
-// MAC once a launch fills the chip (no in-cycle normalisation, 3 waves/SIMD:
-// profiles/r01_modexp_group_sweep_*); a launch that cannot fill it runs with
-// more lanes per instance (L = 9) for lower latency: the largest G whose lanes
-// still fit the resident-wave capacity.  G = 2 (2048-bit) / 4 (4096-bit) only
-// when forced.
+// Lanes per instance.  A launch that cannot fill the chip runs with more lanes
+// per instance for lower latency: the largest G whose lanes still fit the
+// resident-wave capacity.  Past that capacity the throughput shape: 2048-bit
+// G = 4 (L = 18: no in-cycle normalisation, profiles/r01_modexp_group_sweep_*),
+// 4096-bit G = 4 (L = 36; with squaring rows it edges out L = 18 by 4%,
+// profiles/r02h_modexp_sqr.jsonl).  G = 2 (2048-bit) only when forced.
 // ModexpArgs.group or FSDKR_MODEXP_G=<G> force a group size (tuning, tests).
 static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int> allowed, int min_auto) {
   static int forced_env = -1;
@@ -275,7 +275,9 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
     case 128:
       // 32 lanes only on explicit request: it needs KD = 160 constants (mod_setup_g)
       if (a.group == kWideGroup) return launch_modexp<160, 32, 128>(a, st);
-      switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 8)) {
+      // a launch past the resident-lane capacity: 4 lanes (L = 36, squaring rows
+      // with 19 + 36 MACs per row) beat 8 (L = 18) by 4% (profiles/r02h_modexp_sqr.jsonl)
+      switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
         case 16: return launch_modexp<144, 16, 128>(a, st);
         case 8: return launch_modexp<144, 8, 128>(a, st);
         default: return launch_modexp<144, 4, 128>(a, st);
