@@ -208,11 +208,17 @@ def pmc_traffic(count):
 
 
 def phases(ctx, msgs, lk, joins, key_bits):
-    """One instrumented collect: where the host time of a step goes."""
+    """One instrumented collect: where the host time of a step goes (stage-1
+    pack, GA prestart, stage-2 pack overlapping the prestarted chains, prepare,
+    launch + overlapped recovery, finish wait, first error)."""
     from fsdkr.batch import CollectBatch
     from fsdkr.refresh import _speculative
     t0 = time.perf_counter()
-    b = CollectBatch(msgs, lk, joins, 256, key_bits)
+    b = CollectBatch(msgs, lk, joins, 256, key_bits, staged=True)
+    ts = time.perf_counter()
+    ctx.collect_prestart(b)
+    tp = time.perf_counter()
+    b.complete()
     t1 = time.perf_counter()
     ctx.collect_prepare(b)
     t2 = time.perf_counter()
@@ -230,7 +236,8 @@ def phases(ctx, msgs, lk, joins, key_bits):
         a = time.perf_counter()
         ctx.collect_run(b)
         runs.append((time.perf_counter() - a) * 1e3)
-    return b, v, {"pack_ms": (t1 - t0) * 1e3, "prepare_ms": (t2 - t1) * 1e3,
+    return b, v, {"pack_stage1_ms": (ts - t0) * 1e3, "prestart_ms": (tp - ts) * 1e3,
+                  "pack_stage2_ms": (t1 - tp) * 1e3, "prepare_ms": (t2 - t1) * 1e3,
                   "launch_and_overlapped_recovery_ms": (t3 - t2) * 1e3, "finish_wait_ms": (t4 - t3) * 1e3,
                   "first_error_ms": (t5 - t4) * 1e3, "device_pipeline_ms": min(runs)}
 

@@ -376,6 +376,7 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   fsdkr::free_collect_plan(c);
+  fsdkr::free_ga_pre(c);
   delete c;
 }
 

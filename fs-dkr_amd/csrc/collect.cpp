@@ -208,6 +208,10 @@ struct CollectPlan {
   std::vector<uint32_t> ped_zlen;          // readable Z entries (M: all); A short: ped_mode 2
   std::vector<uint8_t> ck_short;           // sigma_vec shorter than 11 (or n = 0): zk-paillier panics
   std::vector<uint8_t> ck_one;             // n = 1: the proof verifies trivially
+  // s^N mod N^2 results computed by fsdkr_collect_prestart (ga_hit): the eq / prod3
+  // operands read them from the prestart buffer once ga_done has fired
+  bool ga_hit = false;
+  hipEvent_t ga_done = nullptr;
   FbJob fb;
   size_t d_FB = 0;
   uint32_t* fb_table = nullptr;
@@ -219,6 +223,108 @@ struct CollectPlan {
 void free_collect_plan(Ctx* c) {
   delete reinterpret_cast<CollectPlan*>(c->plan);
   c->plan = nullptr;
+}
+
+// The long-exponent job GA's J1 half (s2^N | s^N mod N^2 per pair, 2P 4096-bit
+// chains: the critical path of the pipeline) started by fsdkr_collect_prestart
+// from the few fields it reads, while the caller still packs the rest of the
+// batch.  A later prepare of a batch with the same values consumes the results.
+struct GaPre {
+  bool valid = false;
+  uint32_t nl = 0, n = 0, R = 0;
+  std::vector<uint32_t> recv_n, s2, s;   // the inputs, for the match in prepare
+  uint32_t* out = nullptr;               // [2P][nn]: J1 instance order (s2^N rows, then s^N rows)
+  hipEvent_t done = nullptr;
+};
+
+void free_ga_pre(Ctx* c) {
+  GaPre* g = reinterpret_cast<GaPre*>(c->ga_pre);
+  if (g && g->done) (void)hipEventDestroy(g->done);
+  delete g;
+  c->ga_pre = nullptr;
+}
+
+static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
+  if (!c->ga_pre) c->ga_pre = new GaPre();
+  GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
+  g.valid = false;
+  const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
+  if (running && running->launched) {
+    c->fail("fsdkr_collect_prestart: a batch is in flight (call finish first)");
+    return FSDKR_E_ARG;
+  }
+  if (!b || !(b->nl == 64 || b->nl == 96) || !b->recv_n || !b->pdl_s2 || !b->rp_s) {
+    c->fail("fsdkr_collect_prestart: needs nl, recv_n, pdl_s2 and rp_s");
+    return FSDKR_E_ARG;
+  }
+  const uint32_t nl = b->nl, nn = 2 * nl, R = b->n_refresh;
+  const uint32_t n = b->n_recv ? b->n_recv : R + b->n_join;
+  const uint32_t P = R * n;
+  if (P == 0 || n < R) return FSDKR_OK;   // nothing to start (prepare reports bad shapes)
+  for (uint32_t i = 0; i < n; ++i)
+    if (!is_odd(b->recv_n + (size_t)i * nl)) return FSDKR_OK;   // prepare reports it
+  g.recv_n.assign(b->recv_n, b->recv_n + (size_t)n * nl);
+  g.s2.assign(b->pdl_s2, b->pdl_s2 + (size_t)P * nl);
+  g.s.assign(b->rp_s, b->rp_s + (size_t)P * nl);
+  // image: [N^2 | N | s2 | s | descriptors], outputs after it
+  auto al = Img::al;
+  const size_t o_NN = 0, o_rn = al((size_t)n * nn * 4), o_s2 = o_rn + al((size_t)n * nl * 4),
+               o_s = o_s2 + al((size_t)P * nl * 4), o_desc = o_s + al((size_t)P * nl * 4);
+  const size_t desc_bytes = (size_t)2 * P * 32, o_out = o_desc + al(desc_bytes);
+  const size_t total = o_out + (size_t)2 * P * nn * 4;
+  uint8_t* dev = (uint8_t*)c->buf("collect_ga", total);
+  if (!dev) {
+    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
+    return FSDKR_E_OOM;
+  }
+  std::vector<uint8_t> img(o_out, 0);
+  uint32_t recvn_max = 1;
+  for (uint32_t r = 0; r < n; ++r) {
+    const uint32_t* Np = b->recv_n + (size_t)r * nl;
+    const hbn::Limbs N = hbn::from(Np, nl);
+    hbn::store(hbn::mul(N, N), reinterpret_cast<uint32_t*>(img.data() + o_NN) + (size_t)r * nn, nn);
+    recvn_max = std::max(recvn_max, hbn::bitlen(Np, nl));
+  }
+  memcpy(img.data() + o_rn, b->recv_n, (size_t)n * nl * 4);
+  memcpy(img.data() + o_s2, b->pdl_s2, (size_t)P * nl * 4);
+  memcpy(img.data() + o_s, b->rp_s, (size_t)P * nl * 4);
+  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
+  ModexpJob J1;
+  J1.k32 = nn;
+  for (int which = 0; which < 2; ++which)   // the order prepare's J1 uses
+    for (uint32_t p = 0; p < P; ++p) {
+      const uint32_t r = p % n;
+      J1.add(DI((which == 0 ? o_s2 : o_s) + (size_t)p * nl * 4), nl, DI(o_rn + (size_t)r * nl * 4), nl, recvn_max, r);
+    }
+  std::vector<uint8_t> desc;
+  J1.pack(desc);
+  memcpy(img.data() + o_desc, desc.data(), desc.size());
+  hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
+  StreamScope scope(c, gs);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, gs), "prestart H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // img is pageable and local
+    return rc;
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons, "collect_ga_nn"))) return rc;
+  g.out = reinterpret_cast<uint32_t*>(dev + o_out);
+  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 3, 8))) return rc;
+  if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
+  g.nl = nl;
+  g.n = n;
+  g.R = R;
+  g.valid = true;
+  return FSDKR_OK;
+}
+
+// does the prestarted GA belong to this (single-session) batch?
+static bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* b, uint32_t n) {
+  const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
+  if (!g || !g->valid || g->nl != b->nl || g->n != n || g->R != b->n_refresh) return false;
+  const size_t P = (size_t)b->n_refresh * n;
+  return memcmp(g->recv_n.data(), b->recv_n, (size_t)n * b->nl * 4) == 0 &&
+         memcmp(g->s2.data(), b->pdl_s2, P * b->nl * 4) == 0 && memcmp(g->s.data(), b->rp_s, P * b->nl * 4) == 0;
 }
 
 // ------------------------------------------------------------------------------
@@ -305,6 +411,13 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   for (uint32_t p = 0; p < P; ++p) {
     const Sess& x = pl.ss[sess_of_pair[p]];
     recv_of_pair[p] = x.rbase + (p - x.pbase) % x.n;
+  }
+  // a prestarted GA of this batch: J1 is not launched again
+  pl.ga_hit = count == 1 && ga_pre_matches(c, bs, pl.ss[0].n);
+  GaPre* gpre = reinterpret_cast<GaPre*>(c->ga_pre);
+  if (pl.ga_hit) {
+    pl.ga_done = gpre->done;
+    gpre->valid = false;   // consumed (the buffer lives until the next prestart)
   }
   clk.lap("shapes");
 
@@ -622,6 +735,10 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   //   FB (nl, fixed bases h1_i, h2_i, T_m) = h2^s3 | h2^s2A [2P], h1^s1 | h1^s1A [2P], T^Z [Mt*M]
   const size_t x_GA = OUT((size_t)3 * P * nn * 4 + 4);
   const size_t x_J1 = x_GA, x_J9 = x_GA + (size_t)2 * P * nn * 4;
+  // J1 result row k (device address): the GA job's output, or the prestart buffer
+  auto J1_at = [&](size_t k) -> uint64_t {
+    return pl.ga_hit ? (uint64_t)(uintptr_t)(gpre->out + k * nn) : 0;
+  };
   const size_t x_J2 = OUT((size_t)2 * P * nn * 4);
   const size_t x_J5 = OUT((size_t)2 * P * nl * 4);
   const size_t x_GD = OUT(((size_t)4 * J + 1) * nl * 4);
@@ -694,7 +811,8 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
       const uint32_t r = recv_of_pair[p];
       const uint64_t Ni = DI(o_rn + (size_t)r * nl * 4);
       // J1: s2^N (PDL, zk_pdl_with_slack.rs:129-135) | s^N (Alice, range_proofs.rs:148)
-      J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
+      if (!pl.ga_hit)
+        J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
       const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
       if (which == 0) J2.add(cp, nn, DX(x_epdl + (size_t)p * 32), 8, 256, r);
@@ -799,7 +917,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   for (uint32_t p = 0; p < P; ++p) {  // PDL u2: (N+1)^s1 * s2^N == u2 * c^e  (mod N^2), u2 < N^2
     EqOperand& e = eq_nn[p];
     e.a = pdl_small[p] ? DX(x_Bpdl + (size_t)p * nn * 4) : DX(x_J9 + (size_t)j9_index[p] * nn * 4);
-    e.b = DX(x_J1 + (size_t)p * nn * 4);
+    e.b = pl.ga_hit ? J1_at(p) : DX(x_J1 + (size_t)p * nn * 4);
     e.c = DI(o_pu2 + (size_t)p * nn * 4);
     e.d = DX(x_J2 + (size_t)p * nn * 4);
     e.a_len = e.b_len = e.c_len = e.d_len = nn;
@@ -869,7 +987,8 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   // prod3 descriptors: u = gs1 * s^N * (c^e)^-1  (mod N^2) | w = h1^s1 * h2^s2 * (z^e)^-1 (mod N~)
   std::vector<Prod3Operand> p3_nn(P), p3_nl(P);
   for (uint32_t p = 0; p < P; ++p) {
-    p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), DX(x_J1 + ((size_t)P + p) * nn * 4), DX(x_invc + (size_t)p * nn * 4),
+    p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), pl.ga_hit ? J1_at((size_t)P + p) : DX(x_J1 + ((size_t)P + p) * nn * 4),
+                DX(x_invc + (size_t)p * nn * 4),
                 nn, nn, nn, 0};
     p3_nl[p] = {DX(x_J3 + ((size_t)P + p) * nl * 4), DX(x_J4 + ((size_t)P + p) * nl * 4),
                 DX(x_invz + (size_t)p * nl * 4), nl, nl, nl, 0};
@@ -971,7 +1090,8 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   pl.n_p2 = n_p2;
   pl.n_mods_nl = n_mods_nl;
   pl.x_epdl = x_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
-  const size_t xs[CollectPlan::NJOB] = {x_GA, x_GD, x_J2, x_J5, x_GC};
+  // with a prestarted J1 the GA job is J9 alone, written where J9's rows live
+  const size_t xs[CollectPlan::NJOB] = {pl.ga_hit ? x_J9 : x_GA, x_GD, x_J2, x_J5, x_GC};
   const size_t ds[CollectPlan::NJOB] = {d_GA, d_GD, d_J2, d_J5, d_GC};
   const ModexpJob* js[CollectPlan::NJOB] = {&GA, &GD, &J2, &J5, &GC};
   for (int k = 0; k < CollectPlan::NJOB; ++k) {
@@ -1221,6 +1341,7 @@ static int collect_launch_impl(Ctx* c) {
     (void)hipStreamWaitEvent(st, ev, 0);
     (void)hipEventDestroy(ev);
   }
+  if (pl.ga_hit) (void)hipStreamWaitEvent(st, pl.ga_done, 0);   // the prestarted s^N rows
   // equality checks and exact products
   {
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqnn), PI(pl.d_eqnnm), cons_nn, PX(pl.x_pbits), DI(pl.o_one),
@@ -1509,6 +1630,12 @@ int fsdkr_collect_prepare_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch
 
 int fsdkr_collect_prepare(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
   return fsdkr_collect_prepare_multi(ctx, batch, 1);
+}
+
+int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
+  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  return fsdkr::collect_prestart_impl(c, batch);
 }
 
 int fsdkr_collect_launch(fsdkr_ctx* ctx) {

@@ -37,6 +37,7 @@ struct Ctx {
   static constexpr int NSIDE = 11;
   hipStream_t side[NSIDE] = {};   // concurrent streams for independent jobs (lazily created)
   void* plan = nullptr;           // prepared collect() batch (collect.cpp)
+  void* ga_pre = nullptr;         // prestarted s^N mod N^2 job (fsdkr_collect_prestart)
   // pinned host arena for the collect() image (grow-only; one H2D copy per prepare)
   uint8_t* pinned = nullptr;
   size_t pinned_bytes = 0;
@@ -136,6 +137,7 @@ inline uint8_t ped_verdict(const uint32_t* eq, uint32_t M, uint32_t panic_word) 
   return panic_word ? 2 : 1;
 }
 void free_collect_plan(Ctx* c);
+void free_ga_pre(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
                       uint32_t group = 0);
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,

@@ -219,10 +219,23 @@ struct Mont29 {
     if constexpr (ROW_FENCE) __builtin_amdgcn_sched_barrier(0);
   }
 
+  // row R with its streamed digit already in `cur`; first issues the LDS read of
+  // the next row's digit (the next cycle's first digit after the last row), so
+  // the read's latency hides behind this row's MACs instead of stalling the
+  // next row (one wave per SIMD in latency-bound launches has no other wave
+  // to cover it).  arow[L] past the last cycle reads a harmless in-range word.
+  template <int R, bool SQ>
+  __device__ __forceinline__ void row_pf(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* arow,
+                                         uint32_t& cur, uint32_t next_off) const {
+    const uint32_t ai = cur;
+    cur = (R + 1 < L) ? arow[R + 1] : arow[next_off];
+    row<R, SQ>(acc, b, n, ai);
+  }
+
   template <bool SQ, int... Rs>
   __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* arow,
-                                        std::integer_sequence<int, Rs...>) const {
-    (row<Rs, SQ>(acc, b, n, arow[Rs]), ...);
+                                        uint32_t& cur, uint32_t next_off, std::integer_sequence<int, Rs...>) const {
+    (row_pf<Rs, SQ>(acc, b, n, arow, cur, next_off), ...);
   }
 
   // out = a * b / R  (almost Montgomery, < 2N), b = this lane's L digits (regs),
@@ -238,12 +251,13 @@ struct Mont29 {
     uint64_t acc[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) acc[j] = 0;
+    uint32_t cur = a_lds[0];
 #pragma unroll 1
     for (int cyc = 0; cyc < G; ++cyc) {
       // values unchanged; only the optimiser's view of them is reset (see opaque)
       opaque<L>(b);
       opaque<L>(n);
-      cycle<SQ>(acc, b, n, a_lds + cyc * L, std::make_integer_sequence<int, L>{});
+      cycle<SQ>(acc, b, n, a_lds + cyc * L, cur, cyc + 1 < G ? (uint32_t)L : 0u, std::make_integer_sequence<int, L>{});
     }
     // rotation is back to identity; two more carry steps give digits <= 2^29+127
     norm_step<0>(acc);

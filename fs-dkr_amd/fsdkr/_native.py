@@ -96,6 +96,8 @@ def lib():
     L.fsdkr_collect_run.restype = ctypes.c_int
     L.fsdkr_collect_launch.argtypes = [vp]
     L.fsdkr_collect_launch.restype = ctypes.c_int
+    L.fsdkr_collect_prestart.argtypes = [vp, ctypes.POINTER(CollectBatchC)]
+    L.fsdkr_collect_prestart.restype = ctypes.c_int
     L.fsdkr_collect_finish.argtypes = [vp, ctypes.POINTER(VerdictsC)]
     L.fsdkr_collect_finish.restype = ctypes.c_int
     L.fsdkr_collect_prepare_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
@@ -271,6 +273,11 @@ class Context:
         v = Verdicts(batch.R, batch.J, batch.n)
         self.check(self._lib.fsdkr_collect_run(self._h, ctypes.byref(v.c)))
         return v
+
+    def collect_prestart(self, batch):
+        """Start the s^N mod N^2 chains of a batch whose GA fields are packed
+        (CollectBatch(..., staged=True)); the next prepare of it reuses them."""
+        self.check(self._lib.fsdkr_collect_prestart(self._h, ctypes.byref(batch.c)))
 
     def collect_launch(self):
         """Enqueue the kernel pipeline of the prepared batch (returns at once)."""

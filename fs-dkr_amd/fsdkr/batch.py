@@ -106,7 +106,8 @@ class _Gather:
         return arr
 
     def run(self):
-        _convert(self.jobs, host_threads())
+        jobs, self.jobs = self.jobs, []
+        _convert(jobs, host_threads())
 
 
 def _ptr(a):
@@ -140,9 +141,11 @@ class CollectBatch:
     reads is packed (counts, party indices, lengths, ek.n)."""
 
     def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048, n_recv=None,
-                 header_only=False):
+                 header_only=False, staged=False):
         """n_recv: receivers (default R + J); a multi-GPU shard passes its slice of the
-        messages together with the full receiver count."""
+        messages together with the full receiver count.  staged: pack only the
+        fields fsdkr_collect_prestart reads (recv_n, pdl s2, range-proof s; see
+        ga_ready) and leave the rest to complete()."""
         msgs, joins = list(refresh_messages), list(join_messages)
         R, J = len(msgs), len(joins)
         n = n_recv if n_recv else R + J
@@ -171,6 +174,7 @@ class CollectBatch:
         sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
         f_ckn = G.field([m.ek.n for m in all_m] or [0])
         ck_bits = max(1, f_ckn[1])
+        ck_short, f_sig = False, None
         if not self.header_only:
             ck_short = any(len(x) < M2 for x in sig)
             f_sig = G.field([s for row in sig for s in row + [0] * (M2 - len(row))])
@@ -178,6 +182,7 @@ class CollectBatch:
         ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
         if ckl is None:
             raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
+        self._ga, self._pending = None, None
         if self.header_only:
             c.nl = 64 if ck_bits <= 2048 else 96
             c.ckl = max(ckl, c.nl)
@@ -196,17 +201,44 @@ class CollectBatch:
         else:
             rng = [m.range_proofs[i] for m in msgs for i in range(n)]
         # receivers (placeholders past the keys the LocalKey holds: odd modulus 3)
-        rst = list(sts[:avail]) + [None] * (n - avail)
-        F = {
-            "recv_n": G.field([x.n for x in keys[:avail]] + [3] * (n - avail)),
-            "recv_ntilde": G.field([s.N if s else 3 for s in rst]),
-            "recv_h1": G.field([s.g if s else 1 for s in rst]),
-            "recv_h2": G.field([s.ni if s else 1 for s in rst]),
-            "enc": G.field([m.points_encrypted_vec[i] for m in msgs for i in range(n)]),
-        }
-        for a in ("z", "u2", "u3", "s1", "s2", "s3"):
+        F = {"recv_n": G.field([x.n for x in keys[:avail]] + [3] * (n - avail)),
+             "pdl_s2": G.field(pdl, "s2"), "rp_s": G.field(rng, "s")}
+        # stage 1: the fields fsdkr_collect_prestart reads (GA's bases and moduli), at
+        # the width they need; stage 2 (complete) keeps them if the batch width agrees
+        ga_bits = max(1, F["recv_n"][1], F["pdl_s2"][1], F["rp_s"][1])
+        nl_ga = 64 if ga_bits <= 2048 else 96 if ga_bits <= 3072 else None
+        self._ga = None
+        if staged and nl_ga is not None:
+            Gs = _Gather()
+            ga = {name: Gs.slot(F[name], nl_ga) for name in ("recv_n", "pdl_s2", "rp_s")}
+            Gs.run()
+            for name, arr in ga.items():
+                setattr(c, name, k(arr))
+            c.nl = nl_ga
+            self._ga = (nl_ga, ga)
+        self._pending = dict(msgs=msgs, joins=joins, all_m=all_m, n=n, M=M, G=G, F=F, ckl=ckl, f_ckn=f_ckn,
+                             f_sig=f_sig, ck_short=ck_short, sig=sig, pdl=pdl, rng=rng, rst=list(sts[:avail]) +
+                             [None] * (n - avail), t=local_key.t)
+        if not staged:
+            self.complete()
+
+    def complete(self):
+        """Stage 2 of a staged batch (CollectBatch(..., staged=True)): every other field."""
+        st = getattr(self, "_pending", None)
+        if st is None:
+            return self
+        self._pending = None
+        c, k = self.c, self._k
+        msgs, joins, all_m, n, M, G, F = (st[x] for x in ("msgs", "joins", "all_m", "n", "M", "G", "F"))
+        J = len(joins)
+        pdl, rng, rst = st["pdl"], st["rng"], st["rst"]
+        F.update({"recv_ntilde": G.field([s.N if s else 3 for s in rst]),
+                  "recv_h1": G.field([s.g if s else 1 for s in rst]),
+                  "recv_h2": G.field([s.ni if s else 1 for s in rst]),
+                  "enc": G.field([m.points_encrypted_vec[i] for m in msgs for i in range(n)])})
+        for a in ("z", "u2", "u3", "s1", "s3"):
             F["pdl_" + a] = G.field(pdl, a)
-        for a in ("z", "e", "s", "s1", "s2"):
+        for a in ("z", "e", "s1", "s2"):
             F["rp_" + a] = G.field(rng, a)
         for a in ("S", "T", "N"):
             F["ped_" + a] = G.field([m.ring_pedersen_statement for m in all_m], a)
@@ -233,7 +265,7 @@ class CollectBatch:
         if nl is None:
             raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
         c.nl = nl
-        c.ckl = max(ckl, nl)
+        c.ckl = max(st["ckl"], nl)
         c.s1l = _limbs_for(bits("pdl_s1", "rp_s1"))
         c.s3l = _limbs_for(bits("pdl_s3", "rp_s2"))
         c.el = _limbs_for(bits("rp_e"))
@@ -241,21 +273,29 @@ class CollectBatch:
         c.yl = _limbs_for(bits("dlog_y1", "dlog_y2"))
         width = {"enc": 2 * nl, "pdl_u2": 2 * nl, "pdl_s1": c.s1l, "rp_s1": c.s1l, "pdl_s3": c.s3l, "rp_s2": c.s3l,
                  "rp_e": c.el, "ped_Z": c.zl, "dlog_y1": c.yl, "dlog_y2": c.yl}
+        staged = self._ga is not None and self._ga[0] == nl   # stage-1 arrays already at this width
         for name, f in F.items():
-            setattr(c, name, k(G.slot(f, width.get(name, nl))))
-        c.ck_n = k(G.slot(f_ckn, c.ckl))
-        if ck_short:
-            c.ck_lens = k(np.array([len(x) for x in sig], dtype=np.uint32))
-        c.ck_sigma = k(G.slot(f_sig, c.ckl))
+            if not (staged and name in self._ga[1]):
+                setattr(c, name, k(G.slot(f, width.get(name, nl))))
+        c.ck_n = k(G.slot(st["f_ckn"], c.ckl))
+        if st["ck_short"]:
+            c.ck_lens = k(np.array([len(x) for x in st["sig"]], dtype=np.uint32))
+        c.ck_sigma = k(G.slot(st["f_sig"], c.ckl))
         G.run()
         c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
         c.pdl_u1 = k(pack_points(pdl, "u1"))
-        t = local_key.t
+        t = st["t"]
         com = [list(m.coefficients_committed_vec.commitments) for m in msgs]
         if any(len(x) != t + 1 for x in com):   # Horner over each message's own vector
             c.vss_len = k(np.array([len(x) for x in com], dtype=np.uint32))
         c.vss = k(pack_points([p for x in com for p in x] or [None]))
         self.nl = nl
+        return self
+
+    @property
+    def ga_ready(self):
+        """Stage 1 packed the prestart fields (fsdkr_collect_prestart may run)."""
+        return self._ga is not None
 
     def _k(self, arr):
         arr = np.ascontiguousarray(arr, dtype=np.uint32)

@@ -143,7 +143,12 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     """RefreshMessage::collect (refresh_message.rs:321-467)."""
     ctx = _ctx(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
-    batch = CollectBatch(msgs, local_key, joins, m_security, key_bits)
+    # stage 1 packs what the pipeline's longest job reads and starts it on the GPU;
+    # the rest of the batch is packed while those chains run
+    batch = CollectBatch(msgs, local_key, joins, m_security, key_bits, staged=True)
+    if batch.ga_ready:
+        ctx.collect_prestart(batch)
+    batch.complete()
     spec = None
     if batch.header_only:
         verdicts = None

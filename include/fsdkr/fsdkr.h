@@ -188,6 +188,17 @@ int fsdkr_collect_run(fsdkr_ctx* ctx, fsdkr_verdicts* out);
 int fsdkr_collect_launch(fsdkr_ctx* ctx);
 int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
 
+/* Optional head start: launches the pipeline's longest job -- s2^N and s^N mod
+ * N^2 of every (message, receiver) pair (zk_pdl_with_slack.rs:129-135,
+ * range_proofs.rs:148), 2 R n chains of 2048-bit exponents at 4096 bits -- from
+ * the only fields it reads (n_refresh, n_join, n_recv, nl, recv_n, pdl_s2,
+ * rp_s), so it runs while the caller packs the rest of the batch.  The next
+ * fsdkr_collect_prepare of a single batch with equal values of those fields
+ * reuses the results (anything else recomputes them).  Fails with FSDKR_E_ARG
+ * while a launched batch is not finished.  Does not validate: a batch it cannot
+ * start is left to prepare. */
+int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
+
 /* ---- Many independent collect() calls in ONE device pass -------------------
  * `count` sessions (e.g. BASELINE configs[4]: 1024 custody wallets, t=1 n=3,
  * 3072-bit keys), each the batch its own RefreshMessage::collect

@@ -5,6 +5,7 @@ For every scenario both sides run on the same seeded messages; the outcome
 (Ok, or the FsDkrError variant + payload), the side effects on
 paillier_key_vec and, on success, the whole updated LocalKey must be equal."""
 import copy
+import dataclasses
 
 import pytest
 
@@ -211,3 +212,40 @@ def test_paillier_encrypt_job1(gpu_ctx):
     got = gpu_ctx.paillier_encrypt(ms, rs, [k.n for k in keys], idx, 64)
     want = [paillier.encrypt_with_chosen_randomness(keys[i], m, r) for m, r, i in zip(ms, rs, idx)]
     assert got == want
+
+
+def test_prestart_hit_and_miss(gpu_ctx):
+    """fsdkr_collect_prestart: a prepare of the batch it was started for reuses
+    the s^N mod N^2 rows (every proof verifies); a prepare of a DIFFERENT batch
+    (one PDL s2 changed after the prestart) recomputes them, so the changed pair
+    fails u2 and nothing else does; a prestart while a batch is in flight is
+    refused."""
+    from fsdkr.batch import CollectBatch
+    keys, msgs, dks, _ = _dkr(1, 3, "prestart")
+    lk = keys[0]
+    st = CollectBatch(msgs, lk, [], 256, KB, staged=True)
+    assert st.ga_ready
+    gpu_ctx.collect_prestart(st)
+    st.complete()
+    gpu_ctx.collect_prepare(st)
+    v = gpu_ctx.collect_run(st)
+    assert (v.pdl & 7 == 7).all() and (v.range & 1).all()
+    # prestart for the original, prepare a tampered copy: must not reuse the rows
+    gpu_ctx.collect_prestart(CollectBatch(msgs, lk, [], 256, KB, staged=True))
+    bad = copy.deepcopy(msgs)
+    p = bad[1].pdl_proof_vec[2]
+    bad[1].pdl_proof_vec[2] = dataclasses.replace(p, s2=p.s2 + 1)
+    b2 = CollectBatch(bad, lk, [], 256, KB)
+    gpu_ctx.collect_prepare(b2)
+    v2 = gpu_ctx.collect_run(b2)
+    want = [7] * 9
+    want[1 * 3 + 2] = 7 & ~2   # u2 of pair (message 1, receiver 2)
+    assert [int(x) & 7 for x in v2.pdl] == want
+    assert (v2.range & 1).all()
+    # in flight: refused
+    b3 = CollectBatch(msgs, lk, [], 256, KB, staged=True)
+    gpu_ctx.collect_prepare(CollectBatch(msgs, lk, [], 256, KB))
+    gpu_ctx.collect_launch()
+    with pytest.raises(RuntimeError):
+        gpu_ctx.collect_prestart(b3)
+    gpu_ctx.collect_finish(b3.complete())

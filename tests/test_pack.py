@@ -80,3 +80,76 @@ def test_points():
         pack_points([(1 << 256, 1)])
     with pytest.raises(UnsupportedInput):
         pack_points([(1, -1)])
+
+
+def _fake_collect(n=6, t=2, M=8, J=2, seed=3, big_ped=False):
+    rnd = random.Random(seed)
+
+    def r(b):
+        return rnd.getrandbits(b) | 1
+
+    def pt():
+        return (rnd.getrandbits(255), rnd.getrandbits(255))
+
+    def stmt():
+        return NS(N=r(2048), g=r(2040), ni=r(2040))
+    lk = NS(t=t, paillier_key_vec=[NS(n=r(2048)) for _ in range(n)], h1_h2_n_tilde_vec=[stmt() for _ in range(n)])
+
+    def msg(i):
+        return NS(party_index=i + 1,
+                  pdl_proof_vec=[NS(z=r(2040), u1=pt(), u2=r(4090), u3=r(2040), s1=r(1024), s2=r(2040), s3=r(2300))
+                                 for _ in range(n)],
+                  points_committed_vec=[pt() for _ in range(n)], points_encrypted_vec=[r(4090) for _ in range(n)],
+                  range_proofs=[NS(z=r(2040), e=r(256), s=r(2040), s1=r(1024), s2=r(2300)) for _ in range(n)],
+                  coefficients_committed_vec=NS(commitments=[pt() for _ in range(t + 1)]),
+                  ring_pedersen_statement=NS(N=r(3000 if big_ped and i == 1 else 2048), S=r(2040), T=r(2040)),
+                  ring_pedersen_proof=NS(A=[r(2040) for _ in range(M)], Z=[r(2300) for _ in range(M)]),
+                  ek=NS(n=r(2048)), dk_correctness_proof=NS(sigma_vec=[r(2040) for _ in range(11)]))
+    msgs = [msg(i) for i in range(n - J)]
+    joins = []
+    for i in range(J):
+        m = msg(n - J + i)
+        m.dlog_statement = stmt()
+        m.composite_dlog_proof_base_h1 = NS(x=r(2040), y=r(2300))
+        m.composite_dlog_proof_base_h2 = NS(x=r(2040), y=r(2300))
+        joins.append(m)
+    return msgs, joins, lk
+
+
+def _dump(b, M):
+    """Every array of the C batch struct, by the shapes the C ABI documents."""
+    c = b.c
+    R, J, n = b.R, b.J, b.n
+    P, Mt = R * n, R + J
+    V = sum(len(m.coefficients_committed_vec.commitments) for m in b._msgs)
+    rows = {"recv_n": (n, c.nl), "recv_ntilde": (n, c.nl), "recv_h1": (n, c.nl), "recv_h2": (n, c.nl),
+            "enc": (P, 2 * c.nl), "commit": (P, 16), "pdl_z": (P, c.nl), "pdl_u1": (P, 16), "pdl_u2": (P, 2 * c.nl),
+            "pdl_u3": (P, c.nl), "pdl_s1": (P, c.s1l), "pdl_s2": (P, c.nl), "pdl_s3": (P, c.s3l), "rp_z": (P, c.nl),
+            "rp_e": (P, c.el), "rp_s": (P, c.nl), "rp_s1": (P, c.s1l), "rp_s2": (P, c.s3l), "vss": (V, 16),
+            "ped_S": (Mt, c.nl), "ped_T": (Mt, c.nl), "ped_N": (Mt, c.nl), "ped_A": (Mt * M, c.nl),
+            "ped_Z": (Mt * M, c.zl), "ck_n": (Mt, c.ckl), "ck_sigma": (Mt * 11, c.ckl), "dlog_N": (J, c.nl),
+            "dlog_g": (J, c.nl), "dlog_ni": (J, c.nl), "dlog_x1": (J, c.nl), "dlog_x2": (J, c.nl),
+            "dlog_y1": (J, c.yl), "dlog_y2": (J, c.yl)}
+    out = {"widths": (c.nl, c.ckl, c.s1l, c.s3l, c.el, c.zl, c.yl)}
+    for name, (r_, w) in rows.items():
+        out[name] = np.ctypeslib.as_array(getattr(c, name), shape=(r_ * w,)).copy()
+    return out
+
+
+@pytest.mark.parametrize("big_ped", [False, True])
+def test_staged_batch_equals_one_shot(big_ped):
+    """CollectBatch(staged=True) + complete() packs exactly what the one-shot
+    constructor packs, also when stage 1's width is superseded (a 3000-bit
+    ring-Pedersen modulus moves the batch to 3072-bit slots)."""
+    from fsdkr.batch import CollectBatch
+    M = 8
+    msgs, joins, lk = _fake_collect(M=M, big_ped=big_ped)
+    one = CollectBatch(msgs, lk, joins, M, 2048)
+    st = CollectBatch(msgs, lk, joins, M, 2048, staged=True)
+    assert st.ga_ready and st.c.nl == 64
+    st.complete()
+    one._msgs = st._msgs = msgs
+    a, b = _dump(one, M), _dump(st, M)
+    assert a["widths"] == b["widths"] and a["widths"][0] == (96 if big_ped else 64)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
