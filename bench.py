@@ -25,7 +25,8 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
-# collect() runs up to twelve concurrent streams (csrc/collect.cpp stream plan); with
+# collect() runs about twelve concurrent streams (csrc/collect.cpp stream plan; 12
+# hardware queues measured 2-5 % faster than 16, profiles/r02p_hwq.txt); with
 # HIP's default of 4 hardware queues per process (exported as 4 on the GPU
 # boxes) several of them would share queues and serialise.  Raise it (never
 # lower it) before the HIP runtime initialises.

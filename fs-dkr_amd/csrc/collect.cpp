@@ -1169,7 +1169,7 @@ static int collect_launch_impl(Ctx* c) {
   if (ga_group == kWideGroup && pl.jcount[0] &&
       (rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup)))
     return rc;
-  // ---- stream plan (up to twelve concurrent lanes of work: give HIP >= 12 hardware
+  // ---- stream plan (up to thirteen concurrent lanes of work: give HIP >= 12 hardware
   //      queues, GPU_MAX_HW_QUEUES, or streams share queues and serialise):
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
   //   side 8  : FB table chains (h1, h2, T: the longest dependent chain), top priority
@@ -1261,10 +1261,19 @@ static int collect_launch_impl(Ctx* c) {
     c->mark("ec", false, ss);
     if (rc || (rc = join_later(ss))) return rc;
   }
-  {  // GD: DLog g^y / ni^e; GC: correct-key sigma^n (2048-bit exponents, few instances)
+  {  // GD: DLog g^y / ni^e (few long chains); GC: correct-key sigma^n (2048-bit
+     // exponents, Mt*11 instances) on a stream of its own, so the two latency-bound
+     // jobs run side by side (FSDKR_GC_STREAM=0: GC queued behind GD)
     hipStream_t ss = c->side_stream(4);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    if ((rc = launch_group(1, ss, prio[2], 0, cons_nl)) || (rc = launch_group(4, ss, prio[2], 0, cons_ck))) return rc;
+    if ((rc = launch_group(1, ss, prio[2], 0, cons_nl))) return rc;
+    const char* gce = getenv("FSDKR_GC_STREAM");
+    if (!(gce && gce[0] == '0')) {
+      if ((rc = join_later(ss))) return rc;
+      ss = c->side_stream(9);
+      (void)hipStreamWaitEvent(ss, consts_ready, 0);
+    }
+    if ((rc = launch_group(4, ss, prio[2], 0, cons_ck))) return rc;
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqck), PI(pl.d_eqckm), cons_ck, PX(pl.x_pbits), DI(pl.o_one),
                   PX(pl.x_eqck), pl.n_eq_ck};
     c->mark("eq_check", true, ss);

@@ -13,7 +13,9 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
-os.environ["GPU_MAX_HW_QUEUES"] = str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+# FSDKR_HWQ=<q> sets the hardware queue count exactly (A/B across processes)
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("FSDKR_HWQ") or \
+    str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
 
 def main():
