@@ -128,8 +128,8 @@ typedef struct fsdkr_collect_batch {
   const uint32_t* ped_A;    /* [R+J][M][nl] */
   const uint32_t* ped_Z;    /* [R+J][M][zl] */
   /* NiCorrectKeyProof: ek.n and sigma_vec of the R then J messages */
-  const uint32_t* ck_n;     /* [R+J][nl]     */
-  const uint32_t* ck_sigma; /* [R+J][11][nl] */
+  const uint32_t* ck_n;     /* [R+J][ckl]     (ckl below; 0 = nl) */
+  const uint32_t* ck_sigma; /* [R+J][11][ckl] */
   /* join messages: dlog_statement {N, g, ni} and the two CompositeDLogProofs */
   const uint32_t *dlog_N, *dlog_g, *dlog_ni, *dlog_x1, *dlog_x2;      /* [J][nl]  */
   const uint32_t *dlog_y1, *dlog_y2;                                  /* [J][yl]  */

@@ -19,14 +19,18 @@ Fixtures (gzip JSON, codec.py):
                                     JoinMessage::collect() of the joiner, join-path tampers
   job1_kb2048.json.gz               Paillier encryption with chosen randomness (job 1)
   modexp_kat.json.gz                base^exp mod m at 2048/3072/4096/6144-bit moduli
+  sampled_pairs_t8_n16_kb2048.json.gz  BASELINE configs[1] shape: 16 sampled (k, i) PDL + Alice
+                                    pairs of an n=16 refresh and 8 tampered copies, with the
+                                    oracle's per-pair verdicts (python make_golden.py sampled)
 """
 import copy
 import os
 import sys
+from types import SimpleNamespace
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
-sys.path[:0] = [REPO, HERE]
+sys.path[:0] = [REPO, HERE, os.path.dirname(HERE)]
 
 import codec  # noqa: E402
 from oracle import bigint, paillier, protocol, range_proofs  # noqa: E402
@@ -202,6 +206,54 @@ def join_fixture(seed, kb):
             "join_tampers": jt}
 
 
+def sampled_fixture():
+    """BASELINE configs[1] shape (t=8, n=16, 2048-bit keys): 16 sampled (k, i) pairs
+    from four senders' RefreshMessages (SURVEY §8c "n=16 sampled pairs"), each with its
+    PDL-with-slack and Alice proofs, plus 8 tampered copies; expected verdicts by the
+    oracle (pdl bits u1|u2<<1|u3<<2, range ok).  Receivers' keys and DLog statements
+    for all 16 parties."""
+    from tamper import oracle_pair
+    t, n, kb = 8, 16, 2048
+    rng = Rng("golden-n16-sampled")
+    keys = protocol.simulate_keygen(t, n, rng, kb)
+    lk = keys[0].clone()
+    senders = [2, 7, 11, 16]
+    rx = {2: [0, 5, 9, 15], 7: [1, 6, 7, 12], 11: [2, 3, 10, 14], 16: [4, 8, 11, 13]}
+    pairs = []
+    for pi in senders:
+        key = keys[pi - 1].clone()
+        m, _ = protocol.distribute(key.i, key, n, rng, kb)
+        for i in rx[pi]:
+            pairs.append({"k": pi, "i": i, "enc": m.points_encrypted_vec[i], "commit": m.points_committed_vec[i],
+                          "pdl": m.pdl_proof_vec[i], "alice": m.range_proofs[i]})
+    tampers = [("pdl", "s1", 1), ("pdl", "u2", 1), ("pdl", "s3", 1), ("pdl", "z", 1),
+               ("alice", "s2", 1), ("alice", "e", 1), ("alice", "s", 1), ("alice", "z", 1)]
+    import dataclasses
+    entries = []
+    for j, pr in enumerate(pairs):
+        entries.append(dict(pr, tamper=None))
+    for j, (which, f, d) in enumerate(tampers):
+        pr = dict(pairs[(5 * j + 3) % len(pairs)])
+        obj = pr[which]
+        pr[which] = dataclasses.replace(obj, **{f: getattr(obj, f) + d})
+        entries.append(dict(pr, tamper=f"{which}.{f}+{d}"))
+    out = []
+    for e in entries:
+        msg = SimpleNamespace(points_encrypted_vec=[e["enc"]] * n, points_committed_vec=[e["commit"]] * n,
+                              pdl_proof_vec=[e["pdl"]] * n, range_proofs=[e["alice"]] * n)
+        bits, ok = oracle_pair(msg, lk, e["i"])
+        assert (e["tamper"] is None) == (bits == 7 and ok), e["tamper"]
+        out.append({"k": e["k"], "i": e["i"], "tamper": e["tamper"], "enc": codec.enc(e["enc"]),
+                    "commit": codec.enc(e["commit"]),
+                    "pdl": codec.enc(e["pdl"]), "alice": codec.enc(e["alice"]), "expect_pdl_bits": bits,
+                    "expect_range_ok": ok})
+    return {"meta": {"t": t, "n": n, "key_bits": kb, "M": 256, "seed": "golden-n16-sampled",
+                     "senders": senders, "generator": "tests/golden/make_golden.py (oracle restatement, seeded)"},
+            "receivers": {"ek_n": codec.enc([e.n for e in lk.paillier_key_vec]),
+                          "dlog": codec.enc([[s.N, s.g, s.ni] for s in lk.h1_h2_n_tilde_vec])},
+            "pairs": out}
+
+
 def job1_fixture():
     rng = Rng("golden-job1")
     eks = [paillier.keypair_with_modulus_size(2048, rng)[0] for _ in range(3)]
@@ -227,11 +279,15 @@ def modexp_fixture():
 
 
 def main():
+    if sys.argv[1:] == ["sampled"]:    # only the n=16 sampled-pairs fixture
+        codec.save("sampled_pairs_t8_n16_kb2048.json.gz", sampled_fixture())
+        return
     codec.save("transcript_t2_n5_kb1024.json.gz", refresh_fixture(2, 5, "golden-t2n5", 1024, True))
     codec.save("transcript_t1_n3_kb2048.json.gz", refresh_fixture(1, 3, "golden-t1n3-2048", 2048, False))
     codec.save("transcript_join_t1_n4_kb1024.json.gz", join_fixture("golden-join", 1024))
     codec.save("job1_kb2048.json.gz", job1_fixture())
     codec.save("modexp_kat.json.gz", modexp_fixture())
+    codec.save("sampled_pairs_t8_n16_kb2048.json.gz", sampled_fixture())
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".gz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -122,3 +122,35 @@ def test_job1_and_modexp_kat(gpu_ctx):
         out = gpu_ctx.modexp_batch([r["base"] for r in rs], [r["exp"] for r in rs], [r["mod"] for r in rs],
                                    list(range(len(rs))), limbs)
         assert out == [r["out"] for r in rs], limbs
+
+
+def test_sampled_pairs_n16(gpu_ctx):
+    """BASELINE configs[1] shape (n=16, t=8, 2048-bit keys): the 24 sampled (k, i)
+    PDL + Alice pairs of the fixture (16 valid, 8 tampered) through the collect
+    pipeline.  Each pair rides in its own message slot of a receiver-complete
+    batch (n_recv = 16, the multi-GPU slice form); only the sampled pair's verdicts
+    are read and must equal the frozen oracle verdicts."""
+    from types import SimpleNamespace as NS
+    from fsdkr.batch import CollectBatch
+    raw = codec.load_raw("sampled_pairs_t8_n16_kb2048.json.gz")
+    cls = codec.product_classes()
+    rec = codec.dec(raw["receivers"], cls)
+    n, t, M = raw["meta"]["n"], raw["meta"]["t"], raw["meta"]["M"]
+    lk = NS(t=t, paillier_key_vec=[NS(n=x) for x in rec["ek_n"]],
+            h1_h2_n_tilde_vec=[NS(N=s[0], g=s[1], ni=s[2]) for s in rec["dlog"]])
+    pairs = [codec.dec(p, cls) for p in raw["pairs"]]
+    filler_n = rec["ek_n"][0]
+    for lo in range(0, len(pairs), 12):
+        chunk = pairs[lo:lo + 12]
+        msgs = [NS(party_index=d["k"], pdl_proof_vec=[d["pdl"]] * n, points_committed_vec=[d["commit"]] * n,
+                   points_encrypted_vec=[d["enc"]] * n, range_proofs=[d["alice"]] * n,
+                   coefficients_committed_vec=NS(commitments=[d["commit"]] * (t + 1)),
+                   ring_pedersen_statement=NS(N=filler_n, S=2, T=3), ring_pedersen_proof=NS(A=[1] * M, Z=[1] * M),
+                   ek=NS(n=filler_n), dk_correctness_proof=NS(sigma_vec=[1] * 11)) for d in chunk]
+        b = CollectBatch(msgs, lk, [], M, raw["meta"]["key_bits"], n_recv=n)
+        gpu_ctx.collect_prepare(b)
+        v = gpu_ctx.collect_run(b)
+        for r, d in enumerate(chunk):
+            p = r * n + d["i"]
+            assert (int(v.pdl[p]) & 7, bool(v.range[p] & 1)) == (d["expect_pdl_bits"], d["expect_range_ok"]), \
+                d["tamper"]

@@ -102,3 +102,23 @@ def test_every_collect_error_variant_is_covered():
                     "RingPedersenProofError", "RangeProof", "ModuliTooSmall", "PaillierVerificationError",
                     "NewPartyUnassignedIndexError", "BroadcastedPublicKeyError", "DLogProofValidation",
                     "RingPedersenProofValidation"}
+
+
+def test_sampled_pairs_n16():
+    """BASELINE configs[1] shape (n=16, t=8, 2048-bit): the oracle reproduces the
+    per-pair verdicts frozen in the sampled-pairs fixture (16 valid, 8 tampered)."""
+    from types import SimpleNamespace
+    from tamper import oracle_pair
+    from oracle.zk_paillier import DLogStatement
+    raw = codec.load_raw("sampled_pairs_t8_n16_kb2048.json.gz")
+    cls = codec.oracle_classes()
+    rec = codec.dec(raw["receivers"], cls)
+    lk = SimpleNamespace(paillier_key_vec=[paillier.EncryptionKey.from_n(x) for x in rec["ek_n"]],
+                         h1_h2_n_tilde_vec=[DLogStatement(*s) for s in rec["dlog"]])
+    n = raw["meta"]["n"]
+    assert len(raw["pairs"]) == 24 and sum(p["tamper"] is None for p in raw["pairs"]) == 16
+    for p in raw["pairs"]:
+        d = codec.dec(p, cls)
+        m = SimpleNamespace(points_encrypted_vec=[d["enc"]] * n, points_committed_vec=[d["commit"]] * n,
+                            pdl_proof_vec=[d["pdl"]] * n, range_proofs=[d["alice"]] * n)
+        assert oracle_pair(m, lk, d["i"]) == (d["expect_pdl_bits"], d["expect_range_ok"]), p["tamper"]
