@@ -263,7 +263,7 @@ int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, ui
   // the staging buffer is reused by the next call: make this copy complete first
   rc = c->hip_check(hipStreamSynchronize(c->stream), "sync desc");
   if (rc) return rc;
-  return launch_modexp_desc(c, job.k32, count, job.exp_bits, d_desc, d_consts, d_out, nullptr, "mxtable", 0,
+  return launch_modexp_desc(c, job.k32, count, job.exp_bits, d_desc, d_consts, d_out, nullptr, "mxtable", c->prio,
                             group);
 }
 

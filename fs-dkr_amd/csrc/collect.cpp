@@ -212,6 +212,9 @@ struct CollectPlan {
   // operands read them from the prestart buffer once ga_done has fired
   bool ga_hit = false;
   hipEvent_t ga_done = nullptr;
+  // h1 / h2 fixed-base tables built by fsdkr_collect_prestart (fb_hit)
+  bool fb_hit = false;
+  FbPre fb_pre;
   FbJob fb;
   size_t d_FB = 0;
   uint32_t* fb_table = nullptr;
@@ -235,19 +238,168 @@ struct GaPre {
   std::vector<uint32_t> recv_n, s2, s;   // the inputs, for the match in prepare
   uint32_t* out = nullptr;               // [2P][nn]: J1 instance order (s2^N rows, then s^N rows)
   hipEvent_t done = nullptr;
+  // the fixed-base tables of h1_i, h2_i (bases 2i, 2i+1 of prepare's FbJob), built
+  // for exponents of up to bits_h1 / bits_h2 bits with window w
+  bool fb_valid = false;
+  std::vector<uint32_t> ntilde, h1, h2, T, pedmod;   // bases, and the T_m moduli rows
+  uint32_t Mt = 0, fb_w = 0, bits_h1 = 0, bits_h2 = 0, bits_z = 0, fb_entries = 0;
+  uint32_t* fb_table = nullptr;
+  hipEvent_t fb_done = nullptr;     // every table (group B: the h2 chains)
+  hipEvent_t fb_done_a = nullptr;   // group A: h1 and T chains
 };
 
 void free_ga_pre(Ctx* c) {
   GaPre* g = reinterpret_cast<GaPre*>(c->ga_pre);
   if (g && g->done) (void)hipEventDestroy(g->done);
+  if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
+  if (g && g->fb_done_a) (void)hipEventDestroy(g->fb_done_a);
   delete g;
   c->ga_pre = nullptr;
+}
+
+// collect()'s fixed-base tables, base order [h1_i | T_m | h2_i] (FbJob::finalize
+// sizes: one entry per w exponent bits, at least one)
+struct FbLayout {
+  std::vector<uint32_t> h, toff, mod;
+  uint32_t entries = 0;
+};
+static FbLayout fb_layout(uint32_t n, uint32_t Mt, uint32_t w, uint32_t bits_h1, uint32_t bits_h2, uint32_t bits_z) {
+  FbLayout L;
+  auto add = [&](uint32_t bits, uint32_t mod) {
+    const uint32_t h = std::max(1u, (bits + w - 1) / w);
+    L.h.push_back(h);
+    L.toff.push_back(L.entries);
+    L.mod.push_back(mod);
+    L.entries += h;
+  };
+  for (uint32_t r = 0; r < n; ++r) add(bits_h1, r);
+  for (uint32_t m = 0; m < Mt; ++m) add(bits_z, n + m);
+  for (uint32_t r = 0; r < n; ++r) add(bits_h2, r);
+  return L;
+}
+
+// Modulus row of message m's ring-Pedersen T^Z checks, as prepare's pre-pass
+// derives it: the odd part of N, or the placeholder 3 when the proof panics
+// before any check (A shorter than M, N = 0) or the odd part is 1.
+static void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, uint32_t nl, uint32_t* on) {
+  const uint32_t* N = b->ped_N + (size_t)m * b->nl;
+  std::fill(on, on + nl, 0u);
+  const bool panics = (b->ped_lens && b->ped_lens[2 * m] < M) || hbn::is_zero_raw(N, b->nl);
+  if (!panics) {
+    memcpy(on, N, (size_t)b->nl * 4);
+    const uint32_t tz = hbn::ctz_raw(N, b->nl);
+    if (tz) hbn::shr_raw(on, nl, tz);
+    if (!(on[0] == 1 && hbn::is_zero_raw(on + 1, nl - 1))) return;
+  }
+  std::fill(on, on + nl, 0u);
+  on[0] = 3;
+}
+
+// The fixed-base table chains of collect()'s FbJob, in its base order: h1_i, h2_i
+// of every receiver's DLogStatement (h2: one squaring per exponent bit of s3,
+// ~2816 at 2048-bit keys), then every message's ring-Pedersen T, sized by the
+// bit lengths of the exponents they serve (PDL / Alice s1, s3|s2; RP Z), on the
+// table chain's stream.
+static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, uint32_t n, uint32_t P) {
+  if (!b->recv_ntilde || !b->recv_h1 || !b->recv_h2 || !b->pdl_s1 || !b->pdl_s3 || !b->rp_s1 || !b->rp_s2 ||
+      !b->s1l || !b->s3l || !b->ped_T || !b->ped_N || !b->ped_Z || !b->zl || !b->m_security)
+    return FSDKR_OK;   // stage 1 did not pack them: prepare builds every table
+  const char* pfe = getenv("FSDKR_PRE_FB");   // 0: no table prestart (tuning)
+  if (pfe && pfe[0] == '0') return FSDKR_OK;
+  const uint32_t nl = b->nl, Mt = b->n_refresh + b->n_join, M = b->m_security;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!is_odd(b->recv_ntilde + (size_t)i * nl)) return FSDKR_OK;
+  uint32_t bh1 = 1, bh2 = 1, bz = 1;
+  for (size_t p = 0; p < P; ++p) {
+    bh1 = std::max(bh1, std::max(hbn::bitlen(b->pdl_s1 + p * b->s1l, b->s1l), hbn::bitlen(b->rp_s1 + p * b->s1l, b->s1l)));
+    bh2 = std::max(bh2, std::max(hbn::bitlen(b->pdl_s3 + p * b->s3l, b->s3l), hbn::bitlen(b->rp_s2 + p * b->s3l, b->s3l)));
+  }
+  for (size_t k = 0; k < (size_t)Mt * M; ++k) bz = std::max(bz, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
+  const uint32_t w = fb_window(std::max(std::max(bh1, bh2), bz));
+  const FbLayout L = fb_layout(n, Mt, w, bh1, bh2, bz);
+  const uint32_t nb = 2 * n + Mt, entries = L.entries, nmod = n + Mt;
+  const int KD = shape_digits(nl);
+  auto al = Img::al;
+  const size_t o_mod = 0, o_h1 = al((size_t)nmod * nl * 4), o_h2 = o_h1 + al((size_t)n * nl * 4),
+               o_T = o_h2 + al((size_t)n * nl * 4), o_bp = o_T + al((size_t)Mt * nl * 4),
+               o_bl = o_bp + al((size_t)nb * 8), o_bm = o_bl + al((size_t)nb * 4), o_bt = o_bm + al((size_t)nb * 4),
+               o_bh = o_bt + al((size_t)nb * 4), o_tab = o_bh + al((size_t)nb * 4);
+  const size_t total = o_tab + (size_t)entries * KD * 4;
+  uint8_t* dev = (uint8_t*)c->buf("collect_fb_pre", total);
+  if (!dev) {
+    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
+    return FSDKR_E_OOM;
+  }
+  std::vector<uint8_t> img(o_tab, 0);
+  uint32_t* mods = reinterpret_cast<uint32_t*>(img.data() + o_mod);   // [Ntilde_i | RP modulus_m]
+  memcpy(mods, b->recv_ntilde, (size_t)n * nl * 4);
+  for (uint32_t m = 0; m < Mt; ++m) ped_modulus(b, m, M, nl, mods + (size_t)(n + m) * nl);
+  memcpy(img.data() + o_h1, b->recv_h1, (size_t)n * nl * 4);
+  memcpy(img.data() + o_h2, b->recv_h2, (size_t)n * nl * 4);
+  memcpy(img.data() + o_T, b->ped_T, (size_t)Mt * nl * 4);
+  auto* bp = reinterpret_cast<uint64_t*>(img.data() + o_bp);
+  for (uint32_t r = 0; r < n; ++r) {   // prepare's base order [h1_i | T_m | h2_i]
+    bp[r] = (uint64_t)(uintptr_t)(dev + o_h1 + (size_t)r * nl * 4);
+    bp[n + Mt + r] = (uint64_t)(uintptr_t)(dev + o_h2 + (size_t)r * nl * 4);
+  }
+  for (uint32_t m = 0; m < Mt; ++m) bp[n + m] = (uint64_t)(uintptr_t)(dev + o_T + (size_t)m * nl * 4);
+  std::vector<uint32_t> blen(nb, nl);
+  memcpy(img.data() + o_bl, blen.data(), (size_t)nb * 4);
+  memcpy(img.data() + o_bm, L.mod.data(), (size_t)nb * 4);
+  memcpy(img.data() + o_bt, L.toff.data(), (size_t)nb * 4);
+  memcpy(img.data() + o_bh, L.h.data(), (size_t)nb * 4);
+  // group A (h1, T: shorter chains) beside group B (h2: the longest chain, top priority)
+  hipStream_t ts = c->crit_stream();
+  if (!ts) ts = c->side_stream(8);   // launch()'s table-chain stream
+  hipStream_t tsA = c->side_stream(1);   // launch()'s fixed-base exponent stream (idle until then)
+  StreamScope scope(c, ts);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, ts), "prestart fb H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(ts), "prestart fb H2D sync")))
+    return rc;
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl")))
+    return rc;
+  if (!g.fb_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done, hipEventDisableTiming), "event")))
+    return rc;
+  if (!g.fb_done_a && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done_a, hipEventDisableTiming), "event")))
+    return rc;
+  (void)hipEventRecord(g.fb_done_a, ts);   // consts ready
+  (void)hipStreamWaitEvent(tsA, g.fb_done_a, 0);
+  g.fb_table = reinterpret_cast<uint32_t*>(dev + o_tab);
+  auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
+  auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
+  const uint32_t nA = n + Mt;
+  FbTableArgs tb{U64(o_bp) + nA, U32(o_bl) + nA, U32(o_bm) + nA, U32(o_bt) + nA, U32(o_bh) + nA, cons, g.fb_table, w,
+                 n, 3};
+  FbTableArgs ta{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nA, 2};
+  if ((rc = c->hip_check(launch_fb_table(nl, tb, ts), "prestart fb_table h2")) ||
+      (rc = c->hip_check(launch_fb_table(nl, ta, tsA), "prestart fb_table h1/T")))
+    return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.fb_done_a, tsA), "event record"))) return rc;
+  // fb_done covers both groups: the B chain's stream waits for A's as well
+  (void)hipStreamWaitEvent(ts, g.fb_done_a, 0);
+  if ((rc = c->hip_check(hipEventRecord(g.fb_done, ts), "event record"))) return rc;
+  g.ntilde.assign(b->recv_ntilde, b->recv_ntilde + (size_t)n * nl);
+  g.h1.assign(b->recv_h1, b->recv_h1 + (size_t)n * nl);
+  g.h2.assign(b->recv_h2, b->recv_h2 + (size_t)n * nl);
+  g.T.assign(b->ped_T, b->ped_T + (size_t)Mt * nl);
+  g.pedmod.assign(mods + (size_t)n * nl, mods + (size_t)nmod * nl);
+  g.Mt = Mt;
+  g.fb_w = w;
+  g.bits_h1 = bh1;
+  g.bits_h2 = bh2;
+  g.bits_z = bz;
+  g.fb_entries = entries;
+  g.fb_valid = true;
+  return FSDKR_OK;
 }
 
 static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
   if (!c->ga_pre) c->ga_pre = new GaPre();
   GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
   g.valid = false;
+  g.fb_valid = false;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
   if (running && running->launched) {
     c->fail("fsdkr_collect_prestart: a batch is in flight (call finish first)");
@@ -308,14 +460,19 @@ static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons, "collect_ga_nn"))) return rc;
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
-  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 3, 8))) return rc;
+  // issue priority 3 (FSDKR_PRE_GA_PRIO; 2 measured 1-2 ms slower per call,
+  // profiles/r02x_ab_full.jsonl)
+  const char* gpe = getenv("FSDKR_PRE_GA_PRIO");
+  const uint32_t ga_prio = gpe ? (uint32_t)atoi(gpe) : 3u;
+  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, 8)))
+    return rc;
   if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
   g.nl = nl;
   g.n = n;
   g.R = R;
   g.valid = true;
-  return FSDKR_OK;
+  return prestart_fb_tables(c, b, g, n, P);
 }
 
 // does the prestarted GA belong to this (single-session) batch?
@@ -799,12 +956,21 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   FbJob& FB = pl.fb;
   FB = FbJob();
   FB.k32 = nl;
-  std::vector<uint32_t> fb_h1(n), fb_h2(n);
-  for (uint32_t r = 0; r < n; ++r) {
-    fb_h1[r] = FB.add_base(DI(o_h1 + (size_t)r * nl * 4), nl, r);
-    fb_h2[r] = FB.add_base(DI(o_h2 + (size_t)r * nl * 4), nl, r);
-  }
-  for (uint32_t m = 0; m < Mt; ++m) FB.add_base(DI(o_pT + (size_t)m * nl * 4), nl, n + m);
+  // base order [h1_i | T_m | h2_i] and instance order [h1 | T | h2]: group A (the
+  // short h1 chains and the T chains) and group B (the long h2 chains) are
+  // contiguous, so group A's exponents run as soon as its tables exist
+  std::vector<uint32_t> fb_h1(n), fb_h2(n), fb_T(Mt);
+  for (uint32_t r = 0; r < n; ++r) fb_h1[r] = FB.add_base(DI(o_h1 + (size_t)r * nl * 4), nl, r);
+  for (uint32_t m = 0; m < Mt; ++m) fb_T[m] = FB.add_base(DI(o_pT + (size_t)m * nl * 4), nl, n + m);
+  for (uint32_t r = 0; r < n; ++r) fb_h2[r] = FB.add_base(DI(o_h2 + (size_t)r * nl * 4), nl, r);
+  struct FbAdd {
+    uint32_t base;
+    uint64_t exp;
+    uint32_t elen, ebits;
+    uint64_t out;
+  };
+  std::vector<FbAdd> fb_later;   // the h2 instances, added after the T instances
+  fb_later.reserve(2 * (size_t)P);
   std::vector<uint32_t> j9_index(P, 0xFFFFFFFFu);
   for (int which = 0; which < 2; ++which)
     for (uint32_t p = 0; p < P; ++p) {
@@ -821,12 +987,13 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
       const size_t slot = (size_t)which * P + p;
       if (which == 0) {
         FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
-        FB.add(fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4));
+        fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
         J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DX(x_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
         FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
-        FB.add(fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2, DX(x_J4 + slot * nl * 4));
+        fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
+                            DX(x_J4 + slot * nl * 4)});
         J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
       }
     }
@@ -838,8 +1005,16 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
     }
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k)  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144)
-      FB.add(2 * n + m, DI(o_pZ + ((size_t)m * M + k) * zl * 4), zl, z_max,
-             DX(x_RP + ((size_t)m * M + k) * nl * 4));
+      FB.add(fb_T[m], DI(o_pZ + ((size_t)m * M + k) * zl * 4), zl, z_max, DX(x_RP + ((size_t)m * M + k) * nl * 4));
+  // FSDKR_FB_SPLIT=1: group A's exponents start before the h2 tables are done.
+  // Measured 1-2 ms slower than one launch at n = 64 (the early group-A exponents
+  // compete with GA / J2 / J5 for the chip; profiles/r02x_ab_full.jsonl): off.
+  const char* fse = getenv("FSDKR_FB_SPLIT");
+  if (fse && fse[0] == '1') {
+    FB.split_bases = n + Mt;
+    FB.split_inst = (uint32_t)FB.count();
+  }
+  for (const FbAdd& a : fb_later) FB.add(a.base, a.exp, a.elen, a.ebits, a.out);
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < CK_M2; ++k)  // correct-key sigma_k^n mod n
       GC.add(DI(o_cks + ((size_t)m * CK_M2 + k) * ckl * 4), ckl, DI(o_ckn + (size_t)m * ckl * 4), ckl,
@@ -876,7 +1051,39 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   GD.append(J8);
   const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD),
                d_GC = pack_job(GC);
+  // the h1_i / h2_i tables of a prestart: sized for the prestart's exponent bounds
+  // (taller tables only add unused entries), used if the layout then agrees
+  const GaPre* gp = reinterpret_cast<const GaPre*>(c->ga_pre);
+  const bool fb_cand = count == 1 && gp && gp->fb_valid && gp->nl == nl && gp->n == n && gp->Mt == Mt &&
+                       memcmp(gp->ntilde.data(), bs->recv_ntilde, (size_t)n * nl * 4) == 0 &&
+                       memcmp(gp->h1.data(), bs->recv_h1, (size_t)n * nl * 4) == 0 &&
+                       memcmp(gp->h2.data(), bs->recv_h2, (size_t)n * nl * 4) == 0 &&
+                       memcmp(gp->T.data(), bs->ped_T, (size_t)Mt * nl * 4) == 0 &&
+                       memcmp(gp->pedmod.data(), PEDN.data(), (size_t)Mt * nl * 4) == 0 &&
+                       std::max(mx.s1, mx.as1) <= gp->bits_h1 && std::max(mx.s3, mx.as2) <= gp->bits_h2 &&
+                       z_max <= gp->bits_z;
+  if (fb_cand) {
+    for (uint32_t r = 0; r < n; ++r) {
+      FB.b_bits[fb_h1[r]] = gp->bits_h1;
+      FB.b_bits[fb_h2[r]] = gp->bits_h2;
+    }
+    for (uint32_t m = 0; m < Mt; ++m) FB.b_bits[fb_T[m]] = gp->bits_z;
+  }
   FB.finalize();
+  if (fb_cand && FB.w == gp->fb_w && FB.bases() == 2 * (size_t)n + Mt) {
+    const FbLayout L = fb_layout(n, Mt, FB.w, gp->bits_h1, gp->bits_h2, gp->bits_z);
+    bool same = L.entries == gp->fb_entries;
+    for (uint32_t k = 0; k < FB.bases() && same; ++k)
+      same = FB.b_h[k] == L.h[k] && FB.b_toff[k] == L.toff[k] && FB.b_mod[k] == L.mod[k];
+    if (same) {
+      pl.fb_hit = true;
+      pl.fb_pre.table = gp->fb_table;
+      pl.fb_pre.entries = gp->fb_entries;
+      pl.fb_pre.ready_a = gp->fb_done_a;
+      pl.fb_pre.ready_b = gp->fb_done;
+      reinterpret_cast<GaPre*>(c->ga_pre)->fb_valid = false;   // consumed
+    }
+  }
   FB.pack(desc);   // FbJob offsets are positions in `desc`, i.e. relative to desc_base
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N
   std::vector<uint64_t> bs_ptr(2 * (size_t)P), bn_ptr(2 * (size_t)P);
@@ -1233,8 +1440,11 @@ static int collect_launch_impl(Ctx* c) {
     FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps};
     hipStream_t ts = c->crit_stream();
     if (!ts) ts = c->side_stream(8);   // own stream: the chain starts beside fb_sched
+    hipStream_t tsA = ss;   // group A's (h1, T) chains, then fb_sched / fb_exp behind them
     (void)hipStreamWaitEvent(ts, consts_ready, 0);
-    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, (ga_first & 1) ? ga_done : nullptr)) ||
+    (void)hipStreamWaitEvent(tsA, consts_ready, 0);
+    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, (ga_first & 1) ? ga_done : nullptr,
+                        pl.fb_hit ? &pl.fb_pre : nullptr, tsA)) ||
         (rc = join_later(ss)))
       return rc;
   }

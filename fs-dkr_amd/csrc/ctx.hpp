@@ -59,6 +59,9 @@ struct Ctx {
   void tend(size_t idx, hipStream_t st);
   size_t last_mark = (size_t)-1;
   uint32_t modexp_group = 0;   // lanes per modexp instance (0 = by batch size)
+  // issue priority (s_setprio) of the generic entry points' kernels: the share
+  // recovery raises it while it overlaps a launched collect pipeline
+  uint32_t prio = 0;
   hipStream_t side_stream(int k);
   // CU reservation for latency-critical serial chains (FSDKR_RESERVE_CUS = R, a
   // multiple of 8): crit_stream() runs on R CUs spread evenly over the 8 XCDs and
@@ -84,6 +87,14 @@ struct StreamScope {
     if (s) c->stream = s;
   }
   ~StreamScope() { c->stream = saved; }
+};
+
+// Raises the context's kernel issue priority for the calls of one entry point.
+struct PrioScope {
+  Ctx* c;
+  uint32_t saved;
+  PrioScope(Ctx* cx, uint32_t p) : c(cx), saved(cx->prio) { c->prio = p; }
+  ~PrioScope() { c->prio = saved; }
 };
 
 // Host worker threads for the collect() pre-pass (FSDKR_HOST_THREADS, else

@@ -43,6 +43,10 @@ struct FbExpArgs {              // out = base^exp mod N from the base's table
   const uint32_t* nsteps;
   uint32_t stride;
   uint32_t count;
+  // entries [0, split) live in table_pre (tables built ahead by
+  // fsdkr_collect_prestart), the rest in `table` from entry `split` on
+  const uint32_t* table_pre;
+  uint32_t split;
 };
 
 uint32_t fb_window(uint32_t ebits);

@@ -146,7 +146,8 @@ __global__ __launch_bounds__(BLOCK) void fb_exp_kernel(const FbExpArgs a) {
 #pragma unroll
   for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
   M.ninv = C[3 * KD];
-  const uint32_t* T = a.table + (size_t)a.toff[inst] * KD;
+  const uint32_t toff = a.toff[inst];
+  const uint32_t* T = (toff < a.split) ? a.table_pre + (size_t)toff * KD : a.table + (size_t)(toff - a.split) * KD;
   const uint16_t* S = a.sched + (size_t)inst * a.stride;
   const uint32_t nst = a.nsteps[inst];
   uint32_t Bd[L], r[L];

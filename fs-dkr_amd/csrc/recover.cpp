@@ -53,6 +53,7 @@ int fsdkr_paillier_decrypt_multi(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, co
       return FSDKR_E_ARG;
     }
   StreamScope scope(cx, cx->aux_stream());   // overlaps a launched collect batch
+  PrioScope prio(cx, 3);                      // few waves on the critical path: win issue arbitration
   // kzen-paillier CRT decryption with g = N + 1.  Its constants have closed forms:
   // (1+N)^(p-1) = 1 + (p-1)N mod p^2 and (p-1)N = -q p mod p^2, so
   // h_p = L_p(g^(p-1) mod p^2)^-1 = (-q)^-1 mod p = p - q^-1 mod p (likewise h_q);
@@ -226,6 +227,7 @@ int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t*
   if (!c || !points || !scalars || !out || terms == 0) return FSDKR_E_ARG;
   if (count == 0) return FSDKR_OK;
   StreamScope scope(c, c->aux_stream());   // overlaps a launched collect batch
+  PrioScope prio(c, 3);
   const size_t np = (size_t)count * terms;
   uint8_t* d = (uint8_t*)c->buf("msm", np * 16 * 4 + np * 8 * 4 + np * 8 + (size_t)count * 16 * 4 + np * 96 + 1024);
   if (!d) return FSDKR_E_OOM;
@@ -241,7 +243,7 @@ int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t*
       (rc = c->hip_check(hipMemcpyAsync(d_sc, scalars, np * 32, hipMemcpyHostToDevice, c->stream), "H2D sc")) ||
       (rc = c->hip_check(hipMemcpyAsync(d_ptr, ptrs.data(), np * 8, hipMemcpyHostToDevice, c->stream), "H2D ptr")))
     return rc;
-  EcMsmArgs a{d_ptr, d_sc, terms, d_out, count, d_scr};
+  EcMsmArgs a{d_ptr, d_sc, terms, d_out, count, d_scr, c->prio};
   c->mark("ec", true);
   rc = c->hip_check(launch_ec_msm(a, c->stream), "ec_msm");
   c->mark("ec", false);

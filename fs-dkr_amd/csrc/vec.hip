@@ -122,6 +122,9 @@ __global__ void ec_msm_term_kernel(const EcMsmArgs a) {
   using namespace ec;
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= a.count * a.terms) return;
+  if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
   uint32_t* J = a.scratch + (size_t)q * 24;
   const uint32_t* pt = P32(a.pt_ptr[q]);
   const uint32_t* sc = a.scalars + (size_t)q * 8;
@@ -146,6 +149,7 @@ __global__ void ec_msm_sum_kernel(const EcMsmArgs a) {
   using namespace ec;
   const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= a.count) return;
+  if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   Jac acc;
   jac_set_inf(acc);
   for (uint32_t j = 0; j < a.terms; ++j) {

@@ -130,6 +130,7 @@ struct EcMsmArgs {          // out[o] = sum_j scalars[o][j] * P[o][j]
   uint32_t* out;            // [count][16] affine
   uint32_t count;
   uint32_t* scratch;        // [count][terms][24] Jacobian terms
+  uint32_t prio;            // s_setprio level (0..3)
 };
 
 hipError_t launch_binom(const BinomArgs& a, hipStream_t st);

@@ -201,24 +201,46 @@ class CollectBatch:
         else:
             rng = [m.range_proofs[i] for m in msgs for i in range(n)]
         # receivers (placeholders past the keys the LocalKey holds: odd modulus 3)
+        rst = list(sts[:avail]) + [None] * (n - avail)
         F = {"recv_n": G.field([x.n for x in keys[:avail]] + [3] * (n - avail)),
+             "recv_ntilde": G.field([s.N if s else 3 for s in rst]),
+             "recv_h1": G.field([s.g if s else 1 for s in rst]),
+             "recv_h2": G.field([s.ni if s else 1 for s in rst]),
              "pdl_s2": G.field(pdl, "s2"), "rp_s": G.field(rng, "s")}
-        # stage 1: the fields fsdkr_collect_prestart reads (GA's bases and moduli), at
-        # the width they need; stage 2 (complete) keeps them if the batch width agrees
-        ga_bits = max(1, F["recv_n"][1], F["pdl_s2"][1], F["rp_s"][1])
+        for a in ("s1", "s3"):
+            F["pdl_" + a] = G.field(pdl, a)
+        for a in ("s1", "s2"):
+            F["rp_" + a] = G.field(rng, a)
+        for a in ("S", "T", "N"):
+            F["ped_" + a] = G.field([m.ring_pedersen_statement for m in all_m], a)
+        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
+        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
+        if any(len(x) < M for x in A) or any(len(z) < M for z in Z):
+            c.ped_lens = k(np.array([[len(x), len(z)] for x, z in zip(A, Z)], dtype=np.uint32))
+        F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
+        F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
+        c.s1l = _limbs_for(max(F["pdl_s1"][1], F["rp_s1"][1], 1))
+        c.s3l = _limbs_for(max(F["pdl_s3"][1], F["rp_s2"][1], 1))
+        c.zl = _limbs_for(max(F["ped_Z"][1], 1))
+        # stage 1: the fields fsdkr_collect_prestart reads (GA's bases and moduli, the
+        # h1/h2 table bases and the exponents that size the tables), at the width they
+        # need; stage 2 (complete) keeps them if the batch width agrees
+        ga_bits = max(1, *(F[x][1] for x in ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s",
+                                              "ped_T", "ped_N")))
         nl_ga = 64 if ga_bits <= 2048 else 96 if ga_bits <= 3072 else None
         self._ga = None
         if staged and nl_ga is not None:
             Gs = _Gather()
-            ga = {name: Gs.slot(F[name], nl_ga) for name in ("recv_n", "pdl_s2", "rp_s")}
+            ga = {name: Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c))
+                  for name in ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s", "pdl_s1", "rp_s1",
+                               "pdl_s3", "rp_s2", "ped_T", "ped_N", "ped_Z")}
             Gs.run()
             for name, arr in ga.items():
                 setattr(c, name, k(arr))
             c.nl = nl_ga
             self._ga = (nl_ga, ga)
         self._pending = dict(msgs=msgs, joins=joins, all_m=all_m, n=n, M=M, G=G, F=F, ckl=ckl, f_ckn=f_ckn,
-                             f_sig=f_sig, ck_short=ck_short, sig=sig, pdl=pdl, rng=rng, rst=list(sts[:avail]) +
-                             [None] * (n - avail), t=local_key.t)
+                             f_sig=f_sig, ck_short=ck_short, sig=sig, pdl=pdl, rng=rng, t=local_key.t)
         if not staged:
             self.complete()
 
@@ -231,23 +253,12 @@ class CollectBatch:
         c, k = self.c, self._k
         msgs, joins, all_m, n, M, G, F = (st[x] for x in ("msgs", "joins", "all_m", "n", "M", "G", "F"))
         J = len(joins)
-        pdl, rng, rst = st["pdl"], st["rng"], st["rst"]
-        F.update({"recv_ntilde": G.field([s.N if s else 3 for s in rst]),
-                  "recv_h1": G.field([s.g if s else 1 for s in rst]),
-                  "recv_h2": G.field([s.ni if s else 1 for s in rst]),
-                  "enc": G.field([m.points_encrypted_vec[i] for m in msgs for i in range(n)])})
-        for a in ("z", "u2", "u3", "s1", "s3"):
+        pdl, rng = st["pdl"], st["rng"]
+        F["enc"] = G.field([m.points_encrypted_vec[i] for m in msgs for i in range(n)])
+        for a in ("z", "u2", "u3"):
             F["pdl_" + a] = G.field(pdl, a)
-        for a in ("z", "e", "s1", "s2"):
+        for a in ("z", "e"):
             F["rp_" + a] = G.field(rng, a)
-        for a in ("S", "T", "N"):
-            F["ped_" + a] = G.field([m.ring_pedersen_statement for m in all_m], a)
-        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
-        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
-        if any(len(x) < M for x in A) or any(len(z) < M for z in Z):
-            c.ped_lens = k(np.array([[len(x), len(z)] for x, z in zip(A, Z)], dtype=np.uint32))
-        F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
-        F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
         if J:
             for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
                 F["dlog_" + name] = G.field([j.dlog_statement for j in joins], attr)
@@ -266,16 +277,17 @@ class CollectBatch:
             raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
         c.nl = nl
         c.ckl = max(st["ckl"], nl)
-        c.s1l = _limbs_for(bits("pdl_s1", "rp_s1"))
-        c.s3l = _limbs_for(bits("pdl_s3", "rp_s2"))
         c.el = _limbs_for(bits("rp_e"))
-        c.zl = _limbs_for(bits("ped_Z"))
         c.yl = _limbs_for(bits("dlog_y1", "dlog_y2"))
         width = {"enc": 2 * nl, "pdl_u2": 2 * nl, "pdl_s1": c.s1l, "rp_s1": c.s1l, "pdl_s3": c.s3l, "rp_s2": c.s3l,
                  "rp_e": c.el, "ped_Z": c.zl, "dlog_y1": c.yl, "dlog_y2": c.yl}
-        staged = self._ga is not None and self._ga[0] == nl   # stage-1 arrays already at this width
+        # stage-1 arrays: the nl-wide ones are kept if the batch width agrees, the
+        # s1l / s3l-wide ones always (their widths do not depend on nl)
+        keep = set()
+        if self._ga is not None:
+            keep = {x for x in self._ga[1] if self._ga[0] == nl or x in _STAGE1_WIDTH}
         for name, f in F.items():
-            if not (staged and name in self._ga[1]):
+            if name not in keep:
                 setattr(c, name, k(G.slot(f, width.get(name, nl))))
         c.ck_n = k(G.slot(st["f_ckn"], c.ckl))
         if st["ck_short"]:
@@ -310,6 +322,11 @@ class CollectBatch:
         if rc != 0:
             raise RuntimeError(f"fsdkr_collect_first_error failed ({rc})")
         return err
+
+
+# stage-1 fields whose slot width does not depend on nl
+_STAGE1_WIDTH = {"pdl_s1": lambda c: c.s1l, "rp_s1": lambda c: c.s1l, "pdl_s3": lambda c: c.s3l,
+                 "rp_s2": lambda c: c.s3l, "ped_Z": lambda c: c.zl}
 
 
 class _ZeroAlice:

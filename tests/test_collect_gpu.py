@@ -242,6 +242,19 @@ def test_prestart_hit_and_miss(gpu_ctx):
     want[1 * 3 + 2] = 7 & ~2   # u2 of pair (message 1, receiver 2)
     assert [int(x) & 7 for x in v2.pdl] == want
     assert (v2.range & 1).all()
+    # GA rows reusable, h1/h2 tables not: an s3 far wider than the prestart sized
+    # the h2 tables for (u3 of that pair fails; everything else still verifies)
+    gpu_ctx.collect_prestart(CollectBatch(msgs, lk, [], 256, KB, staged=True))
+    wide = copy.deepcopy(msgs)
+    p = wide[2].pdl_proof_vec[0]
+    wide[2].pdl_proof_vec[0] = dataclasses.replace(p, s3=p.s3 << 40)
+    b4 = CollectBatch(wide, lk, [], 256, KB)
+    gpu_ctx.collect_prepare(b4)
+    v4 = gpu_ctx.collect_run(b4)
+    want = [7] * 9
+    want[2 * 3 + 0] = 7 & ~4
+    assert [int(x) & 7 for x in v4.pdl] == want
+    assert (v4.range & 1).all()
     # in flight: refused
     b3 = CollectBatch(msgs, lk, [], 256, KB, staged=True)
     gpu_ctx.collect_prepare(CollectBatch(msgs, lk, [], 256, KB))

@@ -97,12 +97,12 @@ def _fake_collect(n=6, t=2, M=8, J=2, seed=3, big_ped=False):
 
     def msg(i):
         return NS(party_index=i + 1,
-                  pdl_proof_vec=[NS(z=r(2040), u1=pt(), u2=r(4090), u3=r(2040), s1=r(1024), s2=r(2040), s3=r(2300))
-                                 for _ in range(n)],
+                  pdl_proof_vec=[NS(z=r(3000 if big_ped and i == 1 and q == 2 else 2040), u1=pt(), u2=r(4090),
+                                    u3=r(2040), s1=r(1024), s2=r(2040), s3=r(2300)) for q in range(n)],
                   points_committed_vec=[pt() for _ in range(n)], points_encrypted_vec=[r(4090) for _ in range(n)],
                   range_proofs=[NS(z=r(2040), e=r(256), s=r(2040), s1=r(1024), s2=r(2300)) for _ in range(n)],
                   coefficients_committed_vec=NS(commitments=[pt() for _ in range(t + 1)]),
-                  ring_pedersen_statement=NS(N=r(3000 if big_ped and i == 1 else 2048), S=r(2040), T=r(2040)),
+                  ring_pedersen_statement=NS(N=r(2048), S=r(2040), T=r(2040)),
                   ring_pedersen_proof=NS(A=[r(2040) for _ in range(M)], Z=[r(2300) for _ in range(M)]),
                   ek=NS(n=r(2048)), dk_correctness_proof=NS(sigma_vec=[r(2040) for _ in range(11)]))
     msgs = [msg(i) for i in range(n - J)]
@@ -139,8 +139,8 @@ def _dump(b, M):
 @pytest.mark.parametrize("big_ped", [False, True])
 def test_staged_batch_equals_one_shot(big_ped):
     """CollectBatch(staged=True) + complete() packs exactly what the one-shot
-    constructor packs, also when stage 1's width is superseded (a 3000-bit
-    ring-Pedersen modulus moves the batch to 3072-bit slots)."""
+    constructor packs, also when stage 1's width is superseded (a 3000-bit PDL z,
+    a stage-2 field, moves the batch to 3072-bit slots)."""
     from fsdkr.batch import CollectBatch
     M = 8
     msgs, joins, lk = _fake_collect(M=M, big_ped=big_ped)

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--joins", type=int, default=4)
     ap.add_argument("--t", type=int, default=32)
     ap.add_argument("--hwq", type=int, default=0)
+    ap.add_argument("--full", action="store_true",
+                    help="time whole refresh.collect() calls (bench.py's step) instead of collect_run")
     a = ap.parse_args()
     import torch  # noqa: F401
     from fsdkr import Context, synth
@@ -41,6 +43,17 @@ def main():
             print(f"multi-session run {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
         return
     msgs, joins, lk = synth.synth_collect(ctx, a.n - a.joins, a.joins, a.t, 2024)
+    if a.full:
+        import copy
+        from fsdkr import refresh
+        keys = [copy.deepcopy(lk) for _ in range(a.steps + 1)]
+        refresh.collect(msgs, keys[-1], lk.paillier_dk, joins, ctx=ctx)
+        for k in range(a.steps):
+            time.sleep(0.02)
+            t0 = time.perf_counter()
+            refresh.collect(msgs, keys[k], lk.paillier_dk, joins, ctx=ctx)
+            print(f"collect {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+        return
     b = CollectBatch(msgs, lk, joins, 256, 2048)
     ctx.collect_prepare(b)
     for _ in range(a.steps):
