@@ -211,7 +211,8 @@ static void* worker(void* arg) {
 static void run_work(Work* w, int threads) {
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
-  if ((size_t)threads > w->n / CHUNK + 1) threads = (int)(w->n / CHUNK + 1);
+  /* a worker pays for itself past ~16 chunks (thread start ~ tens of us) */
+  if ((size_t)threads > w->n / (16 * CHUNK) + 1) threads = (int)(w->n / (16 * CHUNK) + 1);
   pthread_t tid[64];
   int started = 0;
   for (int i = 1; i < threads; ++i)

@@ -143,15 +143,14 @@ def _ptr(a):
 
 
 def ints_to_limbs(values, limbs):
-    """list of non-negative ints -> (len, limbs) uint32 little-endian array."""
-    out = np.zeros((len(values), limbs), dtype=np.uint32)
-    nbytes = 4 * limbs
-    buf = bytearray(nbytes * len(values))
-    for i, v in enumerate(values):
-        if v < 0 or v.bit_length() > 32 * limbs:
-            raise ValueError(f"value {i} does not fit {limbs} limbs")
-        buf[i * nbytes:(i + 1) * nbytes] = v.to_bytes(nbytes, "little")
-    out[:] = np.frombuffer(bytes(buf), dtype=np.uint32).reshape(len(values), limbs)
+    """list of non-negative ints -> (len, limbs) uint32 little-endian array
+    (csrc/pack.c digit re-slicing); ValueError if a value is negative or too wide."""
+    from . import _pack
+    out = np.empty((len(values), limbs), dtype=np.uint32)
+    try:
+        _pack.pack(values, None, out, limbs)
+    except OverflowError:
+        raise ValueError(f"a value does not fit {limbs} limbs") from None
     return out
 
 
@@ -296,6 +295,17 @@ class Context:
         self._many = arr   # keep the array alive until finish
         self.check(self._lib.fsdkr_collect_prepare_multi(self._h, arr, len(batches)))
 
+    def collect_prepare_set(self, sset):
+        """Prepare every live session of a fsdkr.batch.SessionSet as ONE device image."""
+        self._many = sset   # keep the struct rows alive until finish
+        self.check(self._lib.fsdkr_collect_prepare_multi(self._h, sset.c_array, len(sset.live)))
+
+    def collect_finish_set(self, sset):
+        """Wait for the launched multi-session pipeline; SetVerdicts of the live sessions."""
+        v = sset.verdicts()
+        self.check(self._lib.fsdkr_collect_finish_multi(self._h, v.c_array, len(sset.live)))
+        return v
+
     def collect_finish_many(self, batches):
         """Wait for the launched multi-session pipeline; one Verdicts per session."""
         from .batch import Verdicts
@@ -366,14 +376,11 @@ class Context:
 
     def ec_msm(self, points, scalars):
         """points/scalars: lists (count) of equal-length lists; points are (x, y) or None."""
+        from . import _pack
         count, terms = len(points), len(points[0])
-        Pt = np.zeros((count, terms, 16), dtype=np.uint32)
-        for o in range(count):
-            for j in range(terms):
-                pt = points[o][j]
-                if pt is not None:
-                    Pt[o, j] = ints_to_limbs([pt[0] | (pt[1] << 256)], 16)[0]
-        Sc = ints_to_limbs([s for row in scalars for s in row], 8).reshape(count, terms, 8)
+        Pt = np.empty((count * terms, 16), dtype=np.uint32)
+        _pack.points([pt for row in points for pt in row], None, Pt)
+        Sc = ints_to_limbs([s for row in scalars for s in row], 8)
         O = np.zeros((count, 16), dtype=np.uint32)
         self.check(self._lib.fsdkr_ec_msm(self._h, count, terms, _ptr(Pt), _ptr(Sc), _ptr(O)))
         out = []

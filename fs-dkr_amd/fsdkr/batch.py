@@ -334,3 +334,226 @@ class _ZeroAlice:
 
 
 _ZERO_ALICE = _ZeroAlice()
+
+
+def _struct_dtype(cls):
+    """numpy structured dtype with the exact layout of a ctypes Structure (pointers as u8)."""
+    names, formats, offsets = [], [], []
+    for name, typ in cls._fields_:
+        names.append(name)
+        formats.append(np.uint64 if ctypes.sizeof(typ) == 8 else np.uint32)
+        offsets.append(getattr(cls, name).offset)
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": ctypes.sizeof(cls)})
+
+
+_BATCH_DT = _struct_dtype(CollectBatchC)
+_VERD_DT = _struct_dtype(VerdictsC)
+
+
+def _regular(msgs, lk, joins, M):
+    """The shape a SessionSet packs without per-session optional fields: every
+    vector at full length, the LocalKey holding every receiver's keys, t+1
+    commitments per message, and the threshold / size checks passing."""
+    R, J = len(msgs), len(joins)
+    n = R + J
+    t = lk.t
+    if R == 0 or R <= t or len(lk.paillier_key_vec) < n or len(lk.h1_h2_n_tilde_vec) < n:
+        return False
+    for m in msgs:
+        if not (len(m.pdl_proof_vec) == len(m.points_committed_vec) == len(m.points_encrypted_vec) == n) or \
+                len(m.range_proofs) < n or len(m.coefficients_committed_vec.commitments) != t + 1:
+            return False
+    for m in msgs + joins:
+        if len(m.ring_pedersen_proof.A) < M or len(m.ring_pedersen_proof.Z) < M or \
+                len(m.dk_correctness_proof.sigma_vec) < M2:
+            return False
+    return True
+
+
+class SessionSet:
+    """Many independent collect() sessions (BASELINE configs[4]) packed as ONE set
+    of SoA arrays: every field is gathered across all regular sessions in one
+    pass (one gather, one threaded conversion), and each session's
+    fsdkr_collect_batch points at its rows (a numpy array with the C struct
+    layout, filled vectorised).  Sessions of another shape get their own
+    CollectBatch; header-only sessions (threshold / size failures) are not
+    prepared.  `live` lists the prepared sessions, in `structs` row order."""
+
+    def __init__(self, sessions, m_security=256, key_bits=2048):
+        M = m_security
+        S = len(sessions)
+        self.S = S
+        self.batches = [None] * S
+        reg = [s for s, (m, lk, j) in enumerate(sessions) if _regular(m, lk, j, M)]
+        regset = set(reg)
+        for s, (m, lk, j) in enumerate(sessions):
+            if s not in regset:
+                self.batches[s] = CollectBatch(m, lk, j, M, key_bits)
+        self.live = [s for s in range(S) if s in regset or not self.batches[s].header_only]
+        self.R = np.array([len(sessions[s][0]) for s in range(S)], dtype=np.int64)
+        self.J = np.array([len(sessions[s][2]) for s in range(S)], dtype=np.int64)
+        self.n = self.R + self.J
+        self._keep = []
+        self.structs = np.zeros(len(self.live), dtype=_BATCH_DT)
+        if reg:
+            self._pack_regular(sessions, reg, M, key_bits)
+        row = {s: r for r, s in enumerate(self.live)}
+        for s in self.live:
+            if s not in regset:
+                b = self.batches[s]
+                self.structs[row[s]] = np.frombuffer(ctypes.string_at(ctypes.addressof(b.c), ctypes.sizeof(b.c)),
+                                                     dtype=_BATCH_DT)[0]
+        self.row = row
+
+    def _k(self, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.uint32)
+        self._keep.append(arr)
+        return arr.ctypes.data
+
+    def _pack_regular(self, sessions, reg, M, key_bits):
+        G = _Gather()
+        ses = [sessions[s] for s in reg]
+        R = np.array([len(m) for m, lk, j in ses], dtype=np.int64)
+        J = np.array([len(j) for m, lk, j in ses], dtype=np.int64)
+        n = R + J
+        Mt, P = R + J, R * n
+        t = np.array([lk.t for m, lk, j in ses], dtype=np.int64)
+        V = R * (t + 1)
+        all_m = [m + j for m, lk, j in ses]
+        pdl = [m.pdl_proof_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)]
+        rng = [m.range_proofs[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)]
+        keys = [k for (ms, lk, js), nn in zip(ses, n) for k in lk.paillier_key_vec[:nn]]
+        sts = [s for (ms, lk, js), nn in zip(ses, n) for s in lk.h1_h2_n_tilde_vec[:nn]]
+        msgs = [m for ms, lk, js in ses for m in ms]
+        joins = [j for ms, lk, js in ses for j in js]
+        am = [m for row in all_m for m in row]
+        F = {"recv_n": G.field(keys, "n"), "recv_ntilde": G.field(sts, "N"), "recv_h1": G.field(sts, "g"),
+             "recv_h2": G.field(sts, "ni"),
+             "enc": G.field([m.points_encrypted_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms
+                             for i in range(nn)])}
+        for a in ("z", "u2", "u3", "s1", "s2", "s3"):
+            F["pdl_" + a] = G.field(pdl, a)
+        for a in ("z", "e", "s", "s1", "s2"):
+            F["rp_" + a] = G.field(rng, a)
+        for a in ("S", "T", "N"):
+            F["ped_" + a] = G.field([m.ring_pedersen_statement for m in am], a)
+        F["ped_A"] = G.field([v for m in am for v in m.ring_pedersen_proof.A[:M]])
+        F["ped_Z"] = G.field([v for m in am for v in m.ring_pedersen_proof.Z[:M]])
+        f_ckn = G.field([m.ek.n for m in am])
+        f_sig = G.field([v for m in am for v in m.dk_correctness_proof.sigma_vec[:M2]])
+        if joins:
+            for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
+                F["dlog_" + name] = G.field([j.dlog_statement for j in joins], attr)
+            for name, which, attr in (("x1", 1, "x"), ("x2", 2, "x"), ("y1", 1, "y"), ("y2", 2, "y")):
+                F["dlog_" + name] = G.field([getattr(j, f"composite_dlog_proof_base_h{which}") for j in joins], attr)
+
+        def bits(*names):
+            return max([1] + [F[x][1] for x in names if x in F])
+
+        ck_bits = max(1, f_ckn[1], f_sig[1])
+        ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
+        if ckl is None:
+            raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
+        nl_bits = max(bits("recv_n", "recv_ntilde", "recv_h1", "recv_h2"), bits("ped_N", "ped_S", "ped_T", "ped_A"),
+                      bits("dlog_N", "dlog_g", "dlog_ni", "dlog_x1", "dlog_x2"),
+                      bits("pdl_z", "pdl_u3", "pdl_s2", "rp_z", "rp_s"), (bits("enc", "pdl_u2") + 1) // 2)
+        nl = 64 if nl_bits <= 2048 else 96 if nl_bits <= 3072 else None
+        if nl is None:
+            raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
+        W = {"nl": nl, "ckl": max(ckl, nl), "s1l": _limbs_for(bits("pdl_s1", "rp_s1")),
+             "s3l": _limbs_for(bits("pdl_s3", "rp_s2")), "el": _limbs_for(bits("rp_e")),
+             "zl": _limbs_for(bits("ped_Z")), "yl": _limbs_for(bits("dlog_y1", "dlog_y2"))}
+        width = {"enc": 2 * nl, "pdl_u2": 2 * nl, "pdl_s1": W["s1l"], "rp_s1": W["s1l"], "pdl_s3": W["s3l"],
+                 "rp_s2": W["s3l"], "rp_e": W["el"], "ped_Z": W["zl"], "dlog_y1": W["yl"], "dlog_y2": W["yl"]}
+        arrs = {name: G.slot(f, width.get(name, nl)) for name, f in F.items()}
+        arrs["ck_n"] = G.slot(f_ckn, W["ckl"])
+        arrs["ck_sigma"] = G.slot(f_sig, W["ckl"])
+        G.run()
+        arrs["commit"] = pack_points([m.points_committed_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms
+                                      for i in range(nn)])
+        arrs["pdl_u1"] = pack_points(pdl, "u1")
+        arrs["vss"] = pack_points([p for m in msgs for p in m.coefficients_committed_vec.commitments])
+        # party indices per session: refresh then joins (0 = unassigned)
+        pidx = np.array([x for ms, lk, js in ses for x in [m.party_index for m in ms] +
+                         [(j.party_index or 0) for j in js]], dtype=np.uint32)
+        lens = np.repeat(n, R)[:, None].repeat(3, axis=1).astype(np.uint32)
+        arrs["party_index"], arrs["msg_lens"] = pidx, lens
+        # row offsets of every session, per row class
+        def starts(counts):
+            return np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.uint64)
+        row_of = {"recv": starts(n), "pair": starts(P), "vss": starts(V), "msg": starts(Mt),
+                  "rpm": starts(Mt * M), "sig": starts(Mt * M2), "join": starts(J), "pidx": starts(Mt),
+                  "lens": starts(R)}
+        klass = {"recv_n": "recv", "recv_ntilde": "recv", "recv_h1": "recv", "recv_h2": "recv", "enc": "pair",
+                 "commit": "pair", "pdl_z": "pair", "pdl_u1": "pair", "pdl_u2": "pair", "pdl_u3": "pair",
+                 "pdl_s1": "pair", "pdl_s2": "pair", "pdl_s3": "pair", "rp_z": "pair", "rp_e": "pair",
+                 "rp_s": "pair", "rp_s1": "pair", "rp_s2": "pair", "vss": "vss", "ped_S": "msg", "ped_T": "msg",
+                 "ped_N": "msg", "ped_A": "rpm", "ped_Z": "rpm", "ck_n": "msg", "ck_sigma": "sig",
+                 "dlog_N": "join", "dlog_g": "join", "dlog_ni": "join", "dlog_x1": "join", "dlog_x2": "join",
+                 "dlog_y1": "join", "dlog_y2": "join", "party_index": "pidx", "msg_lens": "lens"}
+        row = {s: r for r, s in enumerate(self.live)}
+        rows = np.array([row[s] for s in reg], dtype=np.int64)
+        st = self.structs
+        for f, v in (("n_refresh", R), ("n_join", J), ("t", t)):
+            st[f][rows] = v
+        for f, v in (("m_security", M), ("key_bits", key_bits)):
+            st[f][rows] = v
+        for f in ("nl", "s1l", "s3l", "el", "zl", "yl", "ckl"):
+            st[f][rows] = W[f]
+        for name, arr in arrs.items():
+            stride = arr.shape[1] * 4 if arr.ndim == 2 else 4
+            base = self._k(arr)
+            st[name][rows] = np.uint64(base) + row_of[klass[name]] * np.uint64(stride)
+
+    @property
+    def c_array(self):
+        """the fsdkr_collect_batch array (live sessions) as ctypes pointer"""
+        return ctypes.cast(self.structs.ctypes.data, ctypes.POINTER(CollectBatchC))
+
+    def verdicts(self):
+        """Verdict arrays of the live sessions and their fsdkr_verdicts array."""
+        return SetVerdicts(self)
+
+    def first_error(self, s, verdicts):
+        """fsdkr_collect_first_error of session s (live: its prepared verdicts; else header only)."""
+        if s not in self.row:
+            return self.batches[s].first_error(None)
+        err = ErrorC()
+        r = self.row[s]
+        bp = ctypes.cast(self.structs.ctypes.data + r * _BATCH_DT.itemsize, ctypes.POINTER(CollectBatchC))
+        vp = ctypes.cast(verdicts.structs.ctypes.data + r * _VERD_DT.itemsize, ctypes.POINTER(VerdictsC))
+        rc = lib().fsdkr_collect_first_error(bp, vp, ctypes.byref(err))
+        if rc != 0:
+            raise RuntimeError(f"fsdkr_collect_first_error failed ({rc})")
+        return err
+
+
+class SetVerdicts:
+    """Verdict bytes of every live session of a SessionSet, one array per kind,
+    and the per-session fsdkr_verdicts rows pointing into them."""
+
+    def __init__(self, sset):
+        live = sset.live
+        R, J, n = sset.R[live], sset.J[live], sset.n[live]
+        P, Mt = R * n, R + J
+        self.P, self.Mt, self.Jn = P, Mt, J
+
+        def starts(c):
+            return np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.uint64)
+        self.feldman = np.zeros(max(int(P.sum()), 1), np.uint8)
+        self.pdl = np.zeros_like(self.feldman)
+        self.range = np.zeros_like(self.feldman)
+        self.ped = np.zeros(max(int(Mt.sum()), 1), np.uint8)
+        self.ck = np.zeros_like(self.ped)
+        self.dlog = np.zeros(max(int(J.sum()), 1), np.uint8)
+        self.off = {"pair": starts(P), "msg": starts(Mt), "join": starts(J)}
+        st = np.zeros(len(live), dtype=_VERD_DT)
+        for name, kind in (("feldman", "pair"), ("pdl", "pair"), ("range", "pair"), ("ped", "msg"), ("ck", "msg"),
+                           ("dlog", "join")):
+            st[name] = np.uint64(getattr(self, name).ctypes.data) + self.off[kind]
+        st["cap_pairs"], st["cap_msgs"], st["cap_joins"] = P, Mt, J
+        self.structs = st
+
+    @property
+    def c_array(self):
+        return ctypes.cast(self.structs.ctypes.data, ctypes.POINTER(VerdictsC))

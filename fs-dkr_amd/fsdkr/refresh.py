@@ -12,7 +12,7 @@ is deterministic, so running it early changes nothing but the latency).
 collect_many() verifies many independent sessions in one device pass
 (BASELINE configs[4]).  There is no CPU fallback."""
 from ._native import Context
-from .batch import CollectBatch
+from .batch import CollectBatch, SessionSet
 
 Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 GX = 0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798
@@ -175,22 +175,26 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
     raise (local_key partially updated as collect() leaves it)."""
     ctx = _ctx(ctx)
     sess = [(list(r), lk, dk, list(j)) for r, lk, dk, j in sessions]
-    batches = [CollectBatch(r, lk, j, m_security, key_bits) for r, lk, dk, j in sess]
-    live = [i for i, b in enumerate(batches) if not b.header_only]
-    verdicts = [None] * len(sess)
+    # one gather across the sessions (SessionSet); sessions of another shape keep
+    # their own batch, header-only ones are mapped without a device pass
+    sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits)
+    live = sset.live
     specs = [None] * len(sess)
+    verdicts = None
     if live:
-        ctx.collect_prepare_many([batches[i] for i in live])
+        ctx.collect_prepare_set(sset)
         ctx.collect_launch()
         res = _speculative(ctx, [(sess[i][0], sess[i][1], len(sess[i][0]) + len(sess[i][3])) for i in live])
         for i, r in zip(live, res):
             specs[i] = r
-        vs = ctx.collect_finish_many([batches[i] for i in live])
-        for i, v in zip(live, vs):
-            verdicts[i] = v
+        verdicts = ctx.collect_finish_set(sset)
     out = []
     for i, (msgs, lk, dk, joins) in enumerate(sess):
-        err, applied = _mapped(ctx, batches[i], msgs, verdicts[i])
+        if i in sset.row:
+            e = sset.first_error(i, verdicts)
+            err, applied = _error_of(e), e.keys_applied
+        else:
+            err, applied = _mapped(ctx, sset.batches[i], msgs, None)
         _apply_keys(lk, msgs, joins, applied)
         if err is None and isinstance(specs[i], Exception):
             err = specs[i]

@@ -132,7 +132,7 @@ def _dump(b, M):
             "dlog_y1": (J, c.yl), "dlog_y2": (J, c.yl)}
     out = {"widths": (c.nl, c.ckl, c.s1l, c.s3l, c.el, c.zl, c.yl)}
     for name, (r_, w) in rows.items():
-        out[name] = np.ctypeslib.as_array(getattr(c, name), shape=(r_ * w,)).copy()
+        out[name] = np.ctypeslib.as_array(getattr(c, name), shape=(r_ * w,)).copy() if r_ * w else None
     return out
 
 
@@ -152,4 +152,40 @@ def test_staged_batch_equals_one_shot(big_ped):
     a, b = _dump(one, M), _dump(st, M)
     assert a["widths"] == b["widths"] and a["widths"][0] == (96 if big_ped else 64)
     for k in a:
-        assert np.array_equal(a[k], b[k]), k
+        assert (a[k] is None and b[k] is None) or np.array_equal(a[k], b[k]), k
+
+
+def test_session_set_equals_per_session_batches():
+    """SessionSet (configs[4]: one gather across all sessions, per-session struct
+    rows filled vectorised) points every regular session at exactly the arrays
+    its own CollectBatch packs; irregular sessions keep their own batch, and a
+    header-only session is not prepared."""
+    from types import SimpleNamespace as NSp
+    from fsdkr._native import CollectBatchC
+    from fsdkr.batch import CollectBatch, SessionSet, _BATCH_DT
+    M = 8
+    sessions = []
+    for s in range(5):
+        msgs, joins, lk = _fake_collect(n=3, t=1, M=M, J=1 if s == 2 else 0, seed=10 + s)
+        sessions.append((msgs, lk, joins))
+    # irregular: a short range_proofs vector; header only: threshold (R <= t)
+    m0 = sessions[3][0][0]
+    m0.range_proofs = m0.range_proofs[:2]
+    hm, hj, hl = _fake_collect(n=3, t=1, M=M, J=0, seed=99)
+    sessions.append((hm[:1], hl, []))
+    ss = SessionSet(sessions, M, 2048)
+    assert ss.live == [0, 1, 2, 3, 4] and ss.batches[5].header_only and ss.batches[3] is not None
+    for s in ss.live:
+        one = CollectBatch(sessions[s][0], sessions[s][1], sessions[s][2], M, 2048)
+        row = NSp(c=CollectBatchC.from_address(ss.structs.ctypes.data + ss.row[s] * _BATCH_DT.itemsize),
+                  R=one.R, J=one.J, n=one.n, _msgs=sessions[s][0])
+        one._msgs = sessions[s][0]
+        a, b = _dump(one, M), _dump(row, M)
+        if one.J == 0:   # yl (DLog y limbs) is the set's width, unused without joins
+            a["widths"], b["widths"] = a["widths"][:-1], b["widths"][:-1]
+        for k in a:
+            assert (a[k] is None and b[k] is None) or np.array_equal(a[k], b[k]), (s, k)
+        for f in ("n_refresh", "n_join", "t", "m_security", "key_bits", "n_recv", "recv_avail"):
+            assert getattr(one.c, f) == getattr(row.c, f), (s, f)
+        pi = np.ctypeslib.as_array(row.c.party_index, shape=(one.R + one.J,))
+        assert list(pi) == [m.party_index for m in sessions[s][0]] + [j.party_index or 0 for j in sessions[s][2]]

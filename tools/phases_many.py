@@ -22,27 +22,27 @@ def main():
     a = ap.parse_args()
     import torch  # noqa: F401
     from fsdkr import Context, synth
-    from fsdkr.batch import CollectBatch
-    from fsdkr.refresh import _mapped, _apply_keys, _apply_share, _speculative, collect_many
+    from fsdkr.refresh import _apply_keys, _apply_share, _speculative, collect_many
     ctx = Context()
     sess = synth.synth_sessions(ctx, a.sessions, n=3, t=1, seed=9, key_bits=3072)
+    from fsdkr.batch import SessionSet
     for rep in range(a.reps):
         work = [(m, copy.deepcopy(lk), dk, j) for (m, j, lk, dk) in sess]
         t0 = time.perf_counter()
-        batches = [CollectBatch(m, lk, j, 256, 3072) for m, lk, dk, j in work]
+        sset = SessionSet([(m, lk, j) for m, lk, dk, j in work], 256, 3072)
         t1 = time.perf_counter()
-        ctx.collect_prepare_many(batches)
+        ctx.collect_prepare_set(sset)
         t2 = time.perf_counter()
         ctx.collect_launch()
         t3 = time.perf_counter()
         specs = _speculative(ctx, [(m, lk, len(m) + len(j)) for m, lk, dk, j in work])
         t4 = time.perf_counter()
-        vs = ctx.collect_finish_many(batches)
+        v = ctx.collect_finish_set(sset)
         t5 = time.perf_counter()
-        for (m, lk, dk, j), b, v, sp in zip(work, batches, vs, specs):
-            err, applied = _mapped(ctx, b, m, v)
-            _apply_keys(lk, m, j, applied)
-            assert err is None and not isinstance(sp, Exception)
+        for s, ((m, lk, dk, j), sp) in enumerate(zip(work, specs)):
+            e = sset.first_error(s, v)
+            _apply_keys(lk, m, j, e.keys_applied)
+            assert e.variant == 0 and not isinstance(sp, Exception)
             _apply_share(lk, dk, sp)
         t6 = time.perf_counter()
         work2 = [(m, copy.deepcopy(lk), dk, j) for (m, j, lk, dk) in sess]
@@ -57,7 +57,7 @@ def main():
     for _ in range(2):
         t0 = time.perf_counter()
         ctx.collect_launch()
-        ctx.collect_finish_many(batches)
+        ctx.collect_finish_set(sset)
         runs.append((time.perf_counter() - t0) * 1e3)
     print(json.dumps({"device_pipeline_ms": min(runs)}), flush=True)
 
