@@ -154,3 +154,17 @@ def test_sampled_pairs_n16(gpu_ctx):
             p = r * n + d["i"]
             assert (int(v.pdl[p]) & 7, bool(v.range[p] & 1)) == (d["expect_pdl_bits"], d["expect_range_ok"]), \
                 d["tamper"]
+
+
+def test_collect_after_wire_round_trip(gpu_ctx):
+    """Messages and the LocalKey read back from their serde wire text
+    (fsdkr.wire) go through the GPU collect() with the frozen outcome: the
+    ingest path for reference-produced transcripts."""
+    from fsdkr import wire
+    raw, cls, d = _load("transcript_t1_n3_kb2048.json.gz")
+    kb = raw["meta"]["key_bits"]
+    msgs = [wire.loads(wire.dumps(m), "RefreshMessage") for m in d["msgs"]]
+    e = d["expect"][1]
+    key = wire.loads(wire.dumps(d["keys"][e["party"]]), "LocalKey")
+    res, k = _collect(msgs, key, d["dks"][e["party"]], [], kb, gpu_ctx)
+    assert res is None and k.x_i == e["key_after"]["x_i"] and list(k.pk_vec) == e["key_after"]["pk_vec"]
