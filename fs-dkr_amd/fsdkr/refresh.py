@@ -207,6 +207,57 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
     return out
 
 
+def _public_view(lk):
+    """What verification reads from a LocalKey: the receivers' keys and statements."""
+    return (lk.t, tuple(e.n for e in lk.paillier_key_vec),
+            tuple((s.N, s.g, s.ni) for s in lk.h1_h2_n_tilde_vec))
+
+
+def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=256, key_bits=2048):
+    """Every party's RefreshMessage::collect over the same broadcast messages,
+    with the proofs verified ONCE.  In the reference each
+    party runs collect() and re-verifies the same n^2 proofs (test.rs:328-331);
+    verification reads only public LocalKey data (paillier_key_vec,
+    h1_h2_n_tilde_vec, t), so parties whose public view agrees share one device
+    pass, one first-error mapping and one batched share recovery (each party
+    decrypts its own ciphertexts).  `parties`: list of (local_key, new_dk).
+    Returns one outcome per party, as collect_many does: None (local_key
+    updated) or the FsDkrError / FsDkrPanic collect() would raise."""
+    ctx = _ctx(ctx)
+    msgs, joins = list(refresh_messages), list(join_messages)
+    groups = {}
+    for p, (lk, dk) in enumerate(parties):
+        groups.setdefault(_public_view(lk), []).append(p)
+    out = [None] * len(parties)
+    for members in groups.values():
+        lk0 = parties[members[0]][0]
+        batch = CollectBatch(msgs, lk0, joins, m_security, key_bits, staged=True)
+        if batch.ga_ready:
+            ctx.collect_prestart(batch)
+        batch.complete()
+        specs = [None] * len(members)
+        verdicts = None
+        if not batch.header_only:
+            ctx.collect_prepare(batch)
+            ctx.collect_launch()
+            specs = _speculative(ctx, [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members])
+            verdicts = ctx.collect_finish(batch)
+        err, applied = _mapped(ctx, batch, msgs, verdicts)
+        for p, spec in zip(members, specs):
+            lk, dk = parties[p]
+            _apply_keys(lk, msgs, joins, applied)
+            e = err
+            if e is None and isinstance(spec, Exception):
+                e = spec
+            if e is None:
+                try:
+                    _apply_share(lk, dk, spec)
+                except FsDkrPanic as x:
+                    e = x
+            out[p] = e
+    return out
+
+
 def _dk_limbs(dk):
     """Limb width holding N = p q of a decryption key (and p^2, q^2)."""
     bits = max((dk.p * dk.q).bit_length(), 2 * dk.p.bit_length(), 2 * dk.q.bit_length())

@@ -168,3 +168,20 @@ def test_collect_after_wire_round_trip(gpu_ctx):
     key = wire.loads(wire.dumps(d["keys"][e["party"]]), "LocalKey")
     res, k = _collect(msgs, key, d["dks"][e["party"]], [], kb, gpu_ctx)
     assert res is None and k.x_i == e["key_after"]["x_i"] and list(k.pk_vec) == e["key_after"]["pk_vec"]
+
+
+@pytest.mark.parametrize("name", TRANSCRIPTS[:2])
+def test_collect_all_parties_one_verification(gpu_ctx, name):
+    """refresh.collect_all: every party's collect() over the
+    same messages with ONE verification pass and one batched share recovery
+    gives each party the frozen updated LocalKey."""
+    from fsdkr import refresh
+    raw, cls, d = _load(name)
+    kb = raw["meta"]["key_bits"]
+    parties = [(copy.deepcopy(d["keys"][e["party"]]), d["dks"][e["party"]]) for e in d["expect"]]
+    res = refresh.collect_all(copy.deepcopy(d["msgs"]), parties, [], ctx=gpu_ctx, key_bits=kb)
+    assert res == [None] * len(parties)
+    for (k, _), e in zip(parties, d["expect"]):
+        want = e["key_after"]
+        assert k.x_i == want["x_i"] and k.y == want["y"] and list(k.pk_vec) == want["pk_vec"]
+        assert [x.n for x in k.paillier_key_vec] == want["paillier_n"]
