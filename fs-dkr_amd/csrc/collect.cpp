@@ -370,13 +370,20 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
   const uint32_t nA = n + Mt;
-  FbTableArgs tb{U64(o_bp) + nA, U32(o_bl) + nA, U32(o_bm) + nA, U32(o_bt) + nA, U32(o_bh) + nA, cons, g.fb_table, w,
-                 n, 3};
-  FbTableArgs ta{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nA, 2};
-  if ((rc = c->hip_check(launch_fb_table(nl, tb, ts), "prestart fb_table h2")) ||
-      (rc = c->hip_check(launch_fb_table(nl, ta, tsA), "prestart fb_table h1/T")))
-    return rc;
-  if ((rc = c->hip_check(hipEventRecord(g.fb_done_a, tsA), "event record"))) return rc;
+  const char* fse = getenv("FSDKR_FB_SPLIT");
+  if (fse && fse[0] == '1') {   // group A (h1, T) beside group B (h2) on its own stream
+    FbTableArgs tb{U64(o_bp) + nA, U32(o_bl) + nA, U32(o_bm) + nA, U32(o_bt) + nA, U32(o_bh) + nA, cons, g.fb_table,
+                   w, n, 3};
+    FbTableArgs ta{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nA, 2};
+    if ((rc = c->hip_check(launch_fb_table(nl, tb, ts), "prestart fb_table h2")) ||
+        (rc = c->hip_check(launch_fb_table(nl, ta, tsA), "prestart fb_table h1/T")))
+      return rc;
+    if ((rc = c->hip_check(hipEventRecord(g.fb_done_a, tsA), "event record"))) return rc;
+  } else {   // one launch on the table stream: the fixed-base exponent stream stays free
+    FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
+    if ((rc = c->hip_check(launch_fb_table(nl, tall, ts), "prestart fb_table"))) return rc;
+    if ((rc = c->hip_check(hipEventRecord(g.fb_done_a, ts), "event record"))) return rc;
+  }
   // fb_done covers both groups: the B chain's stream waits for A's as well
   (void)hipStreamWaitEvent(ts, g.fb_done_a, 0);
   if ((rc = c->hip_check(hipEventRecord(g.fb_done, ts), "event record"))) return rc;
