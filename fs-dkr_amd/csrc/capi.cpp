@@ -463,7 +463,7 @@ int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const
     c->fail("fsdkr_modexp_batch: null pointer or empty table");
     return FSDKR_E_ARG;
   }
-  if (!shape_digits(mod_limbs)) {
+  if (!shape_digits_g(mod_limbs, 0)) {   // the verifier's classes and 1024-bit key-generation moduli
     c->fail("fsdkr_modexp_batch: unsupported modulus width %u limbs", mod_limbs);
     return FSDKR_E_UNSUPPORTED;
   }

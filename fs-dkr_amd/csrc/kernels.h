@@ -37,4 +37,18 @@ hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint3
                        hipStream_t st);
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st);
 
+// Miller–Rabin witness tail (prime.hip): x = b^d mod c from modexp, c - 1 = d 2^s.
+struct MrTailArgs {
+  const uint32_t* x;        // [count][K32] exact
+  const uint32_t* consts;   // [count][3*KD+4]: candidate i is modulus i
+  const uint32_t* s;        // [count]
+  uint32_t s_max;           // max s over the launch (uniform loop bound)
+  uint32_t* verdict;        // [count] 1 = strong probable prime to this base
+  uint32_t count;
+};
+// Modulus widths of key generation: 32 limbs (1024-bit primes, KD = 36) beside
+// the verifier's classes.  Not accepted by the collect() entry points.
+constexpr uint32_t kPrimeLimbs = 32;
+hipError_t mr_tail(uint32_t k32, const MrTailArgs& a, hipStream_t st);
+
 }  // namespace fsdkr

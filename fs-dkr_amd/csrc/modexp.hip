@@ -221,6 +221,7 @@ int shape_digits(uint32_t k32) {
 }
 
 int shape_digits_g(uint32_t k32, uint32_t group) {
+  if (k32 == kPrimeLimbs) return 36;   // key generation only (1024-bit primes)
   return (k32 == 128 && group == kWideGroup) ? 160 : shape_digits(k32);
 }
 
@@ -232,6 +233,7 @@ hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint3
 
 hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
   switch (k32) {
+    case 32: return launch_setup<36, 2, 32>(mods, n_mod, consts, st);
     case 64: return launch_setup<72, 2, 64>(mods, n_mod, consts, st);
     case 96: return launch_setup<108, 4, 96>(mods, n_mod, consts, st);
     case 128: return launch_setup<144, 4, 128>(mods, n_mod, consts, st);
@@ -265,6 +267,9 @@ static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int>
 
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
   switch (k32) {
+    case 32:   // 1024-bit primes of key generation: L = 9 (4 lanes) or 18
+      return pick_group(a.count, (int)a.group, {2, 4}, 4) == 2 ? launch_modexp<36, 2, 32>(a, st)
+                                                              : launch_modexp<36, 4, 32>(a, st);
     case 64:
       switch (pick_group(a.count, (int)a.group, {2, 4, 8}, 4)) {
         case 8: return launch_modexp<72, 8, 64>(a, st);

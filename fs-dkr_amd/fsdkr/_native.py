@@ -124,6 +124,8 @@ def lib():
     L.fsdkr_ctx_set_timing.restype = ctypes.c_int
     L.fsdkr_mod_inverse.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p]
     L.fsdkr_mod_inverse.restype = ctypes.c_int
+    L.fsdkr_miller_rabin.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
+    L.fsdkr_miller_rabin.restype = ctypes.c_int
     L.fsdkr_ec_msm.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
     L.fsdkr_ec_msm.restype = ctypes.c_int
     L.fsdkr_fixed_base_modexp.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, ctypes.c_uint32,
@@ -253,6 +255,17 @@ class Context:
         U = np.zeros(count, dtype=np.uint32)
         self.check(self._lib.fsdkr_mod_inverse(self._h, mod_limbs, count, _ptr(Y), _ptr(M), _ptr(O), _ptr(U)))
         return [v if u else None for v, u in zip(limbs_to_ints(O), U.tolist())]
+
+    def miller_rabin(self, cands, bases, mod_limbs):
+        """[1 if cands[i] is a strong probable prime to base bases[i] else 0] on the GPU."""
+        count = len(cands)
+        if count == 0:
+            return []
+        C = ints_to_limbs(cands, mod_limbs)
+        B = ints_to_limbs(bases, mod_limbs)
+        V = np.zeros(count, dtype=np.uint32)
+        self.check(self._lib.fsdkr_miller_rabin(self._h, mod_limbs, count, _ptr(C), _ptr(B), _ptr(V)))
+        return V.tolist()
 
     # ---- collect() verification -------------------------------------------
     def verify_collect(self, batch):

@@ -7,8 +7,8 @@ Every exponentiation runs on the GPU in a few batched launches:
            commitments h1^x h2^rho, h1^alpha h2^gamma mod N~ and beta^N mod N^2
            (fsdkr_modexp_batch); G*share, G*a_k, G*alpha (fsdkr_ec_msm)
   round 2  r^e mod N for the PDL s2 and Alice s responses (after the challenges)
-  keys     Paillier / ring-Pedersen moduli by a GPU Fermat search
-           (zk_paillier-style prime walk), correct-key sigma_j = rho_j^(N^-1 mod phi),
+  keys     Paillier / ring-Pedersen moduli by the batched GPU Miller-Rabin prime
+           walk (fsdkr/keygen.py), correct-key sigma_j = rho_j^(N^-1 mod phi),
            ring-Pedersen A_i = T^a_i through the fixed-base engine.
 Hashes, small-number arithmetic and the order of random draws are host work.
 
@@ -28,8 +28,6 @@ from .refresh import GX, GY, Q, FsDkrError, FsDkrPanic, _ctx
 from .types import (AliceProof, DecryptionKey, EncryptionKey, NiCorrectKeyProof, PDLwSlackProof, RefreshMessage,
                     RingPedersenProof, RingPedersenStatement, VerifiableSS)
 
-SALT = bytes([75, 90, 101, 110])    # zk-paillier SALT_STRING [dep, unverified]
-M2 = 11                             # NiCorrectKeyProof sigma_vec length
 
 
 class SystemRng:
@@ -89,73 +87,15 @@ def _from_modulo(rng, n):
 
 
 # ---------------------------------------------------------- key generation ----
-_SMALL = None
-
-
-def _small_primorial():
-    global _SMALL
-    if _SMALL is None:
-        n = 2000
-        flags = bytearray([1]) * n
-        flags[0:2] = b"\x00\x00"
-        for i in range(2, int(n ** 0.5) + 1):
-            if flags[i]:
-                flags[i * i::i] = bytearray(len(flags[i * i::i]))
-        _SMALL = math.prod(i for i in range(3, n) if flags[i])
-    return _SMALL
-
-
-def prime(ctx, rng, bits):
-    """A `bits`-bit prime with the top two bits set: a random start, then the
-    first probable prime among the next 4*bits odd numbers (else redraw).
-    Candidates are sieved on the host and Fermat-tested to bases 2, 3 and 5 in
-    one GPU launch per base (a composite passing all three is a ~2^-100 event
-    at these sizes)."""
-    prim = _small_primorial()
-    w = _width(bits)
-    while True:
-        c = rng.bits(bits) | (3 << (bits - 2)) | 1
-        cands = [c + 2 * k for k in range(4 * bits)]
-        surv = [x for x in cands if math.gcd(x, prim) == 1]
-        for base in (2, 3, 5):
-            if not surv:
-                break
-            r = ctx.modexp_batch([base] * len(surv), [x - 1 for x in surv], surv, list(range(len(surv))), w)
-            surv = [x for x, v in zip(surv, r) if v == 1]
-        if surv:
-            return surv[0]
-
-
-def keypair_with_modulus_size(ctx, rng, bits):
-    """Paillier::keypair_with_modulus_size (refresh_message.rs:118)."""
-    while True:
-        p = prime(ctx, rng, bits // 2)
-        q = prime(ctx, rng, bits // 2)
-        if p != q:
-            n = p * q
-            return EncryptionKey(n, n * n), DecryptionKey(p, q)
-
-
-def correct_key_rho(n):
-    """zk-paillier NiCorrectKeyProof rho_j = mask_generation(|n|, H(n, salt, j)) mod n [dep]."""
-    salt = int.from_bytes(SALT, "big")
-    klen = n.bit_length()
-    out = []
-    for j in range(M2):
-        seed = chain_bigint(n, salt, j)
-        msk = sum(chain_bigint(seed, k) << (256 * k) for k in range(klen // 256 + 1))
-        out.append(msk % n)
-    return out
+# Paillier keys, primes and correct-key proofs come from the batched key
+# generation (fsdkr/keygen.py: GPU Miller-Rabin over the oracle's prime walk).
+from .keygen import correct_key_rho, keypair_with_modulus_size, prime  # noqa: E402,F401
+from .keygen import correct_key_proofs  # noqa: E402
 
 
 def correct_key_proof(ctx, dk):
     """NiCorrectKeyProof::proof (refresh_message.rs:119): sigma_j = rho_j^(n^-1 mod phi) mod n."""
-    n = dk.p * dk.q
-    phi = (dk.p - 1) * (dk.q - 1)
-    d = pow(n, -1, phi)
-    rho = correct_key_rho(n)
-    sig = ctx.modexp_batch(rho, [d] * M2, [n], [0] * M2, _width(n.bit_length()))
-    return NiCorrectKeyProof(tuple(sig))
+    return correct_key_proofs(ctx, [dk])[0]
 
 
 def ring_pedersen_generate_and_prove(ctx, rng, key_bits, M):

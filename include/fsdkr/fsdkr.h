@@ -88,6 +88,19 @@ int fsdkr_modexp_batch_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count
                               const uint32_t* d_mod_idx, const uint32_t* d_mods, uint32_t n_mod,
                               uint32_t* d_out);
 
+/* ---- Key generation: batched Miller–Rabin -------------------
+ * verdict[i] = 1 iff cand[i] is a strong probable prime to base bases[i]:
+ * with cand - 1 = d 2^s, b^d == 1 or b^(d 2^j) == cand - 1 for some j < s
+ * (mod cand).  cand: [count][mod_limbs], odd and >= 5; bases: [count][mod_limbs]
+ * (any value; 2 <= b <= cand - 2 for a meaningful round).  mod_limbs in
+ * {32, 64, 96} (1024/2048/3072-bit candidates).  Replaces the primality test
+ * inside kzen-paillier 0.4.3 Paillier::keypair_with_modulus_size, called at
+ * refresh_message.rs:118 (distribute), ring_pedersen_proof.rs:50
+ * (RingPedersenStatement::generate) and add_party_message.rs:51
+ * (generate_h1_h2_n_tilde).  fsdkr.keygen drives the prime walk above it. */
+int fsdkr_miller_rabin(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* cand,
+                       const uint32_t* bases, uint32_t* verdict);
+
 
 /* ---- Job 2: batched verification of RefreshMessage::collect ----------------
  * One call verifies every proof collect() checks (refresh_message.rs:321-437):

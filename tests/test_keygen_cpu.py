@@ -1,0 +1,80 @@
+"""Key generation on the CPU: the oracle's restated prime walk
+is pinned to Rng.prime (the walk every oracle key and golden fixture was made
+with), Miller-Rabin to known strong pseudoprimes, and the product's host
+pieces (sieve, witness bases, batched walk schedule) to the oracle."""
+import pytest
+
+from oracle import keygen as ok
+from oracle import bigint
+from oracle.rng import Rng
+
+
+@pytest.mark.parametrize("bits", [128, 256, 512])
+def test_oracle_walk_is_rng_prime(bits):
+    for s in range(3):
+        assert ok.sample_primes(Rng(("kg", bits, s)), bits, 1)[0] == Rng(("kg", bits, s)).prime(bits)
+
+
+def test_oracle_batch_is_sequential_walks():
+    rng = Rng("batch")
+    got = ok.sample_primes(rng, 256, 6)
+    rng2 = Rng("batch")
+    starts = [rng2.bits(256) | (3 << 254) | 1 for _ in range(6)]
+    assert got == [ok.walk(s, 4 * 256) for s in starts]
+    assert all(bigint.is_probable_prime(p) for p in got)
+
+
+# strong pseudoprimes (the smallest to the listed bases) and Carmichael numbers
+SPSP = [(2047, (2,), 3), (1373653, (2, 3), 5), (25326001, (2, 3, 5), 7), (3215031751, (2, 3, 5, 7), 11),
+        (2152302898747, (2, 3, 5, 7, 11), 13)]
+
+
+@pytest.mark.parametrize("n,liars,witness", SPSP)
+def test_strong_pseudoprimes(n, liars, witness):
+    assert all(ok.strong_probable_prime(n, b) for b in liars)
+    assert not ok.strong_probable_prime(n, witness)
+    assert not ok.is_probable_prime(n)
+
+
+def test_carmichael_and_primes():
+    for n in (561, 41041, 825265, 321197185):
+        assert not ok.strong_probable_prime(n, 2) or not ok.is_probable_prime(n)
+    for p in ((1 << 521) - 1, (1 << 607) - 1, 2 ** 127 - 1):
+        assert ok.is_probable_prime(p)
+        assert all(ok.strong_probable_prime(p, b) for b in (2, 3, p - 1, 1))
+    assert not ok.is_probable_prime(((1 << 521) - 1) * ((1 << 127) - 1))
+
+
+def test_product_sieve_matches_trial_division():
+    from fsdkr import keygen
+    for s in range(3):
+        st = Rng(("sv", s)).bits(1024) | 1 | (3 << 1022)
+        got = set(keygen.sieve(st, 2048).tolist())
+        want = {i for i in range(2048) if all((st + 2 * i) % p for p in ok.SMALL_PRIMES)}
+        assert got == want
+
+
+def test_product_witness_bases_match_oracle():
+    from fsdkr import keygen
+    for c in ((1 << 521) - 1, Rng("w").prime(512), 2047 * 89 + 2):
+        assert keygen.witness_bases(c) == ok.witness_bases(c)
+        assert all(2 <= b <= c - 2 for b in keygen.witness_bases(c))
+
+
+class _CpuMr:
+    """Host-logic harness: answers fsdkr_miller_rabin with the oracle so the
+    batched walk schedule (windows, passers, redraw passes) is checked without
+    a GPU.  Test infrastructure only; the GPU test runs the real kernel."""
+
+    def miller_rabin(self, cands, bases, mod_limbs):
+        assert all(c.bit_length() <= 32 * mod_limbs for c in cands)
+        return [1 if ok.strong_probable_prime(c, b) else 0 for c, b in zip(cands, bases)]
+
+
+@pytest.mark.parametrize("span,window", [(0, 0), (24, 4), (8, 3)])
+def test_product_walk_schedule_matches_oracle(span, window):
+    """Short walks (span 8/24) fail often, exercising the redraw passes."""
+    from fsdkr import keygen
+    got = keygen.sample_primes(_CpuMr(), Rng(("sched", span)), 192, 10, window=window or None, span=span or None)
+    want = ok.sample_primes(Rng(("sched", span)), 192, 10, span=span)
+    assert got == want
