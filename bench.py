@@ -146,6 +146,33 @@ def cpu_baseline_python(msgs, joins, lk, n_pairs):
                       f"1 correct-key; extrapolated to the n={n} proof mix (C++ baseline not built)"}
 
 
+def keygen_bench(ctx, count=64, bits=2048, seed=77):
+    """`count` Paillier keypairs + NiCorrectKeyProof in one batched
+    call (fsdkr.keygen.refresh_keys: GPU Miller-Rabin prime walks, one modexp
+    launch for the proofs), and one keypair alone (the distribute() path)."""
+    import random
+    from fsdkr import keygen
+
+    class _Seeded:   # synthetic draws (bench only); production uses the OS RNG
+        def __init__(self, s):
+            self.r = random.Random(s)
+
+        def bits(self, k):
+            return self.r.getrandbits(k)
+
+    keygen.refresh_keys(ctx, _Seeded(seed), bits, 2)   # warm-up
+    t0 = time.perf_counter()
+    keys = keygen.refresh_keys(ctx, _Seeded(seed + 1), bits, count)
+    batch_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    keygen.keypair_with_modulus_size(ctx, _Seeded(seed + 2), bits)
+    single_s = time.perf_counter() - t0
+    assert all(ek.n.bit_length() == bits for ek, _, _ in keys)
+    return {"bits": bits, "keys": count, "keys_per_s": count / batch_s, "batch_ms": batch_s * 1e3,
+            "single_keypair_ms": single_s * 1e3,
+            "what": "keypairs + correct-key proofs per batched call; single = one keypair (distribute path)"}
+
+
 def modexp_roofline(ctx, count, reps, seed=1234):
     """The dominant kernel on the metric-2 shape: base^N mod N^2, N 2048-bit."""
     import random
@@ -290,6 +317,8 @@ def main():
                          "still checks every pair)")
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="analysis only: run rank 0's slice of a W-way shard on one GPU and report its step time")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="with --emulate-shard: idle gap before each timed whole-call step (profiling)")
     a = ap.parse_args()
 
     import torch
@@ -342,17 +371,25 @@ def main():
                 return 0
 
             def all_reduce(self, t, op=None):
-                t.fill_(1)
+                # every other rank's slice all-valid: feldman 1, pdl 7 (u1|u2|u3), range 1, ped 1, ck 1, dlog 3
+                P, M = R * n, R + J
+                for lo, hi, ok in ((0, P, 1), (P, 2 * P, 7), (2 * P, 3 * P, 1), (3 * P, 3 * P + 2 * M, 1),
+                                   (3 * P + 2 * M, 3 * P + 2 * M + J, 3)):
+                    t[lo:hi] = ok
 
         keys = [copy.deepcopy(lk) for _ in range(a.warmup + a.steps)]
         for k in range(a.warmup):
             shard.collect(_Rank0(), msgs, keys[k], new_dk, joins, ctx, key_bits=a.key_bits)
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        tot = 0.0
         for k in range(a.steps):
+            if a.gap_ms:   # idle gap between steps so a kernel trace can be cut per step
+                time.sleep(a.gap_ms * 1e-3)
+            t0 = time.perf_counter()
             shard.collect(_Rank0(), msgs, keys[a.warmup + k], new_dk, joins, ctx, key_bits=a.key_bits)
-        torch.cuda.synchronize()
-        full_ms = (time.perf_counter() - t0) / a.steps * 1e3
+            torch.cuda.synchronize()
+            tot += time.perf_counter() - t0
+        full_ms = tot / a.steps * 1e3
         print(json.dumps({"emulated_shard": a.emulate_shard, "refresh_slice": [r0, r1], "join_slice": [j0, j1],
                           "device_ms_per_step": dev_ms, "rank0_collect_ms_per_step": full_ms}), flush=True)
         return
@@ -399,6 +436,7 @@ def main():
             cpu = cpu_baseline_python(msgs, joins, lk, 200)
             cpu["cpp_unavailable"] = str(e)
     s4 = sessions_bench(ctx, a.sessions, a.session_steps, a.seed + 4) if a.sessions and world == 1 else None
+    kg = keygen_bench(ctx) if world == 1 else None
     W_collect = collect_work(R, J, n)
     traffic, traffic_src = pmc_traffic(roof["count"])
     out = {
@@ -436,6 +474,7 @@ def main():
                                "device_pipeline_frac_of_peak": W_collect / (ph["device_pipeline_ms"] * 1e-3) /
                                PEAK_MAC},
         "config4_sessions": s4,
+        "keygen": kg,
         "workload_gen_s": gen_s,
         "cpu_baseline": cpu,
     }

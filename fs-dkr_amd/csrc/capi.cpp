@@ -68,8 +68,10 @@ uint8_t* Ctx::host_arena(size_t bytes) {
   return pinned;
 }
 
+static hipStream_t make_stream(const Ctx* c, int masked);
+
 hipStream_t Ctx::aux_stream() {
-  if (!aux && hipStreamCreateWithFlags(&aux, hipStreamNonBlocking) != hipSuccess) aux = nullptr;
+  if (!aux) aux = make_stream(this, ga_cus ? 4 : 0);
   return aux ? aux : stream;
 }
 
@@ -105,28 +107,29 @@ void Ctx::tend(size_t idx, hipStream_t st) {
   pending[idx].e1 = ev;
 }
 
-std::vector<uint32_t> Ctx::cu_mask(bool reserved) const {
+std::vector<uint32_t> Ctx::cu_mask(uint32_t count, bool in) const {
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   if (ncu <= 0) ncu = 256;
   std::vector<uint32_t> m((ncu + 31) / 32, 0u);
   std::vector<bool> res(ncu, false);
-  // R/8 CUs per XCD.  Bit i = 32 j + (j + s (32/per)) mod 32 is balanced over the 8
-  // XCDs whether the driver maps mask bits to XCDs contiguously (i / 32) or
+  // count/8 CUs per XCD.  Bit i = 32 j + (j + s (32/per)) mod 32 is balanced over the
+  // 8 XCDs whether the driver maps mask bits to XCDs contiguously (i / 32) or
   // interleaved (i mod 8).
-  const uint32_t per = reserve_cus / 8;
+  const uint32_t per = count / 8;
   if (ncu == 256 && per)
     for (uint32_t j = 0; j < 8; ++j)
-      for (uint32_t s = 0; s < per; ++s) res[32 * j + (j + s * (32 / per)) % 32] = true;
+      for (uint32_t s = 0; s < per; ++s) res[32 * j + (j + (s * 32) / per) % 32] = true;
   for (int i = 0; i < ncu; ++i)
-    if (res[i] == reserved) m[i / 32] |= 1u << (i % 32);
+    if (res[i] == in) m[i / 32] |= 1u << (i % 32);
   return m;
 }
 
-static hipStream_t make_stream(const Ctx* c, int masked /* 0 none, 1 reserved, 2 complement */) {
+// masked: 0 none, 1 reserved CUs, 2 their complement, 3 the GA set, 4 its complement
+static hipStream_t make_stream(const Ctx* c, int masked) {
   hipStream_t s = nullptr;
   if (masked) {
-    std::vector<uint32_t> m = c->cu_mask(masked == 1);
+    std::vector<uint32_t> m = masked <= 2 ? c->cu_mask(c->reserve_cus, masked == 1) : c->cu_mask(c->ga_cus, masked == 3);
     if (hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()) == hipSuccess) return s;
     s = nullptr;
   }
@@ -136,7 +139,7 @@ static hipStream_t make_stream(const Ctx* c, int masked /* 0 none, 1 reserved, 2
 
 hipStream_t Ctx::side_stream(int k) {
   k %= NSIDE;
-  if (!side[k]) side[k] = make_stream(this, (reserve_cus && reserve_excl) ? 2 : 0);
+  if (!side[k]) side[k] = make_stream(this, ga_cus ? (k == 0 ? 3 : 4) : (reserve_cus && reserve_excl) ? 2 : 0);
   return side[k] ? side[k] : stream;
 }
 
@@ -355,7 +358,11 @@ int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out) {
     c->reserve_cus = (r > 0 && r % 8 == 0 && r <= 128) ? (uint32_t)r : 0u;
   }
   if (const char* e = getenv("FSDKR_RESERVE_EXCL")) c->reserve_excl = atoi(e) != 0;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (const char* e = getenv("FSDKR_GA_CUS")) {
+    const int r = atoi(e);
+    c->ga_cus = (r > 0 && r % 8 == 0 && r <= 224 && !c->reserve_cus) ? (uint32_t)r : 0u;
+  }
+  if (!(c->stream = make_stream(c, c->ga_cus ? 4 : 0))) {
     delete c;
     return FSDKR_E_HIP;
   }
@@ -389,6 +396,33 @@ int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
   if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32)) return FSDKR_E_ARG;
   c->modexp_group = lanes;
+  return FSDKR_OK;
+}
+
+int fsdkr_ctx_set_cu_split(fsdkr_ctx* ctx, uint32_t ga_cus) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c || (ga_cus && (ga_cus % 8 != 0 || ga_cus > 224))) return FSDKR_E_ARG;
+  if (c->ga_cus == ga_cus) return FSDKR_OK;
+  int rc = c->sync();
+  if (rc) return rc;
+  if (c->reserve_cus) {
+    c->fail("fsdkr_ctx_set_cu_split: FSDKR_RESERVE_CUS is set");
+    return FSDKR_E_ARG;
+  }
+  // every stream is re-created lazily with the new masks
+  if ((rc = c->hip_check(hipDeviceSynchronize(), "sync"))) return rc;
+  for (auto& sd : c->side)
+    if (sd) {
+      (void)hipStreamDestroy(sd);
+      sd = nullptr;
+    }
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  c->aux = nullptr;
+  c->ga_cus = ga_cus;
+  hipStream_t s = make_stream(c, ga_cus ? 4 : 0);
+  if (!s) return FSDKR_E_HIP;
+  (void)hipStreamDestroy(c->stream);
+  c->stream = s;
   return FSDKR_OK;
 }
 

@@ -402,6 +402,24 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   return FSDKR_OK;
 }
 
+// GA lanes per instance: GA shares the chip with the other streams, so it takes
+// the largest group that keeps it within about half the resident lanes
+// (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
+// (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants) for latency.
+// FSDKR_COLLECT_GA_G overrides.  Used by the prestart and by launch().
+static uint32_t ga_lanes(uint32_t count, uint32_t nn) {
+  static const uint32_t forced = [] {
+    const char* e = getenv("FSDKR_COLLECT_GA_G");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  uint32_t g = 8;
+  for (uint32_t x : {16u, kWideGroup})
+    if ((uint64_t)count * x <= 65536u) g = x;
+  if (forced) g = forced;
+  if (g == kWideGroup && nn != 128) g = 16;
+  return g;
+}
+
 static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
   if (!c->ga_pre) c->ga_pre = new GaPre();
   GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
@@ -464,14 +482,19 @@ static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
   if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, gs), "prestart H2D")) ||
       (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // img is pageable and local
     return rc;
+  // the lanes launch() would give GA: 32 lanes (KD = 160 constants) for the small
+  // batches of a multi-GPU shard, where GA's chain latency is the critical path
+  const uint32_t group = ga_lanes(2 * P, nn);
   uint32_t* cons = nullptr;
-  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons, "collect_ga_nn"))) return rc;
+  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
+                         group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
+    return rc;
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
   // issue priority 3 (FSDKR_PRE_GA_PRIO; 2 measured 1-2 ms slower per call,
   // profiles/r02x_ab_full.jsonl)
   const char* gpe = getenv("FSDKR_PRE_GA_PRIO");
   const uint32_t ga_prio = gpe ? (uint32_t)atoi(gpe) : 3u;
-  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, 8)))
+  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, group)))
     return rc;
   if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
@@ -1364,21 +1387,13 @@ static int collect_launch_impl(Ctx* c) {
   // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
   // (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants) for latency.
   // FSDKR_COLLECT_GA_G overrides.
-  const uint32_t ga_forced = [] {
-    const char* e = getenv("FSDKR_COLLECT_GA_G");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
   // J2 / J5 (256-bit challenge exponents) lanes per instance: FSDKR_COLLECT_J2_G / _J5_G
   auto env_group = [](const char* k, uint32_t dflt) -> uint32_t {
     const char* e = getenv(k);
     return e ? (uint32_t)atoi(e) : dflt;
   };
   const uint32_t j2_group = env_group("FSDKR_COLLECT_J2_G", 8), j5_group = env_group("FSDKR_COLLECT_J5_G", 8);
-  uint32_t ga_group = 8;
-  for (uint32_t g : {16u, kWideGroup})
-    if ((uint64_t)pl.jcount[0] * g <= 65536u) ga_group = g;
-  if (ga_forced) ga_group = ga_forced;
-  if (ga_group == kWideGroup && nn != 128) ga_group = 16;
+  const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;
   if (ga_group == kWideGroup && pl.jcount[0] &&
       (rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup)))

@@ -70,10 +70,15 @@ struct Ctx {
   // 0 = no reservation (crit_stream() returns nullptr: run on the caller's stream).
   uint32_t reserve_cus = 0;
   bool reserve_excl = true;   // side streams on the complement (false: unmasked)
+  // GA split (FSDKR_GA_CUS = G, a multiple of 8): side stream 0 (GA, the s^N mod
+  // N^2 chains) runs on G CUs spread over the XCDs, every other stream (main,
+  // side, recovery) on the complement, so the longest dependent chains of a
+  // small (sharded) batch never share a SIMD with the throughput jobs.
+  uint32_t ga_cus = 0;
   hipStream_t crit = nullptr;
   hipStream_t crit_stream();
-  // CU mask words of the reserved set (reserved = true) or of its complement
-  std::vector<uint32_t> cu_mask(bool reserved) const;
+  // CU mask words of a balanced set of `count` CUs (in = true) or of its complement
+  std::vector<uint32_t> cu_mask(uint32_t count, bool in) const;
   // synchronise the stream and fold pending events into `times`
   int sync();
 };

@@ -121,6 +121,8 @@ def lib():
     L.fsdkr_ctx_set_modexp_group.argtypes = [vp, ctypes.c_uint32]
     L.fsdkr_ctx_set_modexp_group.restype = ctypes.c_int
     L.fsdkr_ctx_set_timing.argtypes = [vp, ctypes.c_int]
+    L.fsdkr_ctx_set_cu_split.argtypes = [vp, ctypes.c_uint32]
+    L.fsdkr_ctx_set_cu_split.restype = ctypes.c_int
     L.fsdkr_ctx_set_timing.restype = ctypes.c_int
     L.fsdkr_mod_inverse.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p]
     L.fsdkr_mod_inverse.restype = ctypes.c_int
@@ -239,6 +241,10 @@ class Context:
     def set_modexp_group(self, lanes):
         """Force the lanes per modexp instance (0 = automatic)."""
         self.check(self._lib.fsdkr_ctx_set_modexp_group(self._h, lanes))
+
+    def set_cu_split(self, ga_cus):
+        """Multi-GPU shards: GA chains on `ga_cus` CUs, everything else on the rest (0 = off)."""
+        self.check(self._lib.fsdkr_ctx_set_cu_split(self._h, ga_cus))
 
     def set_timing(self, on):
         """Per-kernel HIP-event timing on/off (kernel_time needs it on)."""

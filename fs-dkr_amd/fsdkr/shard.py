@@ -16,6 +16,10 @@ import numpy as np
 from .batch import CollectBatch, Verdicts
 
 
+GA_SPLIT_CUS = 160
+GA_SPLIT_MAX_CHAINS = 1024
+
+
 def shard_range(count, world, rank):
     """Contiguous [lo, hi) slice of `count` units for `rank` of `world`."""
     return rank * count // world, (rank + 1) * count // world
@@ -85,6 +89,12 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
     j0, j1 = shard_range(J, world, rank)
     if r1 == r0 and j1 == j0:
         return None, None
+    # a slice whose s^N mod N^2 chains (2 per pair) leave most of the chip idle is
+    # latency-bound on them: they get 160 CUs of their own, every other stream the
+    # remaining 96 (8-way shard of n=64: 29.4 -> 22.5 ms per rank; no gain at 2-
+    # and 4-way shards, profiles/r02zd_ga_lanes_cus_ab.jsonl)
+    if hasattr(ctx, "set_cu_split"):
+        ctx.set_cu_split(GA_SPLIT_CUS if 2 * (r1 - r0) * n <= GA_SPLIT_MAX_CHAINS else 0)
     b = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], m_security, key_bits, n_recv=n, staged=True)
     if b.header_only:   # an empty refresh slice (joins only) or a size failure the header batch reports
         return None, None

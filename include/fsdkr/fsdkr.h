@@ -56,6 +56,14 @@ int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes);
  * creation.  The events cost ~9 ms per n = 64 collect (eight streams, one
  * event pair per launch), so timed benchmark regions run with it off. */
 int fsdkr_ctx_set_timing(fsdkr_ctx* ctx, int on);
+
+/* Multi-GPU shards: run the s^N mod N^2 chains (GA, the longest dependent
+ * chains of collect()) on `ga_cus` CUs spread over the 8 XCDs and every other
+ * stream on the complement, so a rank's small batch keeps its critical chains
+ * off the SIMDs of the throughput jobs (0 = no split, the single-GPU default).
+ * A multiple of 8, at most 224.  Waits for outstanding work, re-creates the
+ * context's streams.  Performance setting only: results are unchanged. */
+int fsdkr_ctx_set_cu_split(fsdkr_ctx* ctx, uint32_t ga_cus);
 /* 1 if the shared library was built with gfx950 kernels and a device is present. */
 int fsdkr_device_available(void);
 

@@ -173,3 +173,30 @@ def test_sharded_collect_two_emulated_ranks(gpu_ctx, tamper):
     for r in range(2):
         assert res[r][0] == want, (r, res[r][0], want)
         assert res[r][1] == summary(single)
+
+
+@pytest.mark.gpu
+def test_cu_split_keeps_verdicts(gpu_ctx):
+    """fsdkr_ctx_set_cu_split (GA chains on their own CUs, used by shard slices)
+    is a performance setting: the same batch gives the same verdicts with and
+    without it; bad CU counts are rejected."""
+    from fsdkr._native import FsdkrError
+    from fsdkr.batch import CollectBatch
+    raw, cls, d = _fixture()
+    kb = raw["meta"]["key_bits"]
+    msgs = copy.deepcopy(d["msgs"])
+    p = msgs[2].pdl_proof_vec[0]
+    msgs[2].pdl_proof_vec[0] = dataclasses.replace(p, u3=p.u3 + 1)
+    b = CollectBatch(msgs, d["keys"][0], [], 256, kb)
+    base = gpu_ctx.verify_collect(b)
+    try:
+        for cus in (160, 64, 0):
+            gpu_ctx.set_cu_split(cus)
+            v = gpu_ctx.verify_collect(b)
+            for f in ("feldman", "pdl", "range", "ped", "ck"):
+                assert np.array_equal(getattr(base, f), getattr(v, f)), (cus, f)
+        for bad in (12, 232):
+            with pytest.raises(FsdkrError):
+                gpu_ctx.set_cu_split(bad)
+    finally:
+        gpu_ctx.set_cu_split(0)
