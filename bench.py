@@ -426,6 +426,7 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
+    ctx.set_cu_split(0)   # a shard slice may have split the CUs; the single-GPU figures below use the whole chip
     batch, verd, ph = phases(ctx, msgs, lk, joins, a.key_bits)
     roof = modexp_roofline(ctx, a.modexp_count, 3)
     cpu = None

@@ -235,7 +235,12 @@ void free_collect_plan(Ctx* c) {
 struct GaPre {
   bool valid = false;
   uint32_t nl = 0, n = 0, R = 0;
-  std::vector<uint32_t> recv_n, s2, s;   // the inputs, for the match in prepare
+  std::vector<uint32_t> recv_n, s2, s;   // the inputs (each session at its own nl), for the match in prepare
+  struct Sess {
+    uint32_t nl, n, R;
+    size_t rbase, pbase;   // first global receiver / pair of the session
+  };
+  std::vector<Sess> sess;
   uint32_t* out = nullptr;               // [2P][nn]: J1 instance order (s2^N rows, then s^N rows)
   hipEvent_t done = nullptr;
   // the fixed-base tables of h1_i, h2_i (bases 2i, 2i+1 of prepare's FbJob), built
@@ -420,29 +425,53 @@ static uint32_t ga_lanes(uint32_t count, uint32_t nn) {
   return g;
 }
 
-static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
+// GA prestart of `count` sessions (one: fsdkr_collect_prestart; many:
+// fsdkr_collect_prestart_multi), in prepare's global order: session s's
+// receivers and pairs after session s-1's, every row at the widest nl.
+static int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t* n_out, uint32_t* P_out) {
   if (!c->ga_pre) c->ga_pre = new GaPre();
   GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
   g.valid = false;
   g.fb_valid = false;
+  *n_out = *P_out = 0;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
   if (running && running->launched) {
     c->fail("fsdkr_collect_prestart: a batch is in flight (call finish first)");
     return FSDKR_E_ARG;
   }
-  if (!b || !(b->nl == 64 || b->nl == 96) || !b->recv_n || !b->pdl_s2 || !b->rp_s) {
-    c->fail("fsdkr_collect_prestart: needs nl, recv_n, pdl_s2 and rp_s");
+  if (!bs || count == 0) {
+    c->fail("fsdkr_collect_prestart: no batch");
     return FSDKR_E_ARG;
   }
-  const uint32_t nl = b->nl, nn = 2 * nl, R = b->n_refresh;
-  const uint32_t n = b->n_recv ? b->n_recv : R + b->n_join;
-  const uint32_t P = R * n;
-  if (P == 0 || n < R) return FSDKR_OK;   // nothing to start (prepare reports bad shapes)
-  for (uint32_t i = 0; i < n; ++i)
-    if (!is_odd(b->recv_n + (size_t)i * nl)) return FSDKR_OK;   // prepare reports it
-  g.recv_n.assign(b->recv_n, b->recv_n + (size_t)n * nl);
-  g.s2.assign(b->pdl_s2, b->pdl_s2 + (size_t)P * nl);
-  g.s.assign(b->rp_s, b->rp_s + (size_t)P * nl);
+  uint32_t nl = 0, n = 0, P = 0;
+  std::vector<GaPre::Sess> ss(count);
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (!(b->nl == 64 || b->nl == 96) || !b->recv_n || !b->pdl_s2 || !b->rp_s) {
+      c->fail("fsdkr_collect_prestart: session %u needs nl, recv_n, pdl_s2 and rp_s", k);
+      return FSDKR_E_ARG;
+    }
+    const uint32_t R = b->n_refresh, ns = b->n_recv ? b->n_recv : R + b->n_join;
+    if (R == 0 || ns < R) return FSDKR_OK;   // nothing to start (prepare reports bad shapes)
+    for (uint32_t i = 0; i < ns; ++i)
+      if (!is_odd(b->recv_n + (size_t)i * b->nl)) return FSDKR_OK;   // prepare reports it
+    ss[k] = GaPre::Sess{b->nl, ns, R, (size_t)n, (size_t)P};
+    nl = std::max(nl, b->nl);
+    n += ns;
+    P += R * ns;
+  }
+  const uint32_t nn = 2 * nl;
+  // the inputs, at each session's own width, for the match in prepare
+  g.recv_n.clear();
+  g.s2.clear();
+  g.s.clear();
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const GaPre::Sess& x = ss[k];
+    g.recv_n.insert(g.recv_n.end(), b->recv_n, b->recv_n + (size_t)x.n * x.nl);
+    g.s2.insert(g.s2.end(), b->pdl_s2, b->pdl_s2 + (size_t)x.R * x.n * x.nl);
+    g.s.insert(g.s.end(), b->rp_s, b->rp_s + (size_t)x.R * x.n * x.nl);
+  }
   // image: [N^2 | N | s2 | s | descriptors], outputs after it
   auto al = Img::al;
   const size_t o_NN = 0, o_rn = al((size_t)n * nn * 4), o_s2 = o_rn + al((size_t)n * nl * 4),
@@ -455,23 +484,48 @@ static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
     return FSDKR_E_OOM;
   }
   std::vector<uint8_t> img(o_out, 0);
+  uint32_t* NN = reinterpret_cast<uint32_t*>(img.data() + o_NN);
+  uint32_t* RN = reinterpret_cast<uint32_t*>(img.data() + o_rn);
+  uint32_t* S2 = reinterpret_cast<uint32_t*>(img.data() + o_s2);
+  uint32_t* S1 = reinterpret_cast<uint32_t*>(img.data() + o_s);
+  std::vector<uint32_t> rbits(n);
+  std::vector<uint32_t> sess_of_recv(n);
+  for (uint32_t k = 0; k < count; ++k) std::fill(sess_of_recv.begin() + ss[k].rbase, sess_of_recv.begin() + ss[k].rbase + ss[k].n, k);
+  parallel_for(n, 64, [&](size_t r0, size_t r1) {
+    for (size_t r = r0; r < r1; ++r) {
+      const GaPre::Sess& x = ss[sess_of_recv[r]];
+      const uint32_t* Np = bs[sess_of_recv[r]].recv_n + (r - x.rbase) * x.nl;
+      const hbn::Limbs N = hbn::from(Np, x.nl);
+      hbn::store(hbn::mul(N, N), NN + r * nn, nn);
+      memcpy(RN + r * nl, Np, (size_t)x.nl * 4);
+      rbits[r] = hbn::bitlen(Np, x.nl);
+    }
+  });
   uint32_t recvn_max = 1;
-  for (uint32_t r = 0; r < n; ++r) {
-    const uint32_t* Np = b->recv_n + (size_t)r * nl;
-    const hbn::Limbs N = hbn::from(Np, nl);
-    hbn::store(hbn::mul(N, N), reinterpret_cast<uint32_t*>(img.data() + o_NN) + (size_t)r * nn, nn);
-    recvn_max = std::max(recvn_max, hbn::bitlen(Np, nl));
+  for (uint32_t r = 0; r < n; ++r) recvn_max = std::max(recvn_max, rbits[r]);
+  for (uint32_t k = 0; k < count; ++k) {   // pair rows, zero-extended to nl
+    const GaPre::Sess& x = ss[k];
+    const size_t cnt = (size_t)x.R * x.n;
+    if (x.nl == nl) {
+      memcpy(S2 + x.pbase * nl, bs[k].pdl_s2, cnt * nl * 4);
+      memcpy(S1 + x.pbase * nl, bs[k].rp_s, cnt * nl * 4);
+    } else {
+      for (size_t q = 0; q < cnt; ++q) {
+        memcpy(S2 + (x.pbase + q) * nl, bs[k].pdl_s2 + q * x.nl, (size_t)x.nl * 4);
+        memcpy(S1 + (x.pbase + q) * nl, bs[k].rp_s + q * x.nl, (size_t)x.nl * 4);
+      }
+    }
   }
-  memcpy(img.data() + o_rn, b->recv_n, (size_t)n * nl * 4);
-  memcpy(img.data() + o_s2, b->pdl_s2, (size_t)P * nl * 4);
-  memcpy(img.data() + o_s, b->rp_s, (size_t)P * nl * 4);
   auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
   ModexpJob J1;
   J1.k32 = nn;
   for (int which = 0; which < 2; ++which)   // the order prepare's J1 uses
-    for (uint32_t p = 0; p < P; ++p) {
-      const uint32_t r = p % n;
-      J1.add(DI((which == 0 ? o_s2 : o_s) + (size_t)p * nl * 4), nl, DI(o_rn + (size_t)r * nl * 4), nl, recvn_max, r);
+    for (uint32_t k = 0; k < count; ++k) {
+      const GaPre::Sess& x = ss[k];
+      for (uint32_t q = 0; q < x.R * x.n; ++q) {
+        const size_t p = x.pbase + q, r = x.rbase + q % x.n;
+        J1.add(DI((which == 0 ? o_s2 : o_s) + p * nl * 4), nl, DI(o_rn + r * nl * 4), nl, recvn_max, (uint32_t)r);
+      }
     }
   std::vector<uint8_t> desc;
   J1.pack(desc);
@@ -500,18 +554,42 @@ static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
   g.nl = nl;
   g.n = n;
-  g.R = R;
+  g.R = count == 1 ? bs->n_refresh : 0;
+  g.sess = std::move(ss);
   g.valid = true;
-  return prestart_fb_tables(c, b, g, n, P);
+  *n_out = n;
+  *P_out = P;
+  return FSDKR_OK;
 }
 
-// does the prestarted GA belong to this (single-session) batch?
-static bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* b, uint32_t n) {
+static int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
+  uint32_t n = 0, P = 0;
+  int rc = prestart_ga(c, b, 1, &n, &P);
+  if (rc || P == 0) return rc;
+  return prestart_fb_tables(c, b, *reinterpret_cast<GaPre*>(c->ga_pre), n, P);
+}
+
+// does the prestarted GA belong to these sessions (same shapes, same inputs)?
+static bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
   const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
-  if (!g || !g->valid || g->nl != b->nl || g->n != n || g->R != b->n_refresh) return false;
-  const size_t P = (size_t)b->n_refresh * n;
-  return memcmp(g->recv_n.data(), b->recv_n, (size_t)n * b->nl * 4) == 0 &&
-         memcmp(g->s2.data(), b->pdl_s2, P * b->nl * 4) == 0 && memcmp(g->s.data(), b->rp_s, P * b->nl * 4) == 0;
+  if (!g || !g->valid || g->sess.size() != count) return false;
+  uint32_t nl = 0;
+  for (uint32_t k = 0; k < count; ++k) nl = std::max(nl, bs[k].nl);
+  if (g->nl != nl) return false;
+  size_t on = 0, op = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const GaPre::Sess& x = g->sess[k];
+    const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
+    if (x.nl != b->nl || x.n != ns || x.R != b->n_refresh) return false;
+    const size_t rows = (size_t)x.R * x.n * x.nl;
+    if (memcmp(g->recv_n.data() + on, b->recv_n, (size_t)x.n * x.nl * 4) != 0 ||
+        memcmp(g->s2.data() + op, b->pdl_s2, rows * 4) != 0 || memcmp(g->s.data() + op, b->rp_s, rows * 4) != 0)
+      return false;
+    on += (size_t)x.n * x.nl;
+    op += rows;
+  }
+  return true;
 }
 
 // ------------------------------------------------------------------------------
@@ -600,7 +678,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
     recv_of_pair[p] = x.rbase + (p - x.pbase) % x.n;
   }
   // a prestarted GA of this batch: J1 is not launched again
-  pl.ga_hit = count == 1 && ga_pre_matches(c, bs, pl.ss[0].n);
+  pl.ga_hit = ga_pre_matches(c, bs, count);
   GaPre* gpre = reinterpret_cast<GaPre*>(c->ga_pre);
   if (pl.ga_hit) {
     pl.ga_done = gpre->done;
@@ -1877,6 +1955,13 @@ int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
   fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
   if (!c) return FSDKR_E_ARG;
   return fsdkr::collect_prestart_impl(c, batch);
+}
+
+int fsdkr_collect_prestart_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count) {
+  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  uint32_t n = 0, P = 0;
+  return fsdkr::prestart_ga(c, batches, count, &n, &P);
 }
 
 int fsdkr_collect_launch(fsdkr_ctx* ctx) {

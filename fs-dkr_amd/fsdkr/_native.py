@@ -102,6 +102,8 @@ def lib():
     L.fsdkr_collect_finish.restype = ctypes.c_int
     L.fsdkr_collect_prepare_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
     L.fsdkr_collect_prepare_multi.restype = ctypes.c_int
+    L.fsdkr_collect_prestart_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
+    L.fsdkr_collect_prestart_multi.restype = ctypes.c_int
     L.fsdkr_collect_finish_multi.argtypes = [vp, ctypes.POINTER(VerdictsC), ctypes.c_uint32]
     L.fsdkr_collect_finish_multi.restype = ctypes.c_int
     L.fsdkr_verify_collect_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32,
@@ -313,6 +315,13 @@ class Context:
         arr = (CollectBatchC * len(batches))(*[b.c for b in batches])
         self._many = arr   # keep the array alive until finish
         self.check(self._lib.fsdkr_collect_prepare_multi(self._h, arr, len(batches)))
+
+    def collect_prestart_set(self, sset):
+        """Start the GA chains of every regular session of a staged SessionSet."""
+        arr = sset.prestart_array()
+        if arr is not None:
+            self._prestart_keep = sset
+            self.check(self._lib.fsdkr_collect_prestart_multi(self._h, arr, sset.n_prestart))
 
     def collect_prepare_set(self, sset):
         """Prepare every live session of a fsdkr.batch.SessionSet as ONE device image."""

@@ -379,7 +379,10 @@ class SessionSet:
     CollectBatch; header-only sessions (threshold / size failures) are not
     prepared.  `live` lists the prepared sessions, in `structs` row order."""
 
-    def __init__(self, sessions, m_security=256, key_bits=2048):
+    def __init__(self, sessions, m_security=256, key_bits=2048, staged=False):
+        """staged: gather only what fsdkr_collect_prestart_multi reads (recv_n, PDL
+        s2, range-proof s of the regular sessions; prestart_array) and leave the
+        rest to complete(), so the longest chains run while it packs."""
         M = m_security
         S = len(sessions)
         self.S = S
@@ -395,15 +398,65 @@ class SessionSet:
         self.n = self.R + self.J
         self._keep = []
         self.structs = np.zeros(len(self.live), dtype=_BATCH_DT)
+        self.row = {s: r for r, s in enumerate(self.live)}
+        self._pre, self.n_prestart = None, 0
+        self._pending = (sessions, reg, M, key_bits)
+        # the prestart covers the set only when every prepared session is regular
+        # (prepare_multi's session list must equal the prestart's)
+        if staged and reg and len(reg) == len(self.live):
+            self._stage1(sessions, reg)
+        if not staged:
+            self.complete()
+
+    def complete(self):
+        """Stage 2 of a staged set (SessionSet(..., staged=True)): every field."""
+        if self._pending is None:
+            return self
+        sessions, reg, M, key_bits = self._pending
+        self._pending = None
+        regset = set(reg)
         if reg:
             self._pack_regular(sessions, reg, M, key_bits)
-        row = {s: r for r, s in enumerate(self.live)}
         for s in self.live:
             if s not in regset:
                 b = self.batches[s]
-                self.structs[row[s]] = np.frombuffer(ctypes.string_at(ctypes.addressof(b.c), ctypes.sizeof(b.c)),
-                                                     dtype=_BATCH_DT)[0]
-        self.row = row
+                self.structs[self.row[s]] = np.frombuffer(ctypes.string_at(ctypes.addressof(b.c), ctypes.sizeof(b.c)),
+                                                          dtype=_BATCH_DT)[0]
+        return self
+
+    def _stage1(self, sessions, reg):
+        ses = [sessions[s] for s in reg]
+        R = np.array([len(m) for m, lk, j in ses], dtype=np.int64)
+        n = R + np.array([len(j) for m, lk, j in ses], dtype=np.int64)
+        if any(len(lk.paillier_key_vec) < nn for (m, lk, j), nn in zip(ses, n)):
+            return
+        G = _Gather()
+        f_rn = G.field([k for (ms, lk, js), nn in zip(ses, n) for k in lk.paillier_key_vec[:nn]], "n")
+        f_s2 = G.field([m.pdl_proof_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s2")
+        f_s = G.field([m.range_proofs[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s")
+        bits = max(1, f_rn[1], f_s2[1], f_s[1])
+        nl = 64 if bits <= 2048 else 96 if bits <= 3072 else None
+        if nl is None:
+            return
+        a_rn, a_s2, a_s = G.slot(f_rn, nl), G.slot(f_s2, nl), G.slot(f_s, nl)
+        G.run()
+
+        def starts(counts):
+            return np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.uint64)
+        st = np.zeros(len(reg), dtype=_BATCH_DT)
+        st["n_refresh"] = R
+        st["n_join"] = n - R
+        st["nl"] = nl
+        st["recv_n"] = np.uint64(self._k(a_rn)) + starts(n) * np.uint64(nl * 4)
+        st["pdl_s2"] = np.uint64(self._k(a_s2)) + starts(R * n) * np.uint64(nl * 4)
+        st["rp_s"] = np.uint64(self._k(a_s)) + starts(R * n) * np.uint64(nl * 4)
+        self._pre, self.n_prestart = st, len(reg)
+
+    def prestart_array(self):
+        """fsdkr_collect_batch rows for fsdkr_collect_prestart_multi (None: nothing to start)."""
+        if self._pre is None:
+            return None
+        return ctypes.cast(self._pre.ctypes.data, ctypes.POINTER(CollectBatchC))
 
     def _k(self, arr):
         arr = np.ascontiguousarray(arr, dtype=np.uint32)

@@ -177,7 +177,10 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
     sess = [(list(r), lk, dk, list(j)) for r, lk, dk, j in sessions]
     # one gather across the sessions (SessionSet); sessions of another shape keep
     # their own batch, header-only ones are mapped without a device pass
-    sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits)
+    sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits, staged=True)
+    if sset.n_prestart:   # every session's s2^N, s^N mod N^2 chains start while the rest is packed
+        ctx.collect_prestart_set(sset)
+    sset.complete()
     live = sset.live
     specs = [None] * len(sess)
     verdicts = None

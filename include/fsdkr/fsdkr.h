@@ -232,6 +232,13 @@ int fsdkr_verify_collect_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batche
                                fsdkr_verdicts* out);
 int fsdkr_collect_prepare_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count);
 int fsdkr_collect_finish_multi(fsdkr_ctx* ctx, fsdkr_verdicts* out, uint32_t count);
+/* fsdkr_collect_prestart for many sessions: starts every session's s2^N and
+ * s^N mod N^2 chains (GA) in one launch from recv_n, pdl_s2, rp_s (and the
+ * counts, nl) of each batch; a later fsdkr_collect_prepare_multi of batches
+ * with the same values and shapes consumes the results (otherwise it computes
+ * them itself).  Lets the caller pack the other fields of 1024 custody
+ * sessions (BASELINE configs[4]) while the longest chains run. */
+int fsdkr_collect_prestart_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count);
 
 /* FsDkrError variants, in error.rs declaration order (error.rs:6-60). */
 #define FSDKR_ERR_NONE 0

@@ -170,3 +170,34 @@ def test_config4_multi_session_3072(gpu_ctx):
             ko = copy.deepcopy(lk)
             protocol.collect(tamper.to_oracle(msgs), ko, dk, [], Rng("a8"), 3072)
             assert (ko.x_i, ko.y, ko.pk_vec) == (many.x_i, many.y, many.pk_vec)
+
+
+def test_config4_prestart_hit_and_miss(gpu_ctx):
+    """fsdkr_collect_prestart_multi: the prepared set consumes the prestarted
+    s^N chains only when every session's inputs match.  A prestart of a set whose
+    PDL s2 differs in one session must not leak into the prepare of the real
+    set (all proofs still verify), and a matching prestart gives the same
+    verdicts as no prestart at all."""
+    import dataclasses
+    from fsdkr import synth
+    from fsdkr.batch import SessionSet
+    sessions = synth.synth_sessions(gpu_ctx, 6, n=3, t=1, seed=123, key_bits=3072)
+    work = [(m, lk, j) for m, j, lk, dk in sessions]
+    bad = copy.deepcopy(work)
+    p = bad[4][0][1].pdl_proof_vec[2]
+    bad[4][0][1].pdl_proof_vec[2] = dataclasses.replace(p, s2=p.s2 + 1)
+
+    def run(prestart_of):
+        if prestart_of is not None:
+            pre = SessionSet(prestart_of, 256, 3072, staged=True)
+            assert pre.n_prestart == 6
+            gpu_ctx.collect_prestart_set(pre)
+        sset = SessionSet(work, 256, 3072)
+        gpu_ctx.collect_prepare_set(sset)
+        gpu_ctx.collect_launch()
+        v = gpu_ctx.collect_finish_set(sset)
+        return [sset.first_error(s, v).variant for s in range(6)]
+    base = run(None)
+    assert base == [0] * 6
+    assert run(bad) == base      # stale prestart: recomputed
+    assert run(work) == base     # matching prestart: consumed
