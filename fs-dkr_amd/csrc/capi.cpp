@@ -198,6 +198,7 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   // runs only where the caller asked for it (it prepared KD = 160 constants)
   uint32_t grp = c->modexp_group ? c->modexp_group : group;
   if (grp == kWideGroup && (group != kWideGroup || k32 != 128)) grp = 16;
+  if (c->ct) grp = 0;   // the regular-access kernels have one shape per width
   const int KD = shape_digits_g(k32, grp);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
@@ -227,6 +228,7 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.count = count;
   a.prio = prio;
   a.group = grp;
+  a.ct = c->ct ? 1u : 0u;
   const size_t tm = c->tbeg("modexp", st);
   int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
   c->tend(tm, st);
@@ -296,7 +298,7 @@ int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_ba
   if (count == 0) return FSDKR_OK;
   uint32_t* d_consts = nullptr;
   // a context forced to the 32-lane shape (tuning, tests) gets KD = 160 constants here
-  const uint32_t wide = (c->modexp_group == kWideGroup && k32 == 128) ? kWideGroup : 0u;
+  const uint32_t wide = (!c->ct && c->modexp_group == kWideGroup && k32 == 128) ? kWideGroup : 0u;
   int rc = setup_moduli(c, k32, d_mods, n_mod, &d_consts, wide ? "generic_wide" : "generic", wide);
   if (rc) return rc;
   ModexpJob job;
@@ -547,6 +549,15 @@ int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const
   if (rc) return rc;
   if ((rc = c->hip_check(hipMemcpyAsync(out, d_out, nb, hipMemcpyDeviceToHost, c->stream), "D2H out"))) return rc;
   return c->sync();
+}
+
+int fsdkr_modexp_batch_ct(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* base,
+                          const uint32_t* exp, uint32_t exp_limbs, const uint32_t* mod_idx, const uint32_t* mods,
+                          uint32_t n_mod, uint32_t* out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  CtScope ct(c);
+  return fsdkr_modexp_batch(ctx, mod_limbs, count, base, exp, exp_limbs, mod_idx, mods, n_mod, out);
 }
 
 int fsdkr_modexp_batch_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* d_base,

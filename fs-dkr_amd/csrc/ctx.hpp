@@ -62,6 +62,8 @@ struct Ctx {
   // issue priority (s_setprio) of the generic entry points' kernels: the share
   // recovery raises it while it overlaps a launched collect pipeline
   uint32_t prio = 0;
+  // regular-access modexp (secret exponents: prover, key generation, decryption)
+  bool ct = false;
   hipStream_t side_stream(int k);
   // CU reservation for latency-critical serial chains (FSDKR_RESERVE_CUS = R, a
   // multiple of 8): crit_stream() runs on R CUs spread evenly over the 8 XCDs and
@@ -100,6 +102,14 @@ struct PrioScope {
   uint32_t saved;
   PrioScope(Ctx* cx, uint32_t p) : c(cx), saved(cx->prio) { c->prio = p; }
   ~PrioScope() { c->prio = saved; }
+};
+
+// Runs the modexp launches of one entry point in regular-access mode (ModexpArgs.ct).
+struct CtScope {
+  Ctx* c;
+  bool saved;
+  explicit CtScope(Ctx* cx, bool on = true) : c(cx), saved(cx->ct) { c->ct = on; }
+  ~CtScope() { c->ct = saved; }
 };
 
 // Host worker threads for the collect() pre-pass (FSDKR_HOST_THREADS, else

@@ -24,6 +24,8 @@ struct ModexpArgs {
   uint32_t count;
   uint32_t prio;             // > 0: latency-critical launch, its waves raise their issue priority to s_setprio(prio)
   uint32_t group;            // lanes per instance (0 = choose by batch size)
+  uint32_t ct;               // 1: regular access for secret exponents (every window-table read
+                             // scans the whole table; every instance runs `nwin` windows)
 };
 
 int shape_digits(uint32_t k32);   // KD for a K32-limb modulus class (0 if unsupported)

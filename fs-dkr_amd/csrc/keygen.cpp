@@ -87,7 +87,10 @@ extern "C" int fsdkr_miller_rabin(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t c
     job.add((uint64_t)(uintptr_t)(d_base + (size_t)i * K), mod_limbs, (uint64_t)(uintptr_t)(d_exp + (size_t)i * K),
             mod_limbs, eb, i);
   }
-  if ((rc = launch_modexp_job(c, job, d_consts, d_x, "mr"))) return rc;
+  {   // the candidates are secret (the accepted one is a prime factor of a key)
+    CtScope ct(c);
+    if ((rc = launch_modexp_job(c, job, d_consts, d_x, "mr"))) return rc;
+  }
   MrTailArgs a{d_x, d_consts, d_s, s_max, d_v, count};
   c->mark("mr_tail", true);
   rc = c->hip_check(mr_tail(mod_limbs, a, c->stream), "mr_tail launch");

@@ -82,7 +82,23 @@ __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __rest
   if (g == 0) out[3 * KD] = M.ninv;
 }
 
-template <int KD, int G, int K32>
+// dst = this lane's digits of table row d, read by scanning every row and keeping
+// row d through a mask: the addresses and the instruction stream do not depend
+// on d (a secret exponent's window digit).
+template <int L>
+__device__ __forceinline__ void ct_row(uint32_t* dst, const uint32_t* T, uint32_t d, uint32_t rows, int KD, int g) {
+#pragma unroll
+  for (int j = 0; j < L; ++j) dst[j] = 0u;
+  for (uint32_t e = 0; e < rows; ++e) {
+    const uint32_t m = 0u - (uint32_t)(e == d);
+#pragma unroll
+    for (int j = 0; j < L; ++j) dst[j] |= T[(size_t)e * KD + g * L + j] & m;
+  }
+}
+
+// CT: the regular-access variant for secret exponents (a separate instantiation:
+// its table scans would cost the throughput shapes occupancy)
+template <int KD, int G, int K32, bool CT = false>
 __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
@@ -118,7 +134,9 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);
 #pragma unroll
   for (int j = 0; j < L; ++j) T[g * L + j] = C[KD + g * L + j];             // T[0] = R mod N
-  const uint32_t nwin = a.nwin_i ? max(1u, a.nwin_i[inst]) : a.nwin;
+  // regular access (secret exponents): every instance runs the launch's window
+  // count and every window-table read scans the whole table (ct_row below)
+  const uint32_t nwin = (a.nwin_i && !CT) ? max(1u, a.nwin_i[inst]) : a.nwin;
   auto digit = [&](uint32_t k) -> uint32_t {
     const uint32_t p = (nwin - 1 - k) * w;
     const uint32_t lo = p >> 5, sh = p & 31;
@@ -141,8 +159,11 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
     bool from_acc = false, one = false;
     if (st == n_build) {                                                    // start of the ladder
       const uint32_t d0 = digit(0);
+      if constexpr (CT) ct_row<L>(acc, T, d0, tsize, KD, g);
+      else {
 #pragma unroll
-      for (int j = 0; j < L; ++j) acc[j] = T[(size_t)d0 * KD + g * L + j];
+        for (int j = 0; j < L; ++j) acc[j] = T[(size_t)d0 * KD + g * L + j];
+      }
     }
     if (st == 0) {
       src = C + 2 * KD;
@@ -157,6 +178,10 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
     __builtin_amdgcn_wave_barrier();
     if (from_acc) {
       lds_put<KD, G>(stream, acc, g);
+    } else if (CT && st > n_build && st < n_steps - 1) {   // window multiply: scan the table
+      uint32_t row[L];
+      ct_row<L>(row, T, digit(k), tsize, KD, g);
+      lds_put<KD, G>(stream, row, g);
     } else if (one) {
 #pragma unroll
       for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
@@ -200,13 +225,13 @@ static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* c
 constexpr uint32_t kSmallLaunchLanes = 256u * 4u * 64u;
 static inline uint32_t block_threads(uint32_t lanes) { return lanes <= kSmallLaunchLanes ? 64u : (uint32_t)BLOCK; }
 
-template <int KD, int G, int K32>
+template <int KD, int G, int K32, bool CT = false>
 static hipError_t launch_modexp(const ModexpArgs& a, hipStream_t st) {
   const uint32_t bs = block_threads(a.count * G);
   const uint32_t ipb = bs / G;
   const uint32_t blocks = (a.count + ipb - 1) / ipb;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((modexp_kernel<KD, G, K32>), dim3(blocks), dim3(bs), 0, st, a);
+  hipLaunchKernelGGL((modexp_kernel<KD, G, K32, CT>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
@@ -266,6 +291,17 @@ static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int>
 }
 
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
+  if (a.ct) {   // secret exponents: one regular-access shape per width
+    if (a.group == kWideGroup) return hipErrorInvalidValue;
+    switch (k32) {
+      case 32: return launch_modexp<36, 4, 32, true>(a, st);
+      case 64: return launch_modexp<72, 4, 64, true>(a, st);
+      case 96: return launch_modexp<108, 4, 96, true>(a, st);
+      case 128: return launch_modexp<144, 8, 128, true>(a, st);
+      case 192: return launch_modexp<216, 8, 192, true>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (k32) {
     case 32:   // 1024-bit primes of key generation: L = 9 (4 lanes) or 18
       return pick_group(a.count, (int)a.group, {2, 4}, 4) == 2 ? launch_modexp<36, 2, 32>(a, st)

@@ -113,8 +113,9 @@ int fsdkr_paillier_decrypt_multi(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, co
       idx[2 * i + 1] = 2 * key_idx[i] + 1;
     }
   });
-  rc = fsdkr_modexp_batch(ctx, nl, 2 * count, base.data(), ex.data(), nl, idx.data(), mods.data(), 2 * n_keys,
-                          outv.data());
+  // secret exponents p - 1, q - 1: regular-access modexp
+  rc = fsdkr_modexp_batch_ct(ctx, nl, 2 * count, base.data(), ex.data(), nl, idx.data(), mods.data(), 2 * n_keys,
+                             outv.data());
   if (rc) return rc;
   const hbn::Limbs one{1};
   parallel_for_host(count, 16, [&](size_t b0, size_t b1) {

@@ -80,6 +80,8 @@ def lib():
     L.fsdkr_modexp_batch.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_uint32, u32p, u32p,
                                      ctypes.c_uint32, u32p]
     L.fsdkr_modexp_batch.restype = ctypes.c_int
+    L.fsdkr_modexp_batch_ct.argtypes = L.fsdkr_modexp_batch.argtypes
+    L.fsdkr_modexp_batch_ct.restype = ctypes.c_int
     L.fsdkr_modexp_batch_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
                                             ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp]
     L.fsdkr_modexp_batch_device.restype = ctypes.c_int
@@ -208,8 +210,9 @@ class Context:
     def kernel_time_reset(self):
         self._lib.fsdkr_kernel_time_reset(self._h)
 
-    def modexp_batch(self, bases, exps, mods, mod_idx, mod_limbs):
-        """[base_i ^ exp_i mod mods[mod_idx_i]] computed on the GPU."""
+    def modexp_batch(self, bases, exps, mods, mod_idx, mod_limbs, secret=False):
+        """[base_i ^ exp_i mod mods[mod_idx_i]] computed on the GPU.  secret=True:
+        regular-access kernel (fsdkr_modexp_batch_ct) for secret exponents."""
         count = len(bases)
         if count == 0:
             return []
@@ -220,8 +223,8 @@ class Context:
         Mo = ints_to_limbs(mods, mod_limbs)
         I = np.ascontiguousarray(np.asarray(mod_idx, dtype=np.uint32))
         O = np.zeros((count, mod_limbs), dtype=np.uint32)
-        self.check(self._lib.fsdkr_modexp_batch(self._h, mod_limbs, count, _ptr(B), _ptr(E), exp_limbs, _ptr(I),
-                                                _ptr(Mo), len(mods), _ptr(O)))
+        fn = self._lib.fsdkr_modexp_batch_ct if secret else self._lib.fsdkr_modexp_batch
+        self.check(fn(self._h, mod_limbs, count, _ptr(B), _ptr(E), exp_limbs, _ptr(I), _ptr(Mo), len(mods), _ptr(O)))
         return limbs_to_ints(O)
 
     def fixed_base_modexp(self, bases, base_mod_idx, mods, base_idx, exps, mod_limbs):

@@ -9,7 +9,10 @@ Every exponentiation runs on the GPU in a few batched launches:
   round 2  r^e mod N for the PDL s2 and Alice s responses (after the challenges)
   keys     Paillier / ring-Pedersen moduli by the batched GPU Miller-Rabin prime
            walk (fsdkr/keygen.py), correct-key sigma_j = rho_j^(N^-1 mod phi),
-           ring-Pedersen A_i = T^a_i through the fixed-base engine.
+           ring-Pedersen A_i = T^a_i.
+Every exponentiation with a secret exponent (alpha, gamma, rho, the share x,
+a_i, lambda, xhi, N^-1 mod phi, the DLog proof's r) runs through the
+regular-access kernel (fsdkr_modexp_batch_ct: no exponent-dependent addresses).
 Hashes, small-number arithmetic and the order of random draws are host work.
 
 Randomness is injected: `rng` provides sample_below(n) and bits(k) (the
@@ -110,9 +113,11 @@ def ring_pedersen_generate_and_prove(ctx, rng, key_bits, M):
         lam = rng.sample_below(phi)
         T = r * r % N
         w = _width(N.bit_length())
-        S = ctx.modexp_batch([T], [lam], [N], [0], w)[0]
+        S = ctx.modexp_batch([T], [lam], [N], [0], w, secret=True)[0]
         a = [rng.sample_below(phi) for _ in range(M)]
-        A = ctx.fixed_base_modexp([T], [0], [N], [0] * M, a, w)     # T shared by all M: fixed-base engine
+        # secret a_i: the regular-access modexp (the fixed-base engine's digit sort
+        # would order memory accesses by the exponent digits)
+        A = ctx.modexp_batch([T] * M, a, [N], [0] * M, w, secret=True)
         eb = _to_bytes(chain_bigint(*A))
         if 8 * len(eb) < M:
             continue
@@ -182,7 +187,7 @@ def distribute(old_party_index, local_key, new_n, rng=None, ctx=None, key_bits=2
             bases.append(b)
             exps.append(e)
             mods.append(Nt)
-    nt = ctx.modexp_batch(bases, exps, mods, list(range(len(mods))), wN)
+    nt = ctx.modexp_batch(bases, exps, mods, list(range(len(mods))), wN, secret=True)
     bn = ctx.modexp_batch([pd[i]["beta"] for i in range(n)] + [ad[i]["beta"] for i in range(n)],
                           [eks[i].n for i in range(n)] * 2, [eks[i].nn for i in range(n)] * 2,
                           list(range(2 * n)), 2 * wN)
@@ -245,7 +250,7 @@ def generate_h1_h2_n_tilde(ctx, rng, key_bits):
         if math.gcd(xhi, phi) == 1:
             xhi_inv = pow(xhi, -1, phi)
             break
-    h2 = ctx.modexp_batch([h1], [xhi], [ek.n], [0], _width(ek.n.bit_length()))[0]
+    h2 = ctx.modexp_batch([h1], [xhi], [ek.n], [0], _width(ek.n.bit_length()), secret=True)[0]
     return ek.n, h1, h2, phi - xhi, phi - xhi_inv
 
 
@@ -270,7 +275,7 @@ def join_distribute(rng=None, ctx=None, key_bits=2048, m_security=256):
 def _one_dlog_proof(ctx, rng, st, secret):
     from .types import CompositeDLogProof
     r = rng.sample_below((1 << (128 + 128 + 256)) * st.N)
-    x = ctx.modexp_batch([st.g], [r], [st.N], [0], _width(st.N.bit_length()))[0]
+    x = ctx.modexp_batch([st.g], [r], [st.N], [0], _width(st.N.bit_length()), secret=True)[0]
     return CompositeDLogProof(x, r + chain_bigint(x, st.g, st.N, st.ni) * secret)
 
 

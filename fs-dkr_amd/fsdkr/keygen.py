@@ -235,7 +235,7 @@ def correct_key_proofs(ctx, dks):
             exps += [d] * M2
             mods.append(n)
             midx += [m] * M2
-        sig = ctx.modexp_batch(bases, exps, mods, midx, w)
+        sig = ctx.modexp_batch(bases, exps, mods, midx, w, secret=True)   # d = N^-1 mod phi is secret
         for m, k in enumerate(ks):
             out[k] = NiCorrectKeyProof(tuple(sig[M2 * m:M2 * m + M2]))
     return out

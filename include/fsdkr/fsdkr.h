@@ -81,6 +81,18 @@ int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const
                        const uint32_t* exp, uint32_t exp_limbs, const uint32_t* mod_idx,
                        const uint32_t* mods, uint32_t n_mod, uint32_t* out);
 
+/* fsdkr_modexp_batch for SECRET exponents (the prover's alpha, gamma, rho, a_i,
+ * lambda, xhi, sigma's N^-1 mod phi; key generation's candidates; decryption's
+ * p - 1, q - 1): identical results, but the kernel's memory addresses and
+ * instruction stream do not depend on the exponent.  Every window-table read
+ * scans the whole table through a mask, and every instance runs the window
+ * count of the widest exponent of the call (only exp_limbs is visible).  GMP's
+ * mpz_powm, behind the reference's curv BigInt::mod_pow, has no such property
+ * (mpz_powm_sec does). */
+int fsdkr_modexp_batch_ct(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* base,
+                          const uint32_t* exp, uint32_t exp_limbs, const uint32_t* mod_idx,
+                          const uint32_t* mods, uint32_t n_mod, uint32_t* out);
+
 /* out[i] = y[i]^-1 mod m[i] and unit[i] = (gcd(y[i], m[i]) == 1); y[i] < m[i],
  * every m[i] odd, all [count][mod_limbs].  out may be NULL (unit test only).
  * Replaces curv BigInt::mod_inv (GMP mpz_invert) at zk_pdl_with_slack.rs:180

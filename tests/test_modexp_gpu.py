@@ -76,3 +76,21 @@ def test_modexp_every_group_size(gpu_ctx, limbs, group):
     want = [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
     bad = [k for k in range(count) if got[k] != want[k]]
     assert not bad, f"G={group}: {len(bad)} mismatches, first at {bad[0]}"
+
+
+@pytest.mark.parametrize("limbs", [32, 64, 96, 128])
+def test_modexp_regular_access_equals_plain(gpu_ctx, limbs):
+    """fsdkr_modexp_batch_ct (secret exponents: table scans, uniform window count)
+    returns exactly fsdkr_modexp_batch's results, including tiny exponents mixed
+    with full-width ones (one-window instances) and exponent 0."""
+    rnd = random.Random(100 + limbs)
+    bits = 32 * limbs
+    mods = [_odd(rnd, bits) for _ in range(3)] + [_odd(rnd, bits - 61)]
+    count = 120
+    idx = [rnd.randrange(len(mods)) for _ in range(count)]
+    bases = [rnd.getrandbits(bits) for _ in range(count)]
+    exps = [rnd.getrandbits(rnd.choice([1, 3, 6, 64, 700, bits])) for _ in range(count)]
+    exps[:4] = [0, 1, 2, (1 << bits) - 1]
+    got = gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs, secret=True)
+    assert got == [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
+    assert got == gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs)
