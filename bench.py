@@ -325,11 +325,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box (FSDKR_BENCH_REHEARSE=1):
+    # every rank on device 0, gloo instead of RCCL (which needs one GPU per rank)
+    rehearse = os.environ.get("FSDKR_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from fsdkr import Context, refresh, shard, synth
     ctx = Context(device=local)
     R, J, t, n = a.n - a.joins, a.joins, a.t, a.n
