@@ -295,7 +295,7 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
     if (a.group == kWideGroup) return hipErrorInvalidValue;
     switch (k32) {
       case 32: return launch_modexp<36, 4, 32, true>(a, st);
-      case 64: return launch_modexp<72, 4, 64, true>(a, st);
+      case 64: return launch_modexp<72, 8, 64, true>(a, st);   // small launches (decryption): 8 lanes
       case 96: return launch_modexp<108, 4, 96, true>(a, st);
       case 128: return launch_modexp<144, 8, 128, true>(a, st);
       case 192: return launch_modexp<216, 8, 192, true>(a, st);
