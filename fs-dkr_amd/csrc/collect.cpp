@@ -243,6 +243,7 @@ struct GaPre {
   std::vector<Sess> sess;
   uint32_t* out = nullptr;               // [2P][nn]: J1 instance order (s2^N rows, then s^N rows)
   hipEvent_t done = nullptr;
+  hipEvent_t ga_setup = nullptr;   // GA's Montgomery constants ready (before its chains)
   // the fixed-base tables of h1_i, h2_i (bases 2i, 2i+1 of prepare's FbJob), built
   // for exponents of up to bits_h1 / bits_h2 bits with window w
   bool fb_valid = false;
@@ -256,6 +257,7 @@ struct GaPre {
 void free_ga_pre(Ctx* c) {
   GaPre* g = reinterpret_cast<GaPre*>(c->ga_pre);
   if (g && g->done) (void)hipEventDestroy(g->done);
+  if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
   if (g && g->fb_done_a) (void)hipEventDestroy(g->fb_done_a);
   delete g;
@@ -306,20 +308,31 @@ static void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, ui
 // bit lengths of the exponents they serve (PDL / Alice s1, s3|s2; RP Z), on the
 // table chain's stream.
 static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, uint32_t n, uint32_t P) {
-  if (!b->recv_ntilde || !b->recv_h1 || !b->recv_h2 || !b->pdl_s1 || !b->pdl_s3 || !b->rp_s1 || !b->rp_s2 ||
-      !b->s1l || !b->s3l || !b->ped_T || !b->ped_N || !b->ped_Z || !b->zl || !b->m_security)
+  if (!b->recv_ntilde || !b->recv_h1 || !b->recv_h2 || !b->s1l || !b->s3l || !b->ped_T || !b->ped_N || !b->zl ||
+      !b->m_security)
     return FSDKR_OK;   // stage 1 did not pack them: prepare builds every table
+  // exponent bit bounds: exact from the packed exponents, else their slot widths
+  // (a slim stage 1 leaves s1 / s3 / Z to stage 2; tables at most 31 bits longer)
+  const bool exact_s = b->pdl_s1 && b->pdl_s3 && b->rp_s1 && b->rp_s2;
   const char* pfe = getenv("FSDKR_PRE_FB");   // 0: no table prestart (tuning)
   if (pfe && pfe[0] == '0') return FSDKR_OK;
   const uint32_t nl = b->nl, Mt = b->n_refresh + b->n_join, M = b->m_security;
   for (uint32_t i = 0; i < n; ++i)
     if (!is_odd(b->recv_ntilde + (size_t)i * nl)) return FSDKR_OK;
   uint32_t bh1 = 1, bh2 = 1, bz = 1;
-  for (size_t p = 0; p < P; ++p) {
-    bh1 = std::max(bh1, std::max(hbn::bitlen(b->pdl_s1 + p * b->s1l, b->s1l), hbn::bitlen(b->rp_s1 + p * b->s1l, b->s1l)));
-    bh2 = std::max(bh2, std::max(hbn::bitlen(b->pdl_s3 + p * b->s3l, b->s3l), hbn::bitlen(b->rp_s2 + p * b->s3l, b->s3l)));
+  if (exact_s) {
+    for (size_t p = 0; p < P; ++p) {
+      bh1 = std::max(bh1, std::max(hbn::bitlen(b->pdl_s1 + p * b->s1l, b->s1l), hbn::bitlen(b->rp_s1 + p * b->s1l, b->s1l)));
+      bh2 = std::max(bh2, std::max(hbn::bitlen(b->pdl_s3 + p * b->s3l, b->s3l), hbn::bitlen(b->rp_s2 + p * b->s3l, b->s3l)));
+    }
+  } else {
+    bh1 = 32 * b->s1l;
+    bh2 = 32 * b->s3l;
   }
-  for (size_t k = 0; k < (size_t)Mt * M; ++k) bz = std::max(bz, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
+  if (b->ped_Z)
+    for (size_t k = 0; k < (size_t)Mt * M; ++k) bz = std::max(bz, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
+  else
+    bz = 32 * b->zl;
   const uint32_t w = fb_window(std::max(std::max(bh1, bh2), bz));
   const FbLayout L = fb_layout(n, Mt, w, bh1, bh2, bz);
   const uint32_t nb = 2 * n + Mt, entries = L.entries, nmod = n + Mt;
@@ -362,6 +375,10 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, ts), "prestart fb H2D")) ||
       (rc = c->hip_check(hipStreamSynchronize(ts), "prestart fb H2D sync")))
     return rc;
+  // FSDKR_FB_WAIT_GA=1: the table chains start after GA's constants, i.e. right
+  // behind GA's chains (keeps GA dispatched first when stage 1 is quick)
+  if (const char* e = getenv("FSDKR_FB_WAIT_GA"); e && e[0] == '1' && g.ga_setup)
+    (void)hipStreamWaitEvent(ts, g.ga_setup, 0);
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl")))
     return rc;
@@ -544,6 +561,9 @@ static int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, ui
                          group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
     return rc;
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
+  if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
+    return rc;
+  (void)hipEventRecord(g.ga_setup, gs);   // GA's constants are ready
   // issue priority 3 (FSDKR_PRE_GA_PRIO; 2 measured 1-2 ms slower per call,
   // profiles/r02x_ab_full.jsonl)
   const char* gpe = getenv("FSDKR_PRE_GA_PRIO");
