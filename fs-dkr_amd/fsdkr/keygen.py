@@ -30,6 +30,7 @@ from .types import DecryptionKey, EncryptionKey, NiCorrectKeyProof
 
 MR_ROUNDS = 8
 SIEVE_LIMIT = 2000
+MAX_PASSES = 1000
 SALT = bytes([75, 90, 101, 110])    # zk-paillier SALT_STRING [dep, unverified]
 M2 = 11                             # NiCorrectKeyProof sigma_vec length
 
@@ -114,12 +115,16 @@ def sample_primes(ctx, rng, bits, count, window=None, span=None):
     draw = lambda: rng.bits(bits) | (3 << (bits - 2)) | 1   # noqa: E731
     walks = [_Walk(draw(), span) for _ in range(count)]
     out = [None] * count
+    passes = 0
     while True:
         active = [w for w in range(count) if out[w] is None and walks[w].pos < len(walks[w].offs)]
         if not active:
             failed = [w for w in range(count) if out[w] is None]
             if not failed:
                 return out
+            passes += 1
+            if passes > MAX_PASSES:   # never for a working test (a pass fails w.p. ~1e-5 at 4*bits)
+                raise RuntimeError(f"sample_primes: no prime after {MAX_PASSES} walk passes (Miller-Rabin backend?)")
             for w in failed:                       # a new pass, in walk order
                 walks[w] = _Walk(draw(), span)
             continue

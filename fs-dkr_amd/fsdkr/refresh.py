@@ -76,6 +76,13 @@ def _ctx(ctx):
     return _default_ctx
 
 
+def _whole_chip(ctx):
+    """A single-GPU collect uses every CU: undo a shard slice's GA split
+    (fsdkr_ctx_set_cu_split returns at once when nothing changes)."""
+    if hasattr(ctx, "set_cu_split"):
+        ctx.set_cu_split(0)
+
+
 def _error_of(err):
     """fsdkr_error -> None | FsDkrError | FsDkrPanic."""
     if err.variant == 0:
@@ -142,6 +149,7 @@ def _apply_share(local_key, new_dk, rec):
 def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_security=256, key_bits=2048):
     """RefreshMessage::collect (refresh_message.rs:321-467)."""
     ctx = _ctx(ctx)
+    _whole_chip(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
     # stage 1 packs what the pipeline's longest job reads and starts it on the GPU;
     # the rest of the batch is packed while those chains run
@@ -174,6 +182,7 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
     updated as collect() does) or the FsDkrError / FsDkrPanic collect() would
     raise (local_key partially updated as collect() leaves it)."""
     ctx = _ctx(ctx)
+    _whole_chip(ctx)
     sess = [(list(r), lk, dk, list(j)) for r, lk, dk, j in sessions]
     # one gather across the sessions (SessionSet); sessions of another shape keep
     # their own batch, header-only ones are mapped without a device pass
@@ -227,6 +236,7 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
     Returns one outcome per party, as collect_many does: None (local_key
     updated) or the FsDkrError / FsDkrPanic collect() would raise."""
     ctx = _ctx(ctx)
+    _whole_chip(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
     groups = {}
     for p, (lk, dk) in enumerate(parties):
