@@ -55,9 +55,10 @@ def main():
     for rnd in range(a.rounds):
         for W in a.world:
             for env in a.env:
-                k, v = env.split("=", 1)
-                old = os.environ.get(k)
-                os.environ[k] = v
+                kvs = [kv.split("=", 1) for kv in env.split("+")]   # K=V[+K2=V2...]
+                saved = {k: os.environ.get(k) for k, _ in kvs}
+                for k, v in kvs:
+                    os.environ[k] = v
                 ctx = Context()
                 dist = Rank0(W, R, J, n)
                 keys = [copy.deepcopy(lk) for _ in range(a.steps + 2)]
@@ -70,10 +71,11 @@ def main():
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t0) / a.steps * 1e3
                 ctx.close()
-                if old is None:
-                    del os.environ[k]
-                else:
-                    os.environ[k] = old
+                for k, v in saved.items():
+                    if v is None:
+                        del os.environ[k]
+                    else:
+                        os.environ[k] = v
                 res.setdefault((W, env), []).append(ms)
                 print(json.dumps({"world": W, "env": env, "round": rnd, "rank0_collect_ms": ms}), flush=True)
     for (W, env), v in sorted(res.items()):
