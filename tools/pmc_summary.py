@@ -29,7 +29,7 @@ def load(pass_dir, kernel_sub):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--kernel", default="modexp_kernel<144, 4, 128>")
+    ap.add_argument("--kernel", default="modexp_kernel<144, 4, 128, false>")
     ap.add_argument("--instances", type=int, default=65536)
     ap.add_argument("--macs-per-instance", type=float, default=80.86e6)
     a = ap.parse_args()
