@@ -1131,9 +1131,25 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
       j9_index[p] = (uint32_t)J9.size();
       J9.add(DI(o_NP1 + (size_t)r * nn * 4), nn, DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, r);
     }
-  for (uint32_t m = 0; m < Mt; ++m)
-    for (uint32_t k = 0; k < M; ++k)  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144)
-      FB.add(fb_T[m], DI(o_pZ + ((size_t)m * M + k) * zl * 4), zl, z_max, DX(x_RP + ((size_t)m * M + k) * nl * 4));
+  clk.lap("desc pairs");
+  {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
+    const size_t o = FB.grow((size_t)Mt * M);
+    for (uint32_t m = 0; m < Mt; ++m) FB.b_bits[fb_T[m]] = std::max(FB.b_bits[fb_T[m]], std::max(z_max, 1u));
+    parallel_for(Mt, 16, [&](size_t m0, size_t m1) {
+      for (size_t m = m0; m < m1; ++m) {
+        const uint32_t b = fb_T[m], md = FB.b_mod[b];
+        for (uint32_t k = 0; k < M; ++k) {
+          const size_t i = o + m * M + k, z = m * M + k;
+          FB.e_ptr[i] = DI(o_pZ + z * zl * 4);
+          FB.e_len[i] = zl;
+          FB.e_base[i] = b;
+          FB.e_mod[i] = md;
+          FB.o_ptr[i] = DX(x_RP + z * nl * 4);
+        }
+      }
+    });
+  }
+  clk.lap("desc rp");
   // FSDKR_FB_SPLIT=1: group A's exponents start before the h2 tables are done.
   // Measured 1-2 ms slower than one launch at n = 64 (the early group-A exponents
   // compete with GA / J2 / J5 for the chip; profiles/r02x_ab_full.jsonl): off.
@@ -1212,6 +1228,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
       reinterpret_cast<GaPre*>(c->ga_pre)->fb_valid = false;   // consumed
     }
   }
+  clk.lap("desc fb finalize");
   FB.pack(desc);   // FbJob offsets are positions in `desc`, i.e. relative to desc_base
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N
   std::vector<uint64_t> bs_ptr(2 * (size_t)P), bn_ptr(2 * (size_t)P);
@@ -1247,6 +1264,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   const size_t d_iynn = put(inv_y_nn.data(), inv_y_nn.size() * 8), d_imnn = put(inv_m_nn.data(), inv_m_nn.size() * 8);
   const size_t d_iynl = put(inv_y_nl.data(), inv_y_nl.size() * 8), d_imnl = put(inv_m_nl.data(), inv_m_nl.size() * 8);
   // eq_check descriptors
+  clk.lap("desc fb/binom/inv");
   std::vector<EqOperand> eq_nn(P), eq_nl, eq_ck;
   std::vector<uint32_t> eq_nn_mod(P), eq_nl_mod, eq_ck_mod;
   for (uint32_t p = 0; p < P; ++p) {  // PDL u2: (N+1)^s1 * s2^N == u2 * c^e  (mod N^2), u2 < N^2
@@ -1313,6 +1331,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
       eq_ck.push_back(e);
       eq_ck_mod.push_back(m);
     }
+  clk.lap("desc eq build");
   const size_t d_eqnn = put(eq_nn.data(), eq_nn.size() * sizeof(EqOperand)),
                d_eqnnm = put(eq_nn_mod.data(), eq_nn_mod.size() * 4);
   const size_t d_eqnl = put(eq_nl.data(), eq_nl.size() * sizeof(EqOperand)),

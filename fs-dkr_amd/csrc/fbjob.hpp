@@ -48,6 +48,17 @@ struct FbJob {
     o_ptr.push_back(out);
     b_bits[base] = std::max(b_bits[base], std::max(ebits, 1u));
   }
+  // append `cnt` instances to be filled in place (e_ptr, e_len, e_base, e_mod,
+  // o_ptr at [offset, offset + cnt)); the caller raises b_bits itself
+  size_t grow(size_t cnt) {
+    const size_t o = count();
+    e_ptr.resize(o + cnt);
+    e_len.resize(o + cnt);
+    e_base.resize(o + cnt);
+    e_mod.resize(o + cnt);
+    o_ptr.resize(o + cnt);
+    return o;
+  }
   size_t count() const { return e_ptr.size(); }
   size_t bases() const { return b_ptr.size(); }
 
