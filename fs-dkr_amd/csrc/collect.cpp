@@ -456,6 +456,10 @@ static int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, ui
     c->fail("fsdkr_collect_prestart: a batch is in flight (call finish first)");
     return FSDKR_E_ARG;
   }
+  // a prepared plan that consumed the previous prestart reads its s^N rows and
+  // fixed-base tables in place: this prestart overwrites (or reallocates) those
+  // buffers, so the plan is dropped (a later launch reports "no prepared batch")
+  if (running && (running->ga_hit || running->fb_hit)) free_collect_plan(c);
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prestart: no batch");
     return FSDKR_E_ARG;

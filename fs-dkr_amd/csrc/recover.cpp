@@ -141,6 +141,7 @@ int fsdkr_paillier_decrypt_multi(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, co
 
 int fsdkr_paillier_decrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const uint32_t* c, const uint32_t* p,
                            const uint32_t* q, uint32_t* m_out) {
+  if (count == 0) return ctx ? FSDKR_OK : FSDKR_E_ARG;   // an empty batch: nothing to decrypt
   std::vector<uint32_t> key_idx(count, 0u);
   return fsdkr_paillier_decrypt_multi(ctx, nl, count, c, key_idx.data(), p, q, 1, m_out);
 }

@@ -6,12 +6,20 @@ success after mutating `local_key` exactly as collect() does, raises
 FsDkrError with the reference's variant name and payload for the FIRST failing
 check (or FsDkrPanic where the reference panics).  All proof verification runs
 in one batched GPU pass (fsdkr_collect_launch/finish); the share recovery
-(decryption + pk_vec MSM) runs speculatively on the context's recovery stream
-WHILE the proofs are verified and is discarded if a check fails (its result
-is deterministic, so running it early changes nothing but the latency).
+(decryption + pk_vec MSM) by default runs speculatively on the context's
+recovery stream WHILE the proofs are verified and is discarded if a check
+fails (its result is deterministic, so running it early changes nothing but
+the latency).  This departs from the reference, which decrypts with the old
+secret key only after every check has passed (:439); `recovery="after"`
+restores that order (decrypt once the verdicts are in; same LocalKey and
+outcome, tests/test_reference_scenarios_gpu.py), at the cost of the overlap.
+The share recovery's own panics keep the reference's place in the error order:
+get_ciphertext_sum (:367-373) panics before the correct-key / moduli / DLog
+checks and before any paillier_key_vec write; decryption and the pk_vec loop
+(:439-464) after them.
 collect_many() verifies many independent sessions in one device pass
 (BASELINE configs[4]).  There is no CPU fallback."""
-from ._native import Context
+from ._native import Context, FsdkrError
 from .batch import CollectBatch, SessionSet
 
 Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
@@ -48,6 +56,18 @@ class FsDkrError(Exception):
 
 class FsDkrPanic(Exception):
     """The reference panics at this point (unwrap / index / assert)."""
+
+
+class _SumPanic(FsDkrPanic):
+    """get_ciphertext_sum panics (refresh_message.rs:367-373: the old ek, a
+    message's ciphertext for this party, the first t+1 old indices, a repeated
+    index in the Lagrange set): after the ring-Pedersen checks, before the
+    correct-key / moduli / DLog checks and before any paillier_key_vec write."""
+
+
+# first_error variants the reference reaches only after get_ciphertext_sum (:375-437)
+_AFTER_SUM = (7, 8, 9, 11)
+RECOVERY_MODES = ("speculative", "after")
 
 
 def _lagrange(index, s):
@@ -89,9 +109,9 @@ def _error_of(err):
         return None
     name, fields = _VARIANTS[err.variant]
     vals = {f: (bool(err.f[k]) if f in _BOOL_FIELDS else int(err.f[k])) for k, f in enumerate(fields)}
-    if err.panic:
-        return FsDkrPanic(f"reference panics at {name}")
-    return FsDkrError(name, **vals)
+    e = FsDkrPanic(f"reference panics at {name}") if err.panic else FsDkrError(name, **vals)
+    e.code = err.variant
+    return e
 
 
 def _short_share_check(ctx, batch, msgs):
@@ -146,11 +166,73 @@ def _apply_share(local_key, new_dk, rec):
         raise FsDkrPanic("collect: li_vec index out of bounds (local_key.t > vss threshold)")
 
 
-def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_security=256, key_bits=2048):
-    """RefreshMessage::collect (refresh_message.rs:321-467)."""
+def _settle(err, applied, spec):
+    """The reference's order between the verification outcome (err, keys
+    applied) and the share recovery's (spec: the recovery tuple or the panic it
+    hits): a get_ciphertext_sum panic wins over every later check and precedes
+    every key write; a decryption / pk_vec panic comes after all checks."""
+    if isinstance(spec, _SumPanic) and (err is None or getattr(err, "code", None) in _AFTER_SUM):
+        return spec, 0
+    if err is None and isinstance(spec, Exception):
+        return spec, applied
+    return err, applied
+
+
+def _conclude(local_key, new_dk, msgs, joins, err, applied, spec):
+    """collect()'s side effects for one outcome; returns the error collect() raises (or None)."""
+    err, applied = _settle(err, applied, spec)
+    _apply_keys(local_key, msgs, joins, applied)
+    if err is None:
+        try:
+            _apply_share(local_key, new_dk, spec)
+        except FsDkrPanic as e:
+            err = e
+    return err
+
+
+def _needs_recovery(err):
+    return err is None or getattr(err, "code", None) in _AFTER_SUM
+
+
+def _recover_after(ctx, jobs, errs):
+    """recovery="after": decrypt only for the jobs whose checks all passed (the
+    reference's :439); jobs stopped by a later check still get their
+    get_ciphertext_sum panic, which the reference hits first."""
+    out = [None] * len(jobs)
+    live = []
+    for k, (job, err) in enumerate(zip(jobs, errs)):
+        if not _needs_recovery(err):
+            continue
+        if err is None:
+            live.append(k)
+            continue
+        try:
+            _recovery_plan(*job)
+        except _SumPanic as e:
+            out[k] = e
+        except Exception:   # a later (decryption / pk_vec) panic: the check's error comes first
+            pass
+    if live:
+        for k, r in zip(live, _speculative(ctx, [jobs[k] for k in live])):
+            out[k] = r
+    return out
+
+
+def _check_mode(recovery):
+    if recovery not in RECOVERY_MODES:
+        raise ValueError(f"recovery must be one of {RECOVERY_MODES}")
+
+
+def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_security=256, key_bits=2048,
+            recovery="speculative"):
+    """RefreshMessage::collect (refresh_message.rs:321-467).  `recovery`:
+    "speculative" (default) decrypts the new share while the proofs are verified;
+    "after" decrypts once every check has passed, as the reference does (:439)."""
+    _check_mode(recovery)
     ctx = _ctx(ctx)
     _whole_chip(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
+    job = (msgs, local_key, len(msgs) + len(joins))
     # stage 1 packs what the pipeline's longest job reads and starts it on the GPU;
     # the rest of the batch is packed while those chains run
     batch = CollectBatch(msgs, local_key, joins, m_security, key_bits, staged=True)
@@ -163,27 +245,31 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     else:
         ctx.collect_prepare(batch)
         ctx.collect_launch()
-        spec = _speculative(ctx, [(msgs, local_key, len(msgs) + len(joins))])[0]
-        verdicts = ctx.collect_finish(batch)
+        try:
+            if recovery == "speculative":
+                spec = _speculative(ctx, [job])[0]
+        finally:   # the batch never stays in flight
+            verdicts = ctx.collect_finish(batch)
     err, applied = _mapped(ctx, batch, msgs, verdicts)
-    _apply_keys(local_key, msgs, joins, applied)
+    if recovery == "after" or batch.header_only:
+        spec = _recover_after(ctx, [job], [err])[0]
+    err = _conclude(local_key, new_dk, msgs, joins, err, applied, spec)
     if err is not None:
         raise err
-    if isinstance(spec, Exception):
-        raise spec
-    _apply_share(local_key, new_dk, spec)
 
 
-def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
+def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="speculative"):
     """Many independent RefreshMessage::collect calls verified in ONE device pass
     (fsdkr_collect_prepare_multi; BASELINE configs[4]).  `sessions`: list of
     (refresh_messages, local_key, new_dk, join_messages).  Each session gets the
     reference's outcome on its own: returns a list with None (local_key
     updated as collect() does) or the FsDkrError / FsDkrPanic collect() would
     raise (local_key partially updated as collect() leaves it)."""
+    _check_mode(recovery)
     ctx = _ctx(ctx)
     _whole_chip(ctx)
     sess = [(list(r), lk, dk, list(j)) for r, lk, dk, j in sessions]
+    jobs = [(msgs, lk, len(msgs) + len(joins)) for msgs, lk, dk, joins in sess]
     # one gather across the sessions (SessionSet); sessions of another shape keep
     # their own batch, header-only ones are mapped without a device pass
     sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits, staged=True)
@@ -196,27 +282,24 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048):
     if live:
         ctx.collect_prepare_set(sset)
         ctx.collect_launch()
-        res = _speculative(ctx, [(sess[i][0], sess[i][1], len(sess[i][0]) + len(sess[i][3])) for i in live])
-        for i, r in zip(live, res):
-            specs[i] = r
-        verdicts = ctx.collect_finish_set(sset)
-    out = []
+        try:
+            if recovery == "speculative":
+                for i, r in zip(live, _speculative(ctx, [jobs[i] for i in live])):
+                    specs[i] = r
+        finally:   # the batch never stays in flight
+            verdicts = ctx.collect_finish_set(sset)
+    errs = []
     for i, (msgs, lk, dk, joins) in enumerate(sess):
         if i in sset.row:
             e = sset.first_error(i, verdicts)
-            err, applied = _error_of(e), e.keys_applied
+            errs.append((_error_of(e), e.keys_applied))
         else:
-            err, applied = _mapped(ctx, sset.batches[i], msgs, None)
-        _apply_keys(lk, msgs, joins, applied)
-        if err is None and isinstance(specs[i], Exception):
-            err = specs[i]
-        if err is None:
-            try:
-                _apply_share(lk, dk, specs[i])
-            except FsDkrPanic as e:
-                err = e
-        out.append(err)
-    return out
+            errs.append(_mapped(ctx, sset.batches[i], msgs, None))
+    late = [i for i in range(len(sess)) if recovery == "after" or i not in sset.row]
+    for i, r in zip(late, _recover_after(ctx, [jobs[i] for i in late], [errs[i][0] for i in late])):
+        specs[i] = r
+    return [_conclude(lk, dk, msgs, joins, errs[i][0], errs[i][1], specs[i])
+            for i, (msgs, lk, dk, joins) in enumerate(sess)]
 
 
 def _public_view(lk):
@@ -225,7 +308,8 @@ def _public_view(lk):
             tuple((s.N, s.g, s.ni) for s in lk.h1_h2_n_tilde_vec))
 
 
-def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=256, key_bits=2048):
+def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=256, key_bits=2048,
+                recovery="speculative"):
     """Every party's RefreshMessage::collect over the same broadcast messages,
     with the proofs verified ONCE.  In the reference each
     party runs collect() and re-verifies the same n^2 proofs (test.rs:328-331);
@@ -235,6 +319,7 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
     decrypts its own ciphertexts).  `parties`: list of (local_key, new_dk).
     Returns one outcome per party, as collect_many does: None (local_key
     updated) or the FsDkrError / FsDkrPanic collect() would raise."""
+    _check_mode(recovery)
     ctx = _ctx(ctx)
     _whole_chip(ctx)
     msgs, joins = list(refresh_messages), list(join_messages)
@@ -248,26 +333,23 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
         if batch.ga_ready:
             ctx.collect_prestart(batch)
         batch.complete()
+        jobs = [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members]
         specs = [None] * len(members)
         verdicts = None
         if not batch.header_only:
             ctx.collect_prepare(batch)
             ctx.collect_launch()
-            specs = _speculative(ctx, [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members])
-            verdicts = ctx.collect_finish(batch)
+            try:
+                if recovery == "speculative":
+                    specs = _speculative(ctx, jobs)
+            finally:   # the batch never stays in flight
+                verdicts = ctx.collect_finish(batch)
         err, applied = _mapped(ctx, batch, msgs, verdicts)
+        if recovery == "after" or batch.header_only:
+            specs = _recover_after(ctx, jobs, [err] * len(jobs))
         for p, spec in zip(members, specs):
             lk, dk = parties[p]
-            _apply_keys(lk, msgs, joins, applied)
-            e = err
-            if e is None and isinstance(spec, Exception):
-                e = spec
-            if e is None:
-                try:
-                    _apply_share(lk, dk, spec)
-                except FsDkrPanic as x:
-                    e = x
-            out[p] = e
+            out[p] = _conclude(lk, dk, msgs, joins, err, applied, spec)
     return out
 
 
@@ -308,9 +390,17 @@ def _speculative(ctx, jobs):
             continue
         try:
             sig = ctx.paillier_decrypt_many(cts, kidx, ps, qs, w)
-        except ValueError as e:   # a ciphertext wider than N^2 (ints_to_limbs)
-            for j, _, _ in owners:
-                plans[j] = FsDkrPanic(f"share recovery: {e}")
+        except (ValueError, FsdkrError):
+            # a ciphertext wider than N^2 (ints_to_limbs) or a degenerate key the
+            # batched decryption refuses (p == q, p == 1, even p): decrypt each
+            # job on its own so one bad key fails only its own session
+            for j, at, cnt in owners:
+                lk = jobs[j][1]
+                try:
+                    sig_of[j] = ctx.paillier_decrypt_many(plans[j]["cts"], [0] * cnt, [lk.paillier_dk.p],
+                                                          [lk.paillier_dk.q], w)
+                except (ValueError, FsdkrError) as e:
+                    plans[j] = FsDkrPanic(f"share recovery: Paillier::decrypt ({e})")
             continue
         for j, at, cnt in owners:
             sig_of[j] = sig[at:at + cnt]
@@ -357,10 +447,20 @@ def _recovery_plan(msgs, local_key, n_new):
     sum_j l_j * Dec(c_j) mod N: decryption is a homomorphism on units of
     Z_{N^2}, so this equals the reference's decryption of prod_j c_j^l_j *
     Enc(0) (the Enc(0) factor only re-randomises)."""
-    t_vss = local_key.vss_scheme.threshold
-    indices = [msgs[j].old_party_index - 1 for j in range(t_vss + 1)]
-    li = [_lagrange(indices[j], indices) for j in range(t_vss + 1)]
-    cts = [msgs[j].points_encrypted_vec[local_key.i - 1] for j in range(t_vss + 1)]
+    try:   # get_ciphertext_sum (:367-373)
+        i = local_key.i
+        if i < 1:
+            raise IndexError("party index 0")
+        pkv = getattr(local_key, "paillier_key_vec", None)   # JoinMessage::collect passes its own ek
+        if pkv is not None:
+            pkv[i - 1]                                           # old_ek (:367)
+        cts_all = [m.points_encrypted_vec[i - 1] for m in msgs]  # every message's ciphertext (:202-204)
+        t_vss = local_key.vss_scheme.threshold
+        indices = [msgs[j].old_party_index - 1 for j in range(t_vss + 1)]
+        li = [_lagrange(indices[j], indices) for j in range(t_vss + 1)]
+    except (IndexError, AttributeError, TypeError, FsDkrPanic) as e:
+        raise _SumPanic(f"get_ciphertext_sum: {e}") from None
+    cts = cts_all[:t_vss + 1]
     t_key = local_key.t
     terms = min(t_key, t_vss) + 1
     pts = [[msgs[j].points_committed_vec[i] for j in range(terms)] for i in range(n_new)]

@@ -114,33 +114,38 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
 
 
 def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, device=None, m_security=256,
-            key_bits=2048):
+            key_bits=2048, recovery="speculative"):
     """RefreshMessage::collect (refresh_message.rs:321-467) sharded over the ranks of
     `dist` (torch.distributed, initialised): every rank holds every message (the
     broadcast channel of README.md:19) and the same LocalKey; each verifies its
     slice, the verdict bytes are all-reduced once, and every rank returns the
     reference's outcome: None after updating `local_key` as collect() does, or
     raises the FsDkrError / FsDkrPanic collect() raises (with its partial
-    paillier_key_vec updates)."""
-    from .refresh import _apply_keys, _apply_share, _mapped, _speculative
+    paillier_key_vec updates).  `recovery` as in refresh.collect."""
+    from .refresh import _check_mode, _conclude, _mapped, _recover_after, _speculative
+    _check_mode(recovery)
     world, rank = dist.get_world_size(), dist.get_rank()
     msgs, joins = list(refresh_messages), list(join_messages)
     R, J = len(msgs), len(joins)
     n = R + J
     header = CollectBatch(msgs, local_key, joins, m_security, key_bits, header_only=True)
+    job = (msgs, local_key, n)
     spec = None
     if header.size_fail:
         merged = None
     else:
         b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True)
-        # share recovery on the recovery stream while the slice is verified
-        spec = _speculative(ctx, [(msgs, local_key, n)])[0]
-        v = ctx.collect_finish(b) if b is not None else None
+        v = None
+        try:
+            if recovery == "speculative":   # share recovery on the recovery stream while the slice is verified
+                spec = _speculative(ctx, [job])[0]
+        finally:   # the slice never stays in flight
+            if b is not None:
+                v = ctx.collect_finish(b)
         merged = MergedVerdicts(merge(dist, scatter(v, R, J, n, world, rank), device), R, J, n)
     err, applied = _mapped(ctx, header, msgs, merged)
-    _apply_keys(local_key, msgs, joins, applied)
+    if recovery == "after" or header.size_fail:
+        spec = _recover_after(ctx, [job], [err])[0]
+    err = _conclude(local_key, new_dk, msgs, joins, err, applied, spec)
     if err is not None:
         raise err
-    if isinstance(spec, Exception):
-        raise spec
-    _apply_share(local_key, new_dk, spec)

@@ -111,6 +111,41 @@ def mod_pow(base: int, exponent: int, modulus: int) -> int:
     return _powm(base % modulus, exponent, modulus)
 
 
+_POOL = None
+
+
+def pool():
+    """Shared thread pool for the oracle's independent checks: GMP mpz_powm runs
+    through ctypes, which releases the GIL, so per-proof checks overlap.  The
+    caller still consumes the results in the reference's order (the restated
+    semantics -- which check fails or panics first -- are unchanged)."""
+    global _POOL
+    if _POOL is None:
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+        try:
+            ncpu = len(os.sched_getaffinity(0))
+        except AttributeError:
+            ncpu = os.cpu_count() or 1
+        _POOL = ThreadPoolExecutor(max_workers=max(1, min(16, ncpu)))
+    return _POOL
+
+
+def outcome(fn, *args):
+    """Run fn(*args) and capture its result or exception: (True, value) / (False, exc)."""
+    try:
+        return True, fn(*args)
+    except Exception as e:  # re-raised by settle() at the point the reference would reach it
+        return False, e
+
+
+def settle(res):
+    ok, v = res
+    if not ok:
+        raise v
+    return v
+
+
 def mod_inv(a: int, modulus: int):
     """curv BigInt::mod_inv -> GMP mpz_invert; None when gcd(a, m) != 1."""
     if modulus < 1:

@@ -238,19 +238,40 @@ def collect(msgs: List[RefreshMessage], local_key: LocalKey, new_dk: paillier.De
     and the pk_vec insert quirk).  Raises FsDkrError / PanicError."""
     new_n = len(msgs) + len(joins)
     validate_collect(msgs, local_key.t, new_n)
-    for m in msgs:
-        for i in range(new_n):
-            st = pdl.PDLwSlackStatement(m.points_encrypted_vec[i], local_key.paillier_key_vec[i],
-                                        m.points_committed_vec[i], ec.G, local_key.h1_h2_n_tilde_vec[i].g,
-                                        local_key.h1_h2_n_tilde_vec[i].ni, local_key.h1_h2_n_tilde_vec[i].N)
-            try:
-                pdl.verify(m.pdl_proof_vec[i], st)
-            except pdl.PDLwSlackError as e:
-                raise FsDkrError("PDLwSlackProof", is_u1_eq=e.flags[0], is_u2_eq=e.flags[1], is_u3_eq=e.flags[2])
-            if i >= len(m.range_proofs):
-                raise bigint.PanicError("collect: range_proofs[i] out of bounds")
-            if not range_proofs.verify(m.range_proofs[i], st.ciphertext, st.ek, local_key.h1_h2_n_tilde_vec[i]):
-                raise FsDkrError("RangeProof", party_index=i)
+    # the n^2 pair checks are independent: statements are built in the reference's
+    # order (stopping where building one fails), verified concurrently, and their
+    # outcomes consumed in that same order below
+    jobs, build_err = [], None
+    try:
+        for m in msgs:
+            for i in range(new_n):
+                st = pdl.PDLwSlackStatement(m.points_encrypted_vec[i], local_key.paillier_key_vec[i],
+                                            m.points_committed_vec[i], ec.G, local_key.h1_h2_n_tilde_vec[i].g,
+                                            local_key.h1_h2_n_tilde_vec[i].ni, local_key.h1_h2_n_tilde_vec[i].N)
+                jobs.append((m, i, st))
+    except Exception as e:
+        build_err = e
+
+    def _pair(job):
+        m, i, st = job
+        r_pdl = bigint.outcome(lambda: pdl.verify(m.pdl_proof_vec[i], st))
+        r_rng = None
+        if r_pdl[0] and i < len(m.range_proofs):
+            r_rng = bigint.outcome(range_proofs.verify, m.range_proofs[i], st.ciphertext, st.ek,
+                                   local_key.h1_h2_n_tilde_vec[i])
+        return r_pdl, r_rng
+
+    for (m, i, st), (r_pdl, r_rng) in zip(jobs, bigint.pool().map(_pair, jobs)):
+        try:
+            bigint.settle(r_pdl)
+        except pdl.PDLwSlackError as e:
+            raise FsDkrError("PDLwSlackProof", is_u1_eq=e.flags[0], is_u2_eq=e.flags[1], is_u3_eq=e.flags[2])
+        if i >= len(m.range_proofs):
+            raise bigint.PanicError("collect: range_proofs[i] out of bounds")
+        if not bigint.settle(r_rng):
+            raise FsDkrError("RangeProof", party_index=i)
+    if build_err is not None:
+        raise build_err
     for m in msgs:
         if not ring_pedersen.verify(m.ring_pedersen_proof, m.ring_pedersen_statement, M):
             raise FsDkrError("RingPedersenProofError")

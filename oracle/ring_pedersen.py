@@ -67,13 +67,16 @@ def verify(pf: RingPedersenProof, st: RingPedersenStatement, M: int) -> bool:
     if len(pf.A) < M:
         raise bigint.PanicError("RingPedersenProof: A shorter than M")
     eb = bigint.to_bytes(chain_bigint(*pf.A[:M]))
+    # the M exponentiations T^Z_i are independent: computed concurrently, consumed in order
+    todo = min(M, len(pf.Z), 8 * len(eb))
+    lhs_all = list(bigint.pool().map(lambda z: bigint.outcome(bigint.mod_pow, st.T, z, st.N), pf.Z[:todo]))
     for i in range(M):
         if i >= 8 * len(eb):
             raise bigint.PanicError("RingPedersenProof: challenge shorter than M bits (BitVec index)")
         bit = (eb[i >> 3] >> (i & 7)) & 1
         if i >= len(pf.Z):
             raise bigint.PanicError("RingPedersenProof: Z shorter than M")
-        lhs = bigint.mod_pow(st.T, pf.Z[i], st.N)
+        lhs = bigint.settle(lhs_all[i])
         rhs = bigint.mod_mul(pf.A[i], bigint.mod_pow(st.S, bit, st.N), st.N)
         if lhs != rhs:
             return False

@@ -262,3 +262,32 @@ def test_prestart_hit_and_miss(gpu_ctx):
     with pytest.raises(RuntimeError):
         gpu_ctx.collect_prestart(b3)
     gpu_ctx.collect_finish(b3.complete())
+
+
+def test_prestart_drops_a_plan_that_reads_it(gpu_ctx):
+    """A prepared batch that consumed a prestart reads its s^N rows and fixed-base
+    tables in place; a later prestart (of another batch) overwrites those buffers,
+    so it drops that plan: running it again is refused instead of reading the other
+    batch's rows."""
+    from fsdkr.batch import CollectBatch
+    keys, msgs, dks, _ = _dkr(1, 3, "prestart-drop")
+    lk = keys[0]
+    a = CollectBatch(msgs, lk, [], 256, KB, staged=True)
+    gpu_ctx.collect_prestart(a)
+    a.complete()
+    gpu_ctx.collect_prepare(a)
+    v = gpu_ctx.collect_run(a)
+    assert (v.pdl & 7 == 7).all()
+    bad = copy.deepcopy(msgs)
+    p = bad[0].pdl_proof_vec[1]
+    bad[0].pdl_proof_vec[1] = dataclasses.replace(p, s2=p.s2 + 1)
+    gpu_ctx.collect_prestart(CollectBatch(bad, lk, [], 256, KB, staged=True))
+    with pytest.raises(RuntimeError):
+        gpu_ctx.collect_run(a)
+    # the prestart itself is intact: a prepare of its batch consumes it
+    b = CollectBatch(bad, lk, [], 256, KB)
+    gpu_ctx.collect_prepare(b)
+    v2 = gpu_ctx.collect_run(b)
+    want = [7] * 9
+    want[1] = 7 & ~2
+    assert [int(x) & 7 for x in v2.pdl] == want

@@ -288,3 +288,104 @@ def test_even_dlog_modulus(gpu_ctx):
     p = j3.composite_dlog_proof_base_h2
     j3.composite_dlog_proof_base_h2 = CompositeDLogProof((p.x + Nt) % N2, p.y)
     _check(gpu_ctx, msgs, keys[1], dks[1], [j3], expect="DLogProofValidation")
+
+
+# ------------------------------------------------ share recovery in the order --
+def _bad_ck(msgs, k):
+    m2 = copy.deepcopy(msgs)
+    sv = m2[k].dk_correctness_proof.sigma_vec
+    m2[k].dk_correctness_proof = NiCorrectKeyProof((sv[0] + 1,) + tuple(sv[1:]))
+    return m2
+
+
+def test_ciphertext_sum_panic_precedes_later_checks(gpu_ctx, dkr5):
+    """get_ciphertext_sum (refresh_message.rs:367-373) runs after the ring-Pedersen
+    checks and before the correct-key / moduli checks and the paillier_key_vec
+    writes: with a broken correct-key proof AND a LocalKey whose VSS threshold asks
+    for more messages than there are (refresh_messages[i] out of bounds), or whose
+    own index is past the ciphertext vectors, the reference panics and writes no
+    key.  Same on both orders of share recovery."""
+    from fsdkr import refresh
+    keys, msgs, dks, _ = dkr5
+    m2 = _bad_ck(msgs, 2)
+    k1 = keys[0].clone()
+    k1.vss_scheme.threshold = len(msgs)
+    assert _check(gpu_ctx, m2, k1, dks[0], expect="panic")
+    k2 = keys[0].clone()
+    k2.i = len(msgs) + 3
+    assert _check(gpu_ctx, m2, k2, dks[0], expect="panic")
+    for recovery in refresh.RECOVERY_MODES:
+        kg = k1.clone()
+        with pytest.raises(refresh.FsDkrPanic):
+            refresh.collect(copy.deepcopy(m2), kg, dks[0], [], ctx=gpu_ctx, key_bits=KB, recovery=recovery)
+        assert [k.n for k in kg.paillier_key_vec] == [k.n for k in k1.paillier_key_vec]
+    # without the correct-key tamper the reference reaches the same panic
+    _check(gpu_ctx, msgs, k1, dks[0], expect="panic")
+    # a failing check BEFORE get_ciphertext_sum wins over its panic
+    m3 = copy.deepcopy(msgs)
+    p = m3[1].range_proofs[2]
+    m3[1].range_proofs[2] = type(p)(**{**p.__dict__, "s2": p.s2 + 1})
+    _check(gpu_ctx, m3, k1, dks[0], expect="RangeProof")
+
+
+def test_degenerate_local_dk_fails_alone(gpu_ctx, dkr5):
+    """A LocalKey whose Paillier dk the batched decryption refuses (p == q): that
+    collect fails with a panic, the batch is not left in flight (the next collect
+    runs), and in collect_all the other parties still get their keys."""
+    from fsdkr import refresh
+    from fsdkr.types import DecryptionKey
+    keys, msgs, dks, _ = dkr5
+    bad = keys[1].clone()
+    bad.paillier_dk = DecryptionKey(keys[1].paillier_dk.p, keys[1].paillier_dk.p)
+    with pytest.raises(refresh.FsDkrPanic):
+        refresh.collect(copy.deepcopy(msgs), bad, dks[1], [], ctx=gpu_ctx, key_bits=KB)
+    ok = keys[0].clone()
+    refresh.collect(copy.deepcopy(msgs), ok, dks[0], [], ctx=gpu_ctx, key_bits=KB)
+    ko = keys[0].clone()
+    protocol.collect(copy.deepcopy(msgs), ko, dks[0], [], Rng("a8"), KB)
+    _same_key(ko, ok)
+    # (the failed collect above applied every new ek before its decryption panic,
+    # as the reference does: a fresh copy of the degenerate key for collect_all)
+    bad2 = keys[1].clone()
+    bad2.paillier_dk = DecryptionKey(keys[1].paillier_dk.p, keys[1].paillier_dk.p)
+    assert [k.n for k in bad.paillier_key_vec] == [m.ek.n for m in msgs]
+    parties = [(keys[0].clone(), dks[0]), (bad2, dks[1]), (keys[2].clone(), dks[2])]
+    out = refresh.collect_all(copy.deepcopy(msgs), parties, [], ctx=gpu_ctx, key_bits=KB)
+    assert out[0] is None and out[2] is None and isinstance(out[1], refresh.FsDkrPanic)
+    _same_key(ko, parties[0][0])
+
+
+def test_recovery_orders_agree(gpu_ctx, dkr5):
+    """recovery="after" (decrypt once the verdicts are in, refresh_message.rs:439)
+    and the default speculative recovery give the same LocalKey and the same
+    error with the same side effects, for collect, collect_all and collect_many."""
+    from fsdkr import refresh
+    keys, msgs, dks, _ = dkr5
+    outs = {}
+    for recovery in refresh.RECOVERY_MODES:
+        k = keys[3].clone()
+        refresh.collect(copy.deepcopy(msgs), k, dks[3], [], ctx=gpu_ctx, key_bits=KB, recovery=recovery)
+        bad = keys[3].clone()
+        e = None
+        try:
+            refresh.collect(_bad_ck(msgs, 4), bad, dks[3], [], ctx=gpu_ctx, key_bits=KB, recovery=recovery)
+        except refresh.FsDkrError as x:
+            e = (x.variant, x.fields)
+        parties = [(keys[i].clone(), dks[i]) for i in range(3)]
+        res = refresh.collect_all(copy.deepcopy(msgs), parties, [], ctx=gpu_ctx, key_bits=KB, recovery=recovery)
+        sess = [(copy.deepcopy(msgs), keys[i].clone(), dks[i], []) for i in (0, 4)]
+        many = refresh.collect_many(sess, ctx=gpu_ctx, key_bits=KB, recovery=recovery)
+        outs[recovery] = (k, e, [p[0] for p in parties], res, [s[1] for s in sess], many,
+                          [x.n for x in bad.paillier_key_vec])
+    a, b = outs["speculative"], outs["after"]
+    _same_key(a[0], b[0])
+    assert a[1] == b[1] == ("PaillierVerificationError", {"party_index": 5})
+    assert a[6] == b[6]
+    for x, y in zip(a[2], b[2]):
+        _same_key(x, y)
+    assert a[3] == b[3] == [None] * 3
+    for x, y in zip(a[4], b[4]):
+        _same_key(x, y)
+    assert a[5] == b[5] == [None, None]
+    with pytest.raises(ValueError):
+        refresh.collect(msgs, keys[0].clone(), dks[0], [], ctx=gpu_ctx, recovery="later")
