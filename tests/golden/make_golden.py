@@ -14,7 +14,10 @@ Fixtures (gzip JSON, codec.py):
   transcript_t2_n5_kb1024.json.gz   keygen + 5 RefreshMessages, outcome of collect() for
                                     every party, and the tamper table (one vector per
                                     FsDkrError variant collect() can return, PDL x+1)
-  transcript_t1_n3_kb2048.json.gz   the same at the reference's PAILLIER_KEY_SIZE (lib.rs:26)
+  transcript_t2_n5_kb2048.json.gz   the same t=2 n=5 transcript and tamper table at the
+                                    reference's PAILLIER_KEY_SIZE (lib.rs:26; BASELINE configs[0])
+                                    (python make_golden.py t2n5-2048)
+  transcript_t1_n3_kb2048.json.gz   a t=1 n=3 transcript at PAILLIER_KEY_SIZE
   transcript_join_t1_n4_kb1024.json.gz  replace() + JoinMessage: collect() of an old party,
                                     JoinMessage::collect() of the joiner, join-path tampers
   job1_kb2048.json.gz               Paillier encryption with chosen randomness (job 1)
@@ -282,7 +285,11 @@ def main():
     if sys.argv[1:] == ["sampled"]:    # only the n=16 sampled-pairs fixture
         codec.save("sampled_pairs_t8_n16_kb2048.json.gz", sampled_fixture())
         return
+    if sys.argv[1:] == ["t2n5-2048"]:  # only the configs[0] transcript at 2048-bit keys
+        codec.save("transcript_t2_n5_kb2048.json.gz", refresh_fixture(2, 5, "golden-t2n5-2048", 2048, True))
+        return
     codec.save("transcript_t2_n5_kb1024.json.gz", refresh_fixture(2, 5, "golden-t2n5", 1024, True))
+    codec.save("transcript_t2_n5_kb2048.json.gz", refresh_fixture(2, 5, "golden-t2n5-2048", 2048, True))
     codec.save("transcript_t1_n3_kb2048.json.gz", refresh_fixture(1, 3, "golden-t1n3-2048", 2048, False))
     codec.save("transcript_join_t1_n4_kb1024.json.gz", join_fixture("golden-join", 1024))
     codec.save("job1_kb2048.json.gz", job1_fixture())

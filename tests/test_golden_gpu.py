@@ -18,7 +18,7 @@ import codec  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-TRANSCRIPTS = ["transcript_t2_n5_kb1024.json.gz", "transcript_t1_n3_kb2048.json.gz",
+TRANSCRIPTS = ["transcript_t2_n5_kb1024.json.gz", "transcript_t2_n5_kb2048.json.gz", "transcript_t1_n3_kb2048.json.gz",
                "transcript_join_t1_n4_kb1024.json.gz"]
 
 
@@ -94,7 +94,7 @@ def test_join_collect_matches_golden(gpu_ctx):
 def test_ring_pedersen_and_feldman_entry_points(gpu_ctx):
     """The stand-alone C ABI checks on the fixture's messages (valid + tampered)."""
     import dataclasses
-    raw, cls, d = _load("transcript_t2_n5_kb1024.json.gz")
+    raw, cls, d = _load("transcript_t2_n5_kb2048.json.gz")
     msgs = d["msgs"]
     st = [m.ring_pedersen_statement for m in msgs]
     pf = [m.ring_pedersen_proof for m in msgs]

@@ -15,7 +15,7 @@ import codec  # noqa: E402
 from oracle import bigint, paillier, protocol  # noqa: E402
 from oracle.rng import Rng  # noqa: E402
 
-TRANSCRIPTS = ["transcript_t2_n5_kb1024.json.gz", "transcript_t1_n3_kb2048.json.gz",
+TRANSCRIPTS = ["transcript_t2_n5_kb1024.json.gz", "transcript_t2_n5_kb2048.json.gz", "transcript_t1_n3_kb2048.json.gz",
                "transcript_join_t1_n4_kb1024.json.gz"]
 
 
