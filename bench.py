@@ -72,24 +72,31 @@ def collect_work(R, J, n, M=256, k=64):
         J * 2 * (w_modexp(k, b + 512) + w_modexp(k, 256))
 
 
-def collect_issued(R, J, n, M=256, w=6):
+def collect_issued(R, J, n, M=256, w=6, k=64):
     """MACs the GPU actually issues per collect: collect_work with the bases
     shared across exponents (h1_i, h2_i per receiver, ring-Pedersen T per
     message) evaluated by fixed-base BGMW windowing (fixedbase.hip): ceil(L/w) +
     2^w - 1 products per exponent plus one L-squaring table chain per base.
     Reported beside the algorithmic figure so the saving is not read as kernel
-    efficiency."""
-    k = 64
+    efficiency.  k = limbs of N."""
     mm = 2 * k * k + k
+    b = 32 * k
+    s1, s3 = 769, b + 768
 
     def fb(bits):
         return ((bits + w - 1) // w + (1 << w) - 1) * mm
 
-    var = collect_work(R, J, n, M)
-    var -= R * n * 2 * (w_modexp(k, 769) + w_modexp(k, 2816)) + (R + J) * M * w_modexp(k, 2048)
-    fixed = R * n * 2 * (fb(769) + fb(2816)) + (R + J) * M * fb(2048)
-    tables = (n * (769 + 2816) + (R + J) * 2048) * mm
+    var = collect_work(R, J, n, M, k)
+    var -= R * n * 2 * (w_modexp(k, s1) + w_modexp(k, s3)) + (R + J) * M * w_modexp(k, b)
+    fixed = R * n * 2 * (fb(s1) + fb(s3)) + (R + J) * M * fb(b)
+    tables = (n * (s1 + s3) + (R + J) * b) * mm
     return var + fixed + tables
+
+
+def efficiency(work, issued, seconds, world=1):
+    """Algorithmic and issued MAC rates of a timed step as fractions of the peak."""
+    return {"algorithmic_mac_per_step": work, "frac_of_peak": work / seconds / PEAK_MAC / world,
+            "issued_mac_per_step": issued, "issued_frac_of_peak": issued / seconds / PEAK_MAC / world}
 
 
 def cpu_baseline(batch, verdict_ref, proofs, threads, seconds_budget=12.0):
@@ -294,7 +301,41 @@ def sessions_bench(ctx, count, steps, seed):
                         f"(BASELINE configs[4]), one device pass per step", "sessions": count,
             "proofs_per_step": proofs, "steps": steps, "ms_per_step": el * 1e3, "value": proofs / el,
             "unit": "proofs/s", "sessions_per_s": count / el, "workload_gen_s": gen_s,
+            "collect_efficiency": efficiency(count * collect_work(3, 0, 3, k=96),
+                                             count * collect_issued(3, 0, 3, k=96), el),
             "data": "synthetic (seeded GPU prover; keys are distinct products of pairs from a shared prime pool)"}
+
+
+def config3_bench(ctx, steps, seed, unique=16, n=256, t=128):
+    """BASELINE configs[3] (the north_star target): RefreshMessage::collect at n = 256,
+    t = 128, 2048-bit keys, 65 536 PDL + 65 536 Alice proofs + 256 ring-Pedersen +
+    256 correct-key proofs verified in ONE batched pass on ONE GPU (the whole
+    collect() call per step, as the headline).  The prover side generates
+    `unique` distinct messages and tiles them to n senders
+    (synth.synth_collect_tiled): every pair is still verified on its own, only
+    the workload generation is shortened."""
+    import torch
+    from fsdkr import refresh, synth
+    tg = time.perf_counter()
+    msgs, joins, lk = synth.synth_collect_tiled(ctx, n, t, seed, unique)
+    gen_s = time.perf_counter() - tg
+    keys = [copy.deepcopy(lk) for _ in range(steps + 1)]
+    refresh.collect(msgs, keys[0], lk.paillier_dk, joins, ctx=ctx)   # warm-up + correctness gate
+    assert keys[0].x_i != lk.x_i and len(keys[0].pk_vec) == n, "collect() did not update the LocalKey"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        refresh.collect(msgs, keys[s + 1], lk.paillier_dk, joins, ctx=ctx)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    proofs = proofs_of(n, 0, n)
+    return {"workload": f"RefreshMessage::collect n={n} t={t}: {n} refresh messages, M=256, 2048-bit N "
+                        f"(BASELINE configs[3], the north_star target) on ONE GPU; one step = the whole collect() "
+                        f"call", "n": n, "t": t, "proofs_per_step": proofs, "steps": steps, "ms_per_step": el * 1e3,
+            "value": proofs / el, "unit": "proofs/s", "workload_gen_s": gen_s,
+            "collect_efficiency": efficiency(collect_work(n, 0, n), collect_issued(n, 0, n), el),
+            "data": f"synthetic (seeded GPU prover); {unique} distinct refresh messages tiled to {n} senders, "
+                    f"every pair verified independently"}
 
 
 def main():
@@ -312,6 +353,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sessions", type=int, default=1024, help="configs[4] sessions (0: skip)")
     ap.add_argument("--session-steps", type=int, default=2)
+    ap.add_argument("--config3-steps", type=int, default=2, help="configs[3] n=256 whole-call steps (0: skip)")
     ap.add_argument("--unique-msgs", type=int, default=0,
                     help="generate U distinct refresh messages and tile them to n (n = 256 run; the verifier "
                          "still checks every pair)")
@@ -445,6 +487,7 @@ def main():
             cpu = cpu_baseline_python(msgs, joins, lk, 200)
             cpu["cpp_unavailable"] = str(e)
     s4 = sessions_bench(ctx, a.sessions, a.session_steps, a.seed + 4) if a.sessions and world == 1 else None
+    c3 = config3_bench(ctx, a.config3_steps, a.seed + 3) if a.config3_steps and world == 1 and n != 256 else None
     kg = keygen_bench(ctx) if world == 1 else None
     W_collect = collect_work(R, J, n)
     traffic, traffic_src = pmc_traffic(roof["count"])
@@ -482,6 +525,7 @@ def main():
                                / world,
                                "device_pipeline_frac_of_peak": W_collect / (ph["device_pipeline_ms"] * 1e-3) /
                                PEAK_MAC},
+        "config3": c3,
         "config4_sessions": s4,
         "keygen": kg,
         "workload_gen_s": gen_s,

@@ -125,11 +125,11 @@ std::vector<uint32_t> Ctx::cu_mask(uint32_t count, bool in) const {
   return m;
 }
 
-// masked: 0 none, 1 reserved CUs, 2 their complement, 3 the GA set, 4 its complement
+// masked: 0 none, 3 the GA set, 4 its complement
 static hipStream_t make_stream(const Ctx* c, int masked) {
   hipStream_t s = nullptr;
   if (masked) {
-    std::vector<uint32_t> m = masked <= 2 ? c->cu_mask(c->reserve_cus, masked == 1) : c->cu_mask(c->ga_cus, masked == 3);
+    std::vector<uint32_t> m = c->cu_mask(c->ga_cus, masked == 3);
     if (hipExtStreamCreateWithCUMask(&s, (uint32_t)m.size(), m.data()) == hipSuccess) return s;
     s = nullptr;
   }
@@ -139,14 +139,8 @@ static hipStream_t make_stream(const Ctx* c, int masked) {
 
 hipStream_t Ctx::side_stream(int k) {
   k %= NSIDE;
-  if (!side[k]) side[k] = make_stream(this, ga_cus ? (k == 0 ? 3 : 4) : (reserve_cus && reserve_excl) ? 2 : 0);
+  if (!side[k]) side[k] = make_stream(this, ga_cus ? (k == 0 ? 3 : 4) : 0);
   return side[k] ? side[k] : stream;
-}
-
-hipStream_t Ctx::crit_stream() {
-  if (!reserve_cus) return nullptr;
-  if (!crit) crit = make_stream(this, 1);
-  return crit;
 }
 
 int Ctx::sync() {
@@ -355,16 +349,7 @@ int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out) {
   }
   c->device = dev;
   c->timing = cfg && (cfg->flags & FSDKR_CFG_TIMING);
-  if (const char* e = getenv("FSDKR_RESERVE_CUS")) {
-    const int r = atoi(e);
-    c->reserve_cus = (r > 0 && r % 8 == 0 && r <= 128) ? (uint32_t)r : 0u;
-  }
-  if (const char* e = getenv("FSDKR_RESERVE_EXCL")) c->reserve_excl = atoi(e) != 0;
-  if (const char* e = getenv("FSDKR_GA_CUS")) {
-    const int r = atoi(e);
-    c->ga_cus = (r > 0 && r % 8 == 0 && r <= 224 && !c->reserve_cus) ? (uint32_t)r : 0u;
-  }
-  if (!(c->stream = make_stream(c, c->ga_cus ? 4 : 0))) {
+  if (!(c->stream = make_stream(c, 0))) {
     delete c;
     return FSDKR_E_HIP;
   }
@@ -380,7 +365,6 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
     if (kv.second.ptr) (void)hipFree(kv.second.ptr);
   for (auto& sd : c->side)
     if (sd) (void)hipStreamDestroy(sd);
-  if (c->crit) (void)hipStreamDestroy(c->crit);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -407,10 +391,6 @@ int fsdkr_ctx_set_cu_split(fsdkr_ctx* ctx, uint32_t ga_cus) {
   if (c->ga_cus == ga_cus) return FSDKR_OK;
   int rc = c->sync();
   if (rc) return rc;
-  if (c->reserve_cus) {
-    c->fail("fsdkr_ctx_set_cu_split: FSDKR_RESERVE_CUS is set");
-    return FSDKR_E_ARG;
-  }
   // every stream is re-created lazily with the new masks
   if ((rc = c->hip_check(hipDeviceSynchronize(), "sync"))) return rc;
   for (auto& sd : c->side)

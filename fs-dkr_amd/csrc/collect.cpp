@@ -10,10 +10,11 @@
 // pass: the sessions' pairs, receivers, messages and joins are concatenated
 // into a single image (little-endian u32 limbs, one fixed width per field);
 // every descriptor addresses rows of that image.  Pipeline (streams in
-// launch()): pdl_hash, ped_hash -> binom -> modexp jobs (GA, GD, GC, J2, J5, FB)
+// launch()): ped_hash -> binom -> modexp jobs (GA, GD, GC, J2, J5, FB)
 // -> inverses -> eq_check / prod3 -> alice_hash; pdl_u1, Feldman and the 2-adic
 // checks of even moduli beside them -> one D2H of the verdict words (finish()).
 #include <hip/hip_runtime.h>
+#include <openssl/evp.h>
 
 #include <algorithm>
 #include <atomic>
@@ -71,6 +72,70 @@ inline bool is_odd(const uint32_t* p) { return (p[0] & 1u) != 0; }
 
 // to_bytes(x) absorbed for a small non-negative integer
 inline void absorb_u32(Sha256& h, uint32_t v) { h.bigint(&v, 1); }
+
+// curv BigInt::to_bytes of little-endian u32 limbs: the minimal big-endian
+// magnitude, zero as one 0x00 byte
+void put_bigint(std::vector<uint8_t>& out, const uint32_t* x, uint32_t n) {
+  int top = (int)n - 1;
+  while (top >= 0 && x[top] == 0) --top;
+  if (top < 0) {
+    out.push_back(0);
+    return;
+  }
+  int sh = 24;
+  while (sh > 0 && ((x[top] >> sh) & 0xffu) == 0) sh -= 8;
+  for (; sh >= 0; sh -= 8) out.push_back((uint8_t)(x[top] >> sh));
+  for (int k = top - 1; k >= 0; --k) {
+    const uint32_t v = x[k];
+    const uint8_t b[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
+    out.insert(out.end(), b, b + 4);
+  }
+}
+
+// BigInt::from_bytes(P.to_bytes(true)) re-encoded by to_bytes: 33 bytes for a
+// finite point (x limbs 0..7, y limbs 8..15, prefix 2 + y mod 2), 0x00 for infinity
+void put_point(std::vector<uint8_t>& out, const uint32_t* p16) {
+  bool inf = true;
+  for (int i = 0; i < 16; ++i) inf = inf && p16[i] == 0;
+  if (inf) {
+    out.push_back(0);
+    return;
+  }
+  out.push_back((uint8_t)(2 + (p16[8] & 1u)));
+  for (int i = 7; i >= 0; --i) {
+    const uint32_t v = p16[i];
+    const uint8_t b[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
+    out.insert(out.end(), b, b + 4);
+  }
+}
+
+// the secp256k1 generator G, compressed (zk_pdl_with_slack.rs:114: G.to_bytes(true))
+const uint8_t G_COMPRESSED[33] = {0x02, 0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0,
+                                  0x62, 0x95, 0xCE, 0x87, 0x0B, 0x07, 0x02, 0x9B, 0xFC, 0xDB, 0x2D,
+                                  0xCE, 0x28, 0xD9, 0x59, 0xF2, 0x81, 0x5B, 0x16, 0xF8, 0x17, 0x98};
+
+// SHA-256 digest as a 256-bit little-endian limb array (BigInt::from_bytes(digest))
+void digest_le(const uint8_t* d, uint32_t* e8) {
+  for (int i = 0; i < 8; ++i)
+    e8[i] = ((uint32_t)d[28 - 4 * i] << 24) | ((uint32_t)d[29 - 4 * i] << 16) | ((uint32_t)d[30 - 4 * i] << 8) |
+            (uint32_t)d[31 - 4 * i];
+}
+
+// One thread's SHA-256 context (OpenSSL: SHA-NI / AVX2 code paths where the CPU has them)
+struct HostSha {
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  std::vector<uint8_t> buf;
+  ~HostSha() { EVP_MD_CTX_free(ctx); }
+  bool digest(uint32_t* e8) {
+    uint8_t d[32];
+    unsigned int len = 0;
+    const bool ok = ctx && EVP_DigestInit_ex(ctx, EVP_sha256(), nullptr) == 1 &&
+                    EVP_DigestUpdate(ctx, buf.data(), buf.size()) == 1 && EVP_DigestFinal_ex(ctx, d, &len) == 1 &&
+                    len == 32;
+    if (ok) digest_le(d, e8);
+    return ok;
+  }
+};
 
 // f(begin, end) over [0, n) on up to host_threads() threads (inline when small)
 template <class F>
@@ -185,11 +250,11 @@ struct CollectPlan {
   size_t out_off = 0, total = 0;
   uint8_t* dev = nullptr;
   // input offsets used by launches
-  size_t o_Q, o_enc, o_pz, o_pu1, o_pu2, o_pu3, o_ps1, o_pA, o_az, o_ae, o_vss, o_NN, o_mods, o_ckmods, o_one;
+  size_t o_Q, o_enc, o_pz, o_pu1, o_pu2, o_pu3, o_ps1, o_pA, o_az, o_ae, o_vss, o_NN, o_mods, o_ckmods, o_one, o_epdl;
   size_t d_finfo = 0, d_p2 = 0;
   uint32_t n_mods_nl = 0, n_p2 = 0;
   // output offsets
-  size_t x_epdl, x_pbits, x_ppanic, x_Bpdl, x_gs1, x_invc, x_invz, x_unn, x_uzA, x_uzp, x_eq2, x_eq3, x_eqck, x_u,
+  size_t x_pbits, x_ppanic, x_Bpdl, x_gs1, x_invc, x_invz, x_unn, x_uzA, x_uzp, x_eq2, x_eq3, x_eqck, x_u,
       x_w, x_fel, x_pdlv, x_rng, x_p2;
   // modexp jobs: 0 GA (nn long), 1 GD (nl: DLog), 2 J2 (nn short), 3 J5 (nl short), 4 GC (ckl: correct key)
   static constexpr int NJOB = 5;
@@ -208,6 +273,7 @@ struct CollectPlan {
   std::vector<uint32_t> ped_zlen;          // readable Z entries (M: all); A short: ped_mode 2
   std::vector<uint8_t> ck_short;           // sigma_vec shorter than 11 (or n = 0): zk-paillier panics
   std::vector<uint8_t> ck_one;             // n = 1: the proof verifies trivially
+  std::vector<uint32_t> e_pdl;             // PDL challenges [P][8] (host, prepare), also uploaded at o_epdl
   // s^N mod N^2 results computed by fsdkr_collect_prestart (ga_hit): the eq / prod3
   // operands read them from the prestart buffer once ga_done has fired
   bool ga_hit = false;
@@ -250,8 +316,7 @@ struct GaPre {
   std::vector<uint32_t> ntilde, h1, h2, T, pedmod;   // bases, and the T_m moduli rows
   uint32_t Mt = 0, fb_w = 0, bits_h1 = 0, bits_h2 = 0, bits_z = 0, fb_entries = 0;
   uint32_t* fb_table = nullptr;
-  hipEvent_t fb_done = nullptr;     // every table (group B: the h2 chains)
-  hipEvent_t fb_done_a = nullptr;   // group A: h1 and T chains
+  hipEvent_t fb_done = nullptr;     // every table built
 };
 
 void free_ga_pre(Ctx* c) {
@@ -259,7 +324,6 @@ void free_ga_pre(Ctx* c) {
   if (g && g->done) (void)hipEventDestroy(g->done);
   if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
-  if (g && g->fb_done_a) (void)hipEventDestroy(g->fb_done_a);
   delete g;
   c->ga_pre = nullptr;
 }
@@ -314,8 +378,6 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   // exponent bit bounds: exact from the packed exponents, else their slot widths
   // (a slim stage 1 leaves s1 / s3 / Z to stage 2; tables at most 31 bits longer)
   const bool exact_s = b->pdl_s1 && b->pdl_s3 && b->rp_s1 && b->rp_s2;
-  const char* pfe = getenv("FSDKR_PRE_FB");   // 0: no table prestart (tuning)
-  if (pfe && pfe[0] == '0') return FSDKR_OK;
   const uint32_t nl = b->nl, Mt = b->n_refresh + b->n_join, M = b->m_security;
   for (uint32_t i = 0; i < n; ++i)
     if (!is_odd(b->recv_ntilde + (size_t)i * nl)) return FSDKR_OK;
@@ -366,48 +428,24 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   memcpy(img.data() + o_bm, L.mod.data(), (size_t)nb * 4);
   memcpy(img.data() + o_bt, L.toff.data(), (size_t)nb * 4);
   memcpy(img.data() + o_bh, L.h.data(), (size_t)nb * 4);
-  // group A (h1, T: shorter chains) beside group B (h2: the longest chain, top priority)
-  hipStream_t ts = c->crit_stream();
-  if (!ts) ts = c->side_stream(8);   // launch()'s table-chain stream
-  hipStream_t tsA = c->side_stream(1);   // launch()'s fixed-base exponent stream (idle until then)
+  // every table chain in one launch on launch()'s table-chain stream; launch()'s
+  // fixed-base exponent stream waits for it through fb_done
+  hipStream_t ts = c->side_stream(8);
   StreamScope scope(c, ts);
   int rc;
   if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, ts), "prestart fb H2D")) ||
       (rc = c->hip_check(hipStreamSynchronize(ts), "prestart fb H2D sync")))
     return rc;
-  // FSDKR_FB_WAIT_GA=1: the table chains start after GA's constants, i.e. right
-  // behind GA's chains (keeps GA dispatched first when stage 1 is quick)
-  if (const char* e = getenv("FSDKR_FB_WAIT_GA"); e && e[0] == '1' && g.ga_setup)
-    (void)hipStreamWaitEvent(ts, g.ga_setup, 0);
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl")))
     return rc;
   if (!g.fb_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done, hipEventDisableTiming), "event")))
     return rc;
-  if (!g.fb_done_a && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done_a, hipEventDisableTiming), "event")))
-    return rc;
-  (void)hipEventRecord(g.fb_done_a, ts);   // consts ready
-  (void)hipStreamWaitEvent(tsA, g.fb_done_a, 0);
   g.fb_table = reinterpret_cast<uint32_t*>(dev + o_tab);
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
-  const uint32_t nA = n + Mt;
-  const char* fse = getenv("FSDKR_FB_SPLIT");
-  if (fse && fse[0] == '1') {   // group A (h1, T) beside group B (h2) on its own stream
-    FbTableArgs tb{U64(o_bp) + nA, U32(o_bl) + nA, U32(o_bm) + nA, U32(o_bt) + nA, U32(o_bh) + nA, cons, g.fb_table,
-                   w, n, 3};
-    FbTableArgs ta{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nA, 2};
-    if ((rc = c->hip_check(launch_fb_table(nl, tb, ts), "prestart fb_table h2")) ||
-        (rc = c->hip_check(launch_fb_table(nl, ta, tsA), "prestart fb_table h1/T")))
-      return rc;
-    if ((rc = c->hip_check(hipEventRecord(g.fb_done_a, tsA), "event record"))) return rc;
-  } else {   // one launch on the table stream: the fixed-base exponent stream stays free
-    FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
-    if ((rc = c->hip_check(launch_fb_table(nl, tall, ts), "prestart fb_table"))) return rc;
-    if ((rc = c->hip_check(hipEventRecord(g.fb_done_a, ts), "event record"))) return rc;
-  }
-  // fb_done covers both groups: the B chain's stream waits for A's as well
-  (void)hipStreamWaitEvent(ts, g.fb_done_a, 0);
+  FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
+  if ((rc = c->hip_check(launch_fb_table(nl, tall, ts), "prestart fb_table"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.fb_done, ts), "event record"))) return rc;
   g.ntilde.assign(b->recv_ntilde, b->recv_ntilde + (size_t)n * nl);
   g.h1.assign(b->recv_h1, b->recv_h1 + (size_t)n * nl);
@@ -428,16 +466,11 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
 // the largest group that keeps it within about half the resident lanes
 // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
 // (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants) for latency.
-// FSDKR_COLLECT_GA_G overrides.  Used by the prestart and by launch().
+// Used by the prestart and by launch().
 static uint32_t ga_lanes(uint32_t count, uint32_t nn) {
-  static const uint32_t forced = [] {
-    const char* e = getenv("FSDKR_COLLECT_GA_G");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
   uint32_t g = 8;
   for (uint32_t x : {16u, kWideGroup})
     if ((uint64_t)count * x <= 65536u) g = x;
-  if (forced) g = forced;
   if (g == kWideGroup && nn != 128) g = 16;
   return g;
 }
@@ -568,11 +601,8 @@ static int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, ui
   if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
     return rc;
   (void)hipEventRecord(g.ga_setup, gs);   // GA's constants are ready
-  // issue priority 3 (FSDKR_PRE_GA_PRIO; 2 measured 1-2 ms slower per call,
-  // profiles/r02x_ab_full.jsonl)
-  const char* gpe = getenv("FSDKR_PRE_GA_PRIO");
-  const uint32_t ga_prio = gpe ? (uint32_t)atoi(gpe) : 3u;
-  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, group)))
+  // issue priority 3 (2 measured 1-2 ms slower per call, profiles/r02x_ab_full.jsonl)
+  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 3, group)))
     return rc;
   if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
@@ -731,12 +761,28 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   };
   std::vector<Maxes> tmax(host_threads() + 1);
   std::atomic<uint32_t> slot{0};
-  parallel_for(P, 1024, [&](size_t b0, size_t b1) {
+  // PDL challenges e = H(G, Q, c, z, u1, u2, u3) (zk_pdl_with_slack.rs:114-122) on the
+  // host threads of this scan: J2 (c^e), J5 (z^e) and pdl_u1 can start with the pipeline
+  std::vector<uint32_t>& EPDL = pl.e_pdl;
+  EPDL.assign((size_t)P * 8, 0u);
+  std::atomic<bool> sha_fail{false};
+  parallel_for(P, 256, [&](size_t b0, size_t b1) {
     Maxes mx;
+    HostSha sha;
     for (size_t p = b0; p < b1; ++p) {
       const Sess& x = pl.ss[sess_of_pair[p]];
       const fsdkr_collect_batch* b = x.b;
       const size_t lp = p - x.pbase;
+      const uint32_t w = b->nl;
+      sha.buf.clear();
+      sha.buf.insert(sha.buf.end(), G_COMPRESSED, G_COMPRESSED + 33);
+      put_point(sha.buf, b->commit + lp * 16);
+      put_bigint(sha.buf, b->enc + lp * 2 * w, 2 * w);
+      put_bigint(sha.buf, b->pdl_z + lp * w, w);
+      put_point(sha.buf, b->pdl_u1 + lp * 16);
+      put_bigint(sha.buf, b->pdl_u2 + lp * 2 * w, 2 * w);
+      put_bigint(sha.buf, b->pdl_u3 + lp * w, w);
+      if (!sha.digest(EPDL.data() + p * 8)) sha_fail = true;
       const uint32_t* Np = b->recv_n + (size_t)(lp % x.n) * b->nl;
       const uint32_t* s1 = b->pdl_s1 + lp * b->s1l;
       // s1 < N -> (N+1)^s1 mod N^2 = 1 + s1*N  (binomial, bit-identical)
@@ -766,7 +812,11 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
     mx.ae = std::max(mx.ae, t.ae);
     mx.big_s1 = mx.big_s1 || t.big_s1;
   }
-  clk.lap("pair scan");
+  clk.lap("pair scan + PDL challenges");
+  if (sha_fail) {
+    c->fail("fsdkr_collect_prepare: SHA-256 (OpenSSL EVP) failed");
+    return FSDKR_E_ARG;
+  }
   // correct-key: rho_j = mask_generation(len(n), H(n, salt, j)) mod n; primorial gcd.
   // ring-Pedersen modulus split N = 2^k m (even N: 2-adic half in pow2.hip); S mod m.
   std::vector<uint32_t> RHO((size_t)Mt * CK_M2 * ckl, 0u), CKMODS((size_t)Mt * ckl, 0u), CKEXP((size_t)Mt * ckl, 0u),
@@ -1004,6 +1054,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
     I.own_at(o_mods + (size_t)n * nl * 4, std::move(tail));
   }
   const size_t o_finfo = I.own(finfo);
+  const size_t o_epdl = I.own(EPDL);
   clk.lap("layout plan");
 
   // ---------------- device layout: outputs (offsets relative to the output region)
@@ -1013,7 +1064,6 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
     out_bytes = o + Img::al(bytes ? bytes : 1);
     return o;
   };
-  const size_t x_epdl = OUT((size_t)P * 8 * 4);
   const size_t x_pbits = OUT((size_t)Mt * MW * 4), x_ppanic = OUT((size_t)Mt * 4);
   const size_t x_Bpdl = OUT((size_t)P * nn * 4), x_gs1 = OUT((size_t)P * nn * 4);
   //   GA (nn, long)  = s2^N | s^N  [2P]  ++  (N+1)^s1 for s1 >= N  [<= P]
@@ -1113,14 +1163,14 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
         J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
       const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
-      if (which == 0) J2.add(cp, nn, DX(x_epdl + (size_t)p * 32), 8, 256, r);
+      if (which == 0) J2.add(cp, nn, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       else J2.add(cp, nn, DI(o_ae + (size_t)p * el * 4), el, mx.ae, r);
       // fixed bases (FB): h1^s1 -> J3 slot | h2^s3 (s2 for Alice) -> J4 slot;  J5: z^e
       const size_t slot = (size_t)which * P + p;
       if (which == 0) {
         FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
         fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
-        J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DX(x_epdl + (size_t)p * 32), 8, 256, r);
+        J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
         FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
@@ -1154,14 +1204,6 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
     });
   }
   clk.lap("desc rp");
-  // FSDKR_FB_SPLIT=1: group A's exponents start before the h2 tables are done.
-  // Measured 1-2 ms slower than one launch at n = 64 (the early group-A exponents
-  // compete with GA / J2 / J5 for the chip; profiles/r02x_ab_full.jsonl): off.
-  const char* fse = getenv("FSDKR_FB_SPLIT");
-  if (fse && fse[0] == '1') {
-    FB.split_bases = n + Mt;
-    FB.split_inst = (uint32_t)FB.count();
-  }
   for (const FbAdd& a : fb_later) FB.add(a.base, a.exp, a.elen, a.ebits, a.out);
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < CK_M2; ++k)  // correct-key sigma_k^n mod n
@@ -1227,8 +1269,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
       pl.fb_hit = true;
       pl.fb_pre.table = gp->fb_table;
       pl.fb_pre.entries = gp->fb_entries;
-      pl.fb_pre.ready_a = gp->fb_done_a;
-      pl.fb_pre.ready_b = gp->fb_done;
+      pl.fb_pre.ready = gp->fb_done;
       reinterpret_cast<GaPre*>(c->ga_pre)->fb_valid = false;   // consumed
     }
   }
@@ -1447,7 +1488,7 @@ static int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t 
   pl.d_p2 = d_p2;
   pl.n_p2 = n_p2;
   pl.n_mods_nl = n_mods_nl;
-  pl.x_epdl = x_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
+  pl.o_epdl = o_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
   // with a prestarted J1 the GA job is J9 alone, written where J9's rows live
   const size_t xs[CollectPlan::NJOB] = {pl.ga_hit ? x_J9 : x_GA, x_GD, x_J2, x_J5, x_GC};
   const size_t ds[CollectPlan::NJOB] = {d_GA, d_GD, d_J2, d_J5, d_GC};
@@ -1503,17 +1544,8 @@ static int collect_launch_impl(Ctx* c) {
   if ((rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn, "collect_nn"))) return rc;
   if ((rc = setup_moduli(c, nl, PI(pl.o_mods), pl.n_mods_nl, &cons_nl, "collect_nl"))) return rc;
   if ((rc = setup_moduli(c, pl.ckl, PI(pl.o_ckmods), Mt, &cons_ck, "collect_ck"))) return rc;
-  // GA lanes per instance: GA shares the chip with the other streams, so it takes
-  // the largest group that keeps it within about half the resident lanes
-  // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
-  // (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants) for latency.
-  // FSDKR_COLLECT_GA_G overrides.
-  // J2 / J5 (256-bit challenge exponents) lanes per instance: FSDKR_COLLECT_J2_G / _J5_G
-  auto env_group = [](const char* k, uint32_t dflt) -> uint32_t {
-    const char* e = getenv(k);
-    return e ? (uint32_t)atoi(e) : dflt;
-  };
-  const uint32_t j2_group = env_group("FSDKR_COLLECT_J2_G", 8), j5_group = env_group("FSDKR_COLLECT_J5_G", 8);
+  // J2 / J5 (256-bit challenge exponents): 8 lanes per instance
+  const uint32_t j2_group = 8, j5_group = 8;
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;
   if (ga_group == kWideGroup && pl.jcount[0] &&
@@ -1524,18 +1556,16 @@ static int collect_launch_impl(Ctx* c) {
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup
   //   side 8  : FB table chains (h1, h2, T: the longest dependent chain), top priority
   //   side 1  : FB schedules, then (after the tables) fixed-base exponents
-  //   side 7  : J5 + nl inverses instead of st when CUs are reserved (FSDKR_RESERVE_CUS)
   //   side 3  : ped_hash (serial SHA-256 chains, priority) -> 2-adic checks of even moduli
   //   side 4  : GD (DLog), GC (correct key) -> correct-key equalities
   //   side 6  : Feldman (secp256k1 Horner per pair)
-  //   st      : pdl_hash, binom x2 | fork | J5, nl inverses | join | eq, prod3, alice
+  //   st      : binom x2 | fork | J5, nl inverses | join | eq, prod3, alice  (the PDL
+  //             challenges come from prepare's host pass)
   //   side 2  :                    J2 (nn, 256-bit challenges) -> nn inverses
   //   side 5  :                    pdl_u1 (secp256k1)
   std::vector<hipEvent_t> done;
-  // issue-priority levels of the serial chains (tuning knob FSDKR_PRIO="GA,FB,GD,J5";
-  // measured defaults)
+  // issue-priority levels of the serial chains: GA, FB tables, GD/GC, J5 (measured)
   uint32_t prio[4] = {3, 3, 2, 1};
-  if (const char* e = getenv("FSDKR_PRIO")) sscanf(e, "%u,%u,%u,%u", &prio[0], &prio[1], &prio[2], &prio[3]);
   pl.fb.table_prio = prio[1];
   auto fork = [&](hipStream_t from, hipEvent_t* ev) -> int {
     int r = c->hip_check(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event");
@@ -1556,13 +1586,6 @@ static int collect_launch_impl(Ctx* c) {
     return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
                               tags[k], pr, group);
   };
-  // GA-first ordering (tuning knob FSDKR_GA_FIRST, bit mask): the throughput jobs
-  // fb_exp (1), J2 (2) and J5 (4) wait for GA
-  const uint32_t ga_first = [] {
-    const char* e = getenv("FSDKR_GA_FIRST");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  hipEvent_t ga_done = nullptr;
   // (1) chains that need only the inputs and the moduli constants start at once
   hipEvent_t consts_ready;
   if ((rc = fork(st, &consts_ready))) return rc;
@@ -1572,22 +1595,17 @@ static int collect_launch_impl(Ctx* c) {
     // small batches (multi-GPU shards): the h2 fixed-base table chain (2816
     // dependent squarings) is the critical path, so GA steps down one issue
     // priority level below it (8-way shard: 33.4 -> 31.7 ms, tools/ab_hwq.sh)
-    if (ga_group >= 16 && !getenv("FSDKR_PRIO")) prio[0] = 2;
+    if (ga_group >= 16) prio[0] = 2;
     const uint32_t* cga = (ga_group == kWideGroup) ? cons_nn_w : cons_nn;
     if ((rc = launch_group(0, ss, prio[0], ga_group, cga)) || (rc = join_later(ss))) return rc;
-    if (ga_first && (rc = fork(ss, &ga_done))) return rc;
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
     FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps};
-    hipStream_t ts = c->crit_stream();
-    if (!ts) ts = c->side_stream(8);   // own stream: the chain starts beside fb_sched
-    hipStream_t tsA = ss;   // group A's (h1, T) chains, then fb_sched / fb_exp behind them
+    hipStream_t ts = c->side_stream(8);   // own stream: the chain starts beside fb_sched
     (void)hipStreamWaitEvent(ts, consts_ready, 0);
-    (void)hipStreamWaitEvent(tsA, consts_ready, 0);
-    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, (ga_first & 1) ? ga_done : nullptr,
-                        pl.fb_hit ? &pl.fb_pre : nullptr, tsA)) ||
+    if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, pl.fb_hit ? &pl.fb_pre : nullptr)) ||
         (rc = join_later(ss)))
       return rc;
   }
@@ -1616,16 +1634,12 @@ static int collect_launch_impl(Ctx* c) {
   }
   {  // GD: DLog g^y / ni^e (few long chains); GC: correct-key sigma^n (2048-bit
      // exponents, Mt*11 instances) on a stream of its own, so the two latency-bound
-     // jobs run side by side (FSDKR_GC_STREAM=0: GC queued behind GD)
+     // jobs run side by side
     hipStream_t ss = c->side_stream(4);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    if ((rc = launch_group(1, ss, prio[2], 0, cons_nl))) return rc;
-    const char* gce = getenv("FSDKR_GC_STREAM");
-    if (!(gce && gce[0] == '0')) {
-      if ((rc = join_later(ss))) return rc;
-      ss = c->side_stream(9);
-      (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    }
+    if ((rc = launch_group(1, ss, prio[2], 0, cons_nl)) || (rc = join_later(ss))) return rc;
+    ss = c->side_stream(9);
+    (void)hipStreamWaitEvent(ss, consts_ready, 0);
     if ((rc = launch_group(4, ss, prio[2], 0, cons_ck))) return rc;
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqck), PI(pl.d_eqckm), cons_ck, PX(pl.x_pbits), DI(pl.o_one),
                   PX(pl.x_eqck), pl.n_eq_ck};
@@ -1634,15 +1648,7 @@ static int collect_launch_impl(Ctx* c) {
     c->mark("eq_check", false, ss);
     if (rc || (rc = join_later(ss))) return rc;
   }
-  // (2) PDL challenges, then the jobs that exponentiate by them
-  {
-    PdlHashArgs a{PI(pl.o_Q), PI(pl.o_enc), PI(pl.o_pz), PI(pl.o_pu1), PI(pl.o_pu2), PI(pl.o_pu3), nn, nl,
-                  PX(pl.x_epdl), P};
-    c->mark("pdl_hash", true);
-    rc = c->hip_check(launch_pdl_hash(a, st), "pdl_hash");
-    c->mark("pdl_hash", false);
-    if (rc) return rc;
-  }
+  // (2) the jobs that exponentiate by the PDL challenges (hashed on the host by prepare)
   {
     BinomArgs a{(const uint64_t*)(dev + pl.d_bs), (const uint64_t*)(dev + pl.d_bn), pl.s1l, nl, nn, PX(pl.x_Bpdl), P};
     if ((rc = c->hip_check(launch_binom(a, st), "binom"))) return rc;
@@ -1655,7 +1661,6 @@ static int collect_launch_impl(Ctx* c) {
   {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
-    if (ga_first & 2) (void)hipStreamWaitEvent(ss, ga_done, 0);
     if ((rc = launch_group(2, ss, 0, j2_group, cons_nn))) return rc;
     InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
                   PX(pl.x_unn), nullptr, pl.n_inv_nn};
@@ -1667,7 +1672,7 @@ static int collect_launch_impl(Ctx* c) {
   {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
     hipStream_t ss = c->side_stream(5);
     (void)hipStreamWaitEvent(ss, ready, 0);
-    PdlU1Args u{PI(pl.o_ps1), PX(pl.x_epdl), PI(pl.o_Q), PI(pl.o_pu1), pl.s1l, (uint8_t*)(out_base + pl.x_pdlv), P};
+    PdlU1Args u{PI(pl.o_ps1), PI(pl.o_epdl), PI(pl.o_Q), PI(pl.o_pu1), pl.s1l, (uint8_t*)(out_base + pl.x_pdlv), P};
     c->mark("ec", true, ss);
     rc = c->hip_check(launch_pdl_u1(u, ss), "pdl_u1");
     c->mark("ec", false, ss);
@@ -1678,14 +1683,6 @@ static int collect_launch_impl(Ctx* c) {
   (void)hipEventDestroy(ready);
   {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses
     hipStream_t js = st;
-    if (c->reserve_cus) {
-      js = c->side_stream(7);
-      hipEvent_t r2;
-      if ((rc = fork(st, &r2))) return rc;
-      (void)hipStreamWaitEvent(js, r2, 0);
-      (void)hipEventDestroy(r2);
-    }
-    if (ga_first & 4) (void)hipStreamWaitEvent(js, ga_done, 0);
     if ((rc = launch_group(3, js, prio[3], j5_group, cons_nl))) return rc;
     InverseArgs b1{(const uint64_t*)(dev + pl.d_iynl), (const uint64_t*)(dev + pl.d_imnl), PX(pl.x_invz),
                    PX(pl.x_uzA), nullptr, P};
@@ -1696,9 +1693,7 @@ static int collect_launch_impl(Ctx* c) {
     InverseArgs b2{(const uint64_t*)(dev + pl.d_iynl) + P, (const uint64_t*)(dev + pl.d_imnl) + P, nullptr,
                    PX(pl.x_uzp), nullptr, P};
     if ((rc = c->hip_check(launch_inverse(nl, b2, js), "inverse nl 2"))) return rc;
-    if (js != st && (rc = join_later(js))) return rc;
   }
-  if (ga_done) (void)hipEventDestroy(ga_done);
   for (hipEvent_t ev : done) {
     (void)hipStreamWaitEvent(st, ev, 0);
     (void)hipEventDestroy(ev);
@@ -1762,7 +1757,8 @@ static int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
   const uint32_t P = pl.P, Mt = pl.Mt, M = pl.M;
   uint8_t* const out_base = pl.dev + pl.out_off;
   hipStream_t st = c->stream;
-  std::vector<uint32_t> e_pdl((size_t)P * 8), ppanic(Mt), unn(pl.n_inv_nn), uzA(P), uzp(P), eq2(P), eq3(pl.n_eq_nl),
+  const std::vector<uint32_t>& e_pdl = pl.e_pdl;
+  std::vector<uint32_t> ppanic(Mt), unn(pl.n_inv_nn), uzA(P), uzp(P), eq2(P), eq3(pl.n_eq_nl),
       eqck(pl.n_eq_ck), p2(pl.n_p2);
   std::vector<uint8_t> fel(P), pdlv(P), rng(P);
   int rc;
@@ -1770,7 +1766,7 @@ static int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
     if (!bytes) return (int)FSDKR_OK;
     return c->hip_check(hipMemcpyAsync(dst, out_base + off, bytes, hipMemcpyDeviceToHost, st), "D2H verdicts");
   };
-  if ((rc = D2H(e_pdl.data(), pl.x_epdl, e_pdl.size() * 4)) || (rc = D2H(ppanic.data(), pl.x_ppanic, Mt * 4)) ||
+  if ((rc = D2H(ppanic.data(), pl.x_ppanic, Mt * 4)) ||
       (rc = D2H(unn.data(), pl.x_unn, unn.size() * 4)) || (rc = D2H(uzA.data(), pl.x_uzA, P * 4)) ||
       (rc = D2H(uzp.data(), pl.x_uzp, P * 4)) || (rc = D2H(eq2.data(), pl.x_eq2, P * 4)) ||
       (rc = D2H(eq3.data(), pl.x_eq3, eq3.size() * 4)) || (rc = D2H(eqck.data(), pl.x_eqck, eqck.size() * 4)) ||

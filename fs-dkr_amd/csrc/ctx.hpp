@@ -65,20 +65,11 @@ struct Ctx {
   // regular-access modexp (secret exponents: prover, key generation, decryption)
   bool ct = false;
   hipStream_t side_stream(int k);
-  // CU reservation for latency-critical serial chains (FSDKR_RESERVE_CUS = R, a
-  // multiple of 8): crit_stream() runs on R CUs spread evenly over the 8 XCDs and
-  // every side stream on the complement, so a chain of dependent products (the
-  // fixed-base table squarings) never shares a CU with the throughput jobs.
-  // 0 = no reservation (crit_stream() returns nullptr: run on the caller's stream).
-  uint32_t reserve_cus = 0;
-  bool reserve_excl = true;   // side streams on the complement (false: unmasked)
-  // GA split (FSDKR_GA_CUS = G, a multiple of 8): side stream 0 (GA, the s^N mod
-  // N^2 chains) runs on G CUs spread over the XCDs, every other stream (main,
-  // side, recovery) on the complement, so the longest dependent chains of a
-  // small (sharded) batch never share a SIMD with the throughput jobs.
+  // GA split (fsdkr_ctx_set_cu_split(G), G a multiple of 8): side stream 0 (GA,
+  // the s^N mod N^2 chains) runs on G CUs spread over the XCDs, every other
+  // stream (main, side, recovery) on the complement, so the longest dependent
+  // chains of a small (sharded) batch never share a SIMD with the throughput jobs.
   uint32_t ga_cus = 0;
-  hipStream_t crit = nullptr;
-  hipStream_t crit_stream();
   // CU mask words of a balanced set of `count` CUs (in = true) or of its complement
   std::vector<uint32_t> cu_mask(uint32_t count, bool in) const;
   // synchronise the stream and fold pending events into `times`

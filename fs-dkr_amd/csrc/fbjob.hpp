@@ -17,10 +17,6 @@ namespace fsdkr {
 struct FbJob {
   uint32_t k32 = 0;
   uint32_t table_prio = 3;   // s_setprio of the table chain (a long serial chain, few waves)
-  // optional split into group A = bases [0, split_bases), instances [0, split_inst)
-  // and group B = the rest: B's table chains are the long ones, so A's exponents
-  // run as soon as A's tables exist (0 = one group)
-  uint32_t split_bases = 0, split_inst = 0;
   // bases
   std::vector<uint64_t> b_ptr;
   std::vector<uint32_t> b_len, b_mod, b_bits;
@@ -123,21 +119,17 @@ struct FbDev {
   uint32_t* nsteps = nullptr;
 };
 
-// table, schedule and exponent kernels; `st_table` may differ from `st` (the
-// schedule kernel runs beside the table chain), the exponent kernel waits for both.
-// table_st: stream of the table chain (nullptr = st); st waits for it (and for
-// exp_wait, if given) before fb_exp
-// pre: every base's table was built ahead into pre->table (fsdkr_collect_prestart,
-// same layout); group A's are complete at ready_a, group B's at ready_b.
+// table, schedule and exponent kernels.  table_st: stream of the table chain
+// (nullptr = st; the schedule kernel runs beside it on st), and fb_exp on st
+// waits for it.  pre: every base's table was built ahead into pre->table
+// (fsdkr_collect_prestart, same layout), complete at pre->ready.
 struct FbPre {
   const uint32_t* table = nullptr;
   uint32_t entries = 0;
-  hipEvent_t ready_a = nullptr, ready_b = nullptr;
+  hipEvent_t ready = nullptr;
 };
-// table_st_a: stream of group A's table chains (nullptr = table_st)
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
-              hipStream_t table_st = nullptr, hipEvent_t exp_wait = nullptr, const FbPre* pre = nullptr,
-              hipStream_t table_st_a = nullptr);
+              hipStream_t table_st = nullptr, const FbPre* pre = nullptr);
 // upload + launch + wait (stand-alone callers)
 int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag);
 

@@ -20,62 +20,40 @@ static int fb_group(Ctx* c, size_t count) {
 }
 
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
-              hipStream_t table_st, hipEvent_t exp_wait, const FbPre* pre, hipStream_t table_st_a) {
+              hipStream_t table_st, const FbPre* pre) {
   if (j.count() == 0) return FSDKR_OK;
   const uint8_t* I = d.img;
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(I + o); };
   const uint32_t nb = (uint32_t)j.bases(), ni = (uint32_t)j.count();
-  const uint32_t nbA = j.split_bases ? j.split_bases : nb, niA = j.split_bases ? j.split_inst : ni;
-  const uint32_t* table_pre = pre ? pre->table : nullptr;
-  const uint32_t split = pre ? pre->entries : 0u;   // every entry prestarted, or none
   int rc;
-  auto event_on = [&](hipStream_t s, hipEvent_t* ev) -> int {
-    int r = c->hip_check(hipEventCreateWithFlags(ev, hipEventDisableTiming), "event");
-    if (!r) r = c->hip_check(hipEventRecord(*ev, s), "event record");
-    return r;
-  };
-  // the table chains (own streams, from t = 0 beside fb_sched), group A then B
-  hipStream_t tsB = table_st ? table_st : st, tsA = table_st_a ? table_st_a : tsB;
-  hipEvent_t evA = pre ? pre->ready_a : nullptr, evB = pre ? pre->ready_b : nullptr;
-  bool own_a = false, own_b = false;
+  // the table chains (own stream, from t = 0 beside fb_sched), unless prestarted
+  hipStream_t ts = table_st ? table_st : st;
+  hipEvent_t ready = pre ? pre->ready : nullptr;
+  bool own = false;
   if (!pre) {
-    auto tables = [&](uint32_t b0, uint32_t b1, hipStream_t s) -> int {
-      if (b1 <= b0) return FSDKR_OK;
-      FbTableArgs ta{U64(j.off.b_ptr) + b0, U32(j.off.b_len) + b0, U32(j.off.b_mod) + b0, U32(j.off.b_toff) + b0,
-                     U32(j.off.b_h) + b0, consts, d.table, j.w, b1 - b0, j.table_prio};
-      size_t m = c->tbeg("fb_table", s);
-      int r = c->hip_check(launch_fb_table(j.k32, ta, s), "fb_table launch");
-      c->tend(m, s);
-      return r;
-    };
-    if ((rc = tables(nbA, nb, tsB)) || (rc = tables(0, nbA, tsA))) return rc;
-    if (tsA != st && (rc = event_on(tsA, &evA))) return rc;
-    own_a = tsA != st;
-    if (nbA < nb && tsB != st) {
-      if ((rc = event_on(tsB, &evB))) return rc;
-      own_b = true;
+    FbTableArgs ta{U64(j.off.b_ptr), U32(j.off.b_len), U32(j.off.b_mod), U32(j.off.b_toff), U32(j.off.b_h), consts,
+                   d.table, j.w, nb, j.table_prio};
+    size_t m = c->tbeg("fb_table", ts);
+    rc = c->hip_check(launch_fb_table(j.k32, ta, ts), "fb_table launch");
+    c->tend(m, ts);
+    if (rc) return rc;
+    if (ts != st) {
+      if ((rc = c->hip_check(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "event")) ||
+          (rc = c->hip_check(hipEventRecord(ready, ts), "event record")))
+        return rc;
+      own = true;
     }
   }
   FbSchedArgs sa{U64(j.off.e_ptr), U32(j.off.e_len), U32(j.off.i_h), d.sched, d.nsteps, j.stride, j.w, ni};
   if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
-  if (exp_wait) (void)hipStreamWaitEvent(st, exp_wait, 0);
-  auto exps = [&](uint32_t i0, uint32_t i1) -> int {
-    if (i1 <= i0) return FSDKR_OK;
-    FbExpArgs ea{U32(j.off.i_toff) + i0, U32(j.off.e_mod) + i0, U64(j.off.o_ptr) + i0, consts, d.table,
-                 d.sched + (size_t)i0 * j.stride, d.nsteps + i0, j.stride, i1 - i0, table_pre, split};
-    size_t m = c->tbeg("fb_exp", st);
-    int r = c->hip_check(launch_fb_exp(j.k32, ea, fb_group(c, i1 - i0), st), tag);
-    c->tend(m, st);
-    return r;
-  };
-  if (evA) (void)hipStreamWaitEvent(st, evA, 0);
-  if (niA == ni && evB) (void)hipStreamWaitEvent(st, evB, 0);   // one group: every table first
-  if ((rc = exps(0, niA))) return rc;
-  if (evB) (void)hipStreamWaitEvent(st, evB, 0);
-  rc = exps(niA, ni);
-  if (own_a) (void)hipEventDestroy(evA);
-  if (own_b) (void)hipEventDestroy(evB);
+  if (ready) (void)hipStreamWaitEvent(st, ready, 0);
+  FbExpArgs ea{U32(j.off.i_toff), U32(j.off.e_mod), U64(j.off.o_ptr), consts, d.table, d.sched, d.nsteps, j.stride,
+               ni, pre ? pre->table : nullptr, pre ? pre->entries : 0u};
+  size_t m = c->tbeg("fb_exp", st);
+  rc = c->hip_check(launch_fb_exp(j.k32, ea, fb_group(c, ni), st), tag);
+  c->tend(m, st);
+  if (own) (void)hipEventDestroy(ready);
   return rc;
 }
 

@@ -17,13 +17,6 @@ struct BinomArgs {          // out = 1 + s * n
   uint32_t count;
 };
 
-struct PdlHashArgs {        // e = H(G, Q, c, z, u1, u2, u3)
-  const uint32_t *Q, *c, *z, *u1, *u2, *u3;
-  uint32_t c_len, z_len;
-  uint32_t* e_out;          // [count][8]
-  uint32_t count;
-};
-
 struct PedHashArgs {        // ring-Pedersen challenge bits
   const uint32_t* A;        // [count][M][a_len]
   uint32_t M, a_len;
@@ -134,7 +127,6 @@ struct EcMsmArgs {          // out[o] = sum_j scalars[o][j] * P[o][j]
 };
 
 hipError_t launch_binom(const BinomArgs& a, hipStream_t st);
-hipError_t launch_pdl_hash(const PdlHashArgs& a, hipStream_t st);
 hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st);
 hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st);
 hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);

@@ -1,7 +1,8 @@
 // Hashing and small-arithmetic kernels of the batched collect() job (gfx950).
 // Fiat-Shamir transcripts restated from curv DigestExt::chain_bigint (SHA-256
 // over BigInt::to_bytes):
-//   pdl_hash        e = H(G,Q,c,z,u1,u2,u3)                    zk_pdl_with_slack.rs:114-122
+//   (the PDL challenge e = H(G,Q,c,z,u1,u2,u3), zk_pdl_with_slack.rs:114-122, is
+//    hashed on the host by fsdkr_collect_prepare: collect.cpp)
 //   alice_hash      e' = H(N,N+1,c,z,u,w) == e                 range_proofs.rs:150-163
 //   ped_hash        e = H(A_0..A_M-1), Lsb0 bits              ring_pedersen_proof.rs:130-142
 //   binom           (N+1)^s1 = 1 + s1*N  (s1 < N)              zk_pdl_with_slack.rs:129-135
@@ -48,46 +49,6 @@ __global__ void binom_kernel(const BinomArgs a) {
 }
 
 // ------------------------------------------------------------- hashing --------
-__constant__ const uint8_t G_COMPRESSED[33] = {
-    0x02, 0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0, 0x62, 0x95, 0xCE, 0x87, 0x0B, 0x07,
-    0x02, 0x9B, 0xFC, 0xDB, 0x2D, 0xCE, 0x28, 0xD9, 0x59, 0xF2, 0x81, 0x5B, 0x16, 0xF8, 0x17, 0x98};
-
-// BigInt::from_bytes(P.to_bytes(true)) re-encoded by to_bytes: 33 bytes for a
-// finite point (prefix 2/3 is nonzero), a single 0x00 for infinity.
-__device__ __forceinline__ void absorb_point(Sha256& h, const uint32_t* p16) {
-  bool inf = true;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) inf = inf && (p16[i] == 0);
-  if (inf) {
-    h.byte(0);
-    return;
-  }
-  h.byte((uint8_t)(2 + (p16[8] & 1u)));
-  for (int i = 7; i >= 0; --i) {
-    const uint32_t x = p16[i];
-    h.byte((uint8_t)(x >> 24));
-    h.byte((uint8_t)(x >> 16));
-    h.byte((uint8_t)(x >> 8));
-    h.byte((uint8_t)x);
-  }
-}
-
-__global__ void pdl_hash_kernel(const PdlHashArgs a) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.count) return;
-  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
-  Sha256 h;
-  h.init(sha_w + threadIdx.x * 16);
-  for (int i = 0; i < 33; ++i) h.byte(G_COMPRESSED[i]);
-  absorb_point(h, a.Q + (size_t)p * 16);
-  h.bigint(a.c + (size_t)p * a.c_len, a.c_len);
-  h.bigint(a.z + (size_t)p * a.z_len, a.z_len);
-  absorb_point(h, a.u1 + (size_t)p * 16);
-  h.bigint(a.u2 + (size_t)p * a.c_len, a.c_len);
-  h.bigint(a.u3 + (size_t)p * a.z_len, a.z_len);
-  h.finish_le(a.e_out + (size_t)p * 8);
-}
-
 // e = H(A_0 .. A_{M-1}); bits[m][i/32] bit i%32 = Lsb0 bit i of e.to_bytes();
 // panic[m] != 0 if e.to_bytes() is shorter than M bits (BitVec index panic at bit
 // panic[m]-1; checks before that index still run and may fail first).
@@ -240,11 +201,6 @@ __global__ void alice_hash_kernel(const AliceHashArgs a) {
 hipError_t launch_binom(const BinomArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
   hipLaunchKernelGGL(binom_kernel, dim3(blocks_for(a.count, 128)), dim3(128), 0, st, a);
-  return hipGetLastError();
-}
-hipError_t launch_pdl_hash(const PdlHashArgs& a, hipStream_t st) {
-  if (!a.count) return hipSuccess;
-  hipLaunchKernelGGL(pdl_hash_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st) {

@@ -231,9 +231,8 @@ class CollectBatch:
         self._ga = None
         if staged and nl_ga is not None:
             Gs = _Gather()
-            names = ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s", "ped_T", "ped_N")
-            if os.environ.get("FSDKR_SLIM_STAGE1") != "1":   # tuning knob: s1 / s3 / Z to stage 2
-                names += ("pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
+            names = ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s", "ped_T", "ped_N",
+                     "pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
             ga = {name: Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c)) for name in names}
             Gs.run()
             for name, arr in ga.items():

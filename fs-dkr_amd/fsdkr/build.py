@@ -86,7 +86,7 @@ def build(verbose=False, force=False):
         with cf.ThreadPoolExecutor(max_workers=min(8, len(todo))) as ex:
             list(ex.map(lambda s: _compile(s, verbose), todo))
     if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lcrypto"]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

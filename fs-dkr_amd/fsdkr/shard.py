@@ -11,14 +11,12 @@ No other data crosses the interconnect.  collect() then maps the merged
 verdicts to the reference's first error on a header-only batch of the whole
 message set (threshold, sizes, party indices, ek.n) and applies collect()'s
 side effects and share recovery (refresh_message.rs:330-464) on every rank."""
-import os
-
 import numpy as np
 
 from .batch import CollectBatch, Verdicts
 
 
-# tuning knobs FSDKR_SHARD_GA_CUS / FSDKR_SHARD_GA_MAX (read per slice)
+# GA split of a small slice (measured: profiles/r02zd_ga_lanes_cus_ab.jsonl, r02zn_ga_split_size_ab.jsonl)
 GA_SPLIT_CUS = 160
 GA_SPLIT_MAX_CHAINS = 1024
 
@@ -97,9 +95,7 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
     # remaining 96 (8-way shard of n=64: 29.4 -> 22.5 ms per rank; no gain at 2-
     # and 4-way shards, profiles/r02zd_ga_lanes_cus_ab.jsonl)
     if hasattr(ctx, "set_cu_split"):
-        cus = int(os.environ.get("FSDKR_SHARD_GA_CUS", GA_SPLIT_CUS))
-        most = int(os.environ.get("FSDKR_SHARD_GA_MAX", GA_SPLIT_MAX_CHAINS))
-        ctx.set_cu_split(cus if 2 * (r1 - r0) * n <= most else 0)
+        ctx.set_cu_split(GA_SPLIT_CUS if 2 * (r1 - r0) * n <= GA_SPLIT_MAX_CHAINS else 0)
     b = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], m_security, key_bits, n_recv=n, staged=True)
     if b.header_only:   # an empty refresh slice (joins only) or a size failure the header batch reports
         return None, None

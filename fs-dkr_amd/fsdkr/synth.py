@@ -89,9 +89,12 @@ _SIEVE = None
 
 
 def _primorial_16():
+    """Product of the odd primes below 2^12: a gcd against it drops 87 % of odd
+    candidates for 0.02 ms each (the 2^16 primorial drops 90 % for 0.27 ms: the
+    n = 256 workload's 52 k candidates took 14 s of host time)."""
     global _SIEVE
     if _SIEVE is None:
-        n = 1 << 16
+        n = 1 << 12
         flags = bytearray([1]) * n
         flags[0:2] = b"\x00\x00"
         for i in range(2, int(n ** 0.5) + 1):

@@ -16,6 +16,9 @@ for step in "$@"; do
     bench) timeout -k 10 420 python $R/bench.py > $OUT/bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 $OUT/bench.log; exit 1; } ;;
     benchq) timeout -k 10 300 python $R/bench.py --no-cpu-baseline > $OUT/bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 $OUT/bench.log; exit 1; } ;;
     prof) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1) || { echo "prof failed rc=$?"; tail -30 $OUT/prof.log; exit 1; } ;;
+    trace) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr -- python3 $R/tools/prof_collect.py --full --steps 4 > $OUT/trace.log 2>&1) || { echo "trace failed rc=$?"; tail -30 $OUT/trace.log; exit 1; }
+      f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
+      python $R/tools/prof_summary.py "$f" --gap 10 --step 2 > $OUT/trace_summary.txt || exit 1 ;;
     *) timeout -k 10 420 bash -c "$step" > $OUT/extra.log 2>&1 || { echo "step failed rc=$?"; tail -30 $OUT/extra.log; exit 1; } ;;
   esac
   echo "step $step ok"

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace run (rocpd SQLite .db or the CSV
 kernel_trace file): per-kernel stats (calls, total/avg/min/max ms, share) and
-the kernel timeline of one collect() step (the `--step`-th pdl_hash launch up
-to the next one).  Used to produce the profiles/*.txt summaries."""
+the kernel timeline of one collect() step (the `--step`-th launch of the
+--marker kernel up to the next one, or bursts split at --gap ms of idle device).  Used to produce the profiles/*.txt summaries."""
 import argparse
 import csv
 import sqlite3
@@ -34,6 +34,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=2)
     ap.add_argument("--gap", type=float, default=0.0, help="split steps at device idle gaps of this many ms")
+    ap.add_argument("--marker", default="ped_hash", help="kernel launched once per step")
     a = ap.parse_args()
     rows = load(a.trace)
     by = {}
@@ -54,7 +55,7 @@ def main():
                 idx.append(i)
             end = r[2] if end is None else max(end, r[2])
     else:
-        idx = [i for i, r in enumerate(rows) if "pdl_hash" in r[0]]
+        idx = [i for i, r in enumerate(rows) if a.marker in r[0]]
     step = a.step if a.step >= 0 else len(idx) + a.step
     if 0 <= step < len(idx):
         i0 = idx[step]
