@@ -1,0 +1,279 @@
+// fsdkr_collect_prestart[_multi]: the longest device chains of a collect()
+// batch -- GA (s2^N, s^N mod N^2 per pair, zk_pdl_with_slack.rs:129-135,
+// range_proofs.rs:148) and the fixed-base tables of h1_i, h2_i and every
+// ring-Pedersen T -- started from the few fields stage 1 packs, while the caller
+// packs the rest.  prepare consumes them when the batch matches.
+#include "collect.hpp"
+
+namespace fsdkr {
+
+
+// The fixed-base table chains of collect()'s FbJob, in its base order: h1_i, h2_i
+// of every receiver's DLogStatement (h2: one squaring per exponent bit of s3,
+// ~2816 at 2048-bit keys), then every message's ring-Pedersen T, sized by the
+// bit lengths of the exponents they serve (PDL / Alice s1, s3|s2; RP Z), on the
+// table chain's stream.
+static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, uint32_t n, uint32_t P) {
+  if (!b->recv_ntilde || !b->recv_h1 || !b->recv_h2 || !b->s1l || !b->s3l || !b->ped_T || !b->ped_N || !b->zl ||
+      !b->m_security)
+    return FSDKR_OK;   // stage 1 did not pack them: prepare builds every table
+  // exponent bit bounds: exact from the packed exponents, else their slot widths
+  // (a slim stage 1 leaves s1 / s3 / Z to stage 2; tables at most 31 bits longer)
+  const bool exact_s = b->pdl_s1 && b->pdl_s3 && b->rp_s1 && b->rp_s2;
+  const uint32_t nl = b->nl, Mt = b->n_refresh + b->n_join, M = b->m_security;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!is_odd(b->recv_ntilde + (size_t)i * nl)) return FSDKR_OK;
+  uint32_t bh1 = 1, bh2 = 1, bz = 1;
+  if (exact_s) {
+    for (size_t p = 0; p < P; ++p) {
+      bh1 = std::max(bh1, std::max(hbn::bitlen(b->pdl_s1 + p * b->s1l, b->s1l), hbn::bitlen(b->rp_s1 + p * b->s1l, b->s1l)));
+      bh2 = std::max(bh2, std::max(hbn::bitlen(b->pdl_s3 + p * b->s3l, b->s3l), hbn::bitlen(b->rp_s2 + p * b->s3l, b->s3l)));
+    }
+  } else {
+    bh1 = 32 * b->s1l;
+    bh2 = 32 * b->s3l;
+  }
+  if (b->ped_Z)
+    for (size_t k = 0; k < (size_t)Mt * M; ++k) bz = std::max(bz, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
+  else
+    bz = 32 * b->zl;
+  const uint32_t w = fb_window(std::max(std::max(bh1, bh2), bz));
+  const FbLayout L = fb_layout(n, Mt, w, bh1, bh2, bz);
+  const uint32_t nb = 2 * n + Mt, entries = L.entries, nmod = n + Mt;
+  const int KD = shape_digits(nl);
+  auto al = Img::al;
+  const size_t o_mod = 0, o_h1 = al((size_t)nmod * nl * 4), o_h2 = o_h1 + al((size_t)n * nl * 4),
+               o_T = o_h2 + al((size_t)n * nl * 4), o_bp = o_T + al((size_t)Mt * nl * 4),
+               o_bl = o_bp + al((size_t)nb * 8), o_bm = o_bl + al((size_t)nb * 4), o_bt = o_bm + al((size_t)nb * 4),
+               o_bh = o_bt + al((size_t)nb * 4), o_tab = o_bh + al((size_t)nb * 4);
+  const size_t total = o_tab + (size_t)entries * KD * 4;
+  uint8_t* dev = (uint8_t*)c->buf("collect_fb_pre", total);
+  if (!dev) {
+    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
+    return FSDKR_E_OOM;
+  }
+  std::vector<uint8_t> img(o_tab, 0);
+  uint32_t* mods = reinterpret_cast<uint32_t*>(img.data() + o_mod);   // [Ntilde_i | RP modulus_m]
+  memcpy(mods, b->recv_ntilde, (size_t)n * nl * 4);
+  for (uint32_t m = 0; m < Mt; ++m) ped_modulus(b, m, M, nl, mods + (size_t)(n + m) * nl);
+  memcpy(img.data() + o_h1, b->recv_h1, (size_t)n * nl * 4);
+  memcpy(img.data() + o_h2, b->recv_h2, (size_t)n * nl * 4);
+  memcpy(img.data() + o_T, b->ped_T, (size_t)Mt * nl * 4);
+  auto* bp = reinterpret_cast<uint64_t*>(img.data() + o_bp);
+  for (uint32_t r = 0; r < n; ++r) {   // prepare's base order [h1_i | T_m | h2_i]
+    bp[r] = (uint64_t)(uintptr_t)(dev + o_h1 + (size_t)r * nl * 4);
+    bp[n + Mt + r] = (uint64_t)(uintptr_t)(dev + o_h2 + (size_t)r * nl * 4);
+  }
+  for (uint32_t m = 0; m < Mt; ++m) bp[n + m] = (uint64_t)(uintptr_t)(dev + o_T + (size_t)m * nl * 4);
+  std::vector<uint32_t> blen(nb, nl);
+  memcpy(img.data() + o_bl, blen.data(), (size_t)nb * 4);
+  memcpy(img.data() + o_bm, L.mod.data(), (size_t)nb * 4);
+  memcpy(img.data() + o_bt, L.toff.data(), (size_t)nb * 4);
+  memcpy(img.data() + o_bh, L.h.data(), (size_t)nb * 4);
+  // every table chain in one launch on launch()'s table-chain stream; launch()'s
+  // fixed-base exponent stream waits for it through fb_done
+  hipStream_t ts = c->side_stream(8);
+  StreamScope scope(c, ts);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, ts), "prestart fb H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(ts), "prestart fb H2D sync")))
+    return rc;
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl")))
+    return rc;
+  if (!g.fb_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done, hipEventDisableTiming), "event")))
+    return rc;
+  g.fb_table = reinterpret_cast<uint32_t*>(dev + o_tab);
+  auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
+  auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
+  FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
+  if ((rc = c->hip_check(launch_fb_table(nl, tall, ts), "prestart fb_table"))) return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.fb_done, ts), "event record"))) return rc;
+  g.ntilde.assign(b->recv_ntilde, b->recv_ntilde + (size_t)n * nl);
+  g.h1.assign(b->recv_h1, b->recv_h1 + (size_t)n * nl);
+  g.h2.assign(b->recv_h2, b->recv_h2 + (size_t)n * nl);
+  g.T.assign(b->ped_T, b->ped_T + (size_t)Mt * nl);
+  g.pedmod.assign(mods + (size_t)n * nl, mods + (size_t)nmod * nl);
+  g.Mt = Mt;
+  g.fb_w = w;
+  g.bits_h1 = bh1;
+  g.bits_h2 = bh2;
+  g.bits_z = bz;
+  g.fb_entries = entries;
+  g.fb_valid = true;
+  return FSDKR_OK;
+}
+
+
+// GA prestart of `count` sessions (one: fsdkr_collect_prestart; many:
+// fsdkr_collect_prestart_multi), in prepare's global order: session s's
+// receivers and pairs after session s-1's, every row at the widest nl.
+int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t* n_out, uint32_t* P_out) {
+  if (!c->ga_pre) c->ga_pre = new GaPre();
+  GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
+  g.valid = false;
+  g.fb_valid = false;
+  *n_out = *P_out = 0;
+  const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
+  if (running && running->launched) {
+    c->fail("fsdkr_collect_prestart: a batch is in flight (call finish first)");
+    return FSDKR_E_ARG;
+  }
+  // a prepared plan that consumed the previous prestart reads its s^N rows and
+  // fixed-base tables in place: this prestart overwrites (or reallocates) those
+  // buffers, so the plan is dropped (a later launch reports "no prepared batch")
+  if (running && (running->ga_hit || running->fb_hit)) free_collect_plan(c);
+  if (!bs || count == 0) {
+    c->fail("fsdkr_collect_prestart: no batch");
+    return FSDKR_E_ARG;
+  }
+  uint32_t nl = 0, n = 0, P = 0;
+  std::vector<GaPre::Sess> ss(count);
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (!(b->nl == 64 || b->nl == 96) || !b->recv_n || !b->pdl_s2 || !b->rp_s) {
+      c->fail("fsdkr_collect_prestart: session %u needs nl, recv_n, pdl_s2 and rp_s", k);
+      return FSDKR_E_ARG;
+    }
+    const uint32_t R = b->n_refresh, ns = b->n_recv ? b->n_recv : R + b->n_join;
+    if (R == 0 || ns < R) return FSDKR_OK;   // nothing to start (prepare reports bad shapes)
+    for (uint32_t i = 0; i < ns; ++i)
+      if (!is_odd(b->recv_n + (size_t)i * b->nl)) return FSDKR_OK;   // prepare reports it
+    ss[k] = GaPre::Sess{b->nl, ns, R, (size_t)n, (size_t)P};
+    nl = std::max(nl, b->nl);
+    n += ns;
+    P += R * ns;
+  }
+  const uint32_t nn = 2 * nl;
+  // the inputs, at each session's own width, for the match in prepare
+  g.recv_n.clear();
+  g.s2.clear();
+  g.s.clear();
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const GaPre::Sess& x = ss[k];
+    g.recv_n.insert(g.recv_n.end(), b->recv_n, b->recv_n + (size_t)x.n * x.nl);
+    g.s2.insert(g.s2.end(), b->pdl_s2, b->pdl_s2 + (size_t)x.R * x.n * x.nl);
+    g.s.insert(g.s.end(), b->rp_s, b->rp_s + (size_t)x.R * x.n * x.nl);
+  }
+  // image: [N^2 | N | s2 | s | descriptors], outputs after it
+  auto al = Img::al;
+  const size_t o_NN = 0, o_rn = al((size_t)n * nn * 4), o_s2 = o_rn + al((size_t)n * nl * 4),
+               o_s = o_s2 + al((size_t)P * nl * 4), o_desc = o_s + al((size_t)P * nl * 4);
+  const size_t desc_bytes = (size_t)2 * P * 32, o_out = o_desc + al(desc_bytes);
+  const size_t total = o_out + (size_t)2 * P * nn * 4;
+  uint8_t* dev = (uint8_t*)c->buf("collect_ga", total);
+  if (!dev) {
+    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
+    return FSDKR_E_OOM;
+  }
+  std::vector<uint8_t> img(o_out, 0);
+  uint32_t* NN = reinterpret_cast<uint32_t*>(img.data() + o_NN);
+  uint32_t* RN = reinterpret_cast<uint32_t*>(img.data() + o_rn);
+  uint32_t* S2 = reinterpret_cast<uint32_t*>(img.data() + o_s2);
+  uint32_t* S1 = reinterpret_cast<uint32_t*>(img.data() + o_s);
+  std::vector<uint32_t> rbits(n);
+  std::vector<uint32_t> sess_of_recv(n);
+  for (uint32_t k = 0; k < count; ++k) std::fill(sess_of_recv.begin() + ss[k].rbase, sess_of_recv.begin() + ss[k].rbase + ss[k].n, k);
+  parallel_for(n, 64, [&](size_t r0, size_t r1) {
+    for (size_t r = r0; r < r1; ++r) {
+      const GaPre::Sess& x = ss[sess_of_recv[r]];
+      const uint32_t* Np = bs[sess_of_recv[r]].recv_n + (r - x.rbase) * x.nl;
+      const hbn::Limbs N = hbn::from(Np, x.nl);
+      hbn::store(hbn::mul(N, N), NN + r * nn, nn);
+      memcpy(RN + r * nl, Np, (size_t)x.nl * 4);
+      rbits[r] = hbn::bitlen(Np, x.nl);
+    }
+  });
+  uint32_t recvn_max = 1;
+  for (uint32_t r = 0; r < n; ++r) recvn_max = std::max(recvn_max, rbits[r]);
+  for (uint32_t k = 0; k < count; ++k) {   // pair rows, zero-extended to nl
+    const GaPre::Sess& x = ss[k];
+    const size_t cnt = (size_t)x.R * x.n;
+    if (x.nl == nl) {
+      memcpy(S2 + x.pbase * nl, bs[k].pdl_s2, cnt * nl * 4);
+      memcpy(S1 + x.pbase * nl, bs[k].rp_s, cnt * nl * 4);
+    } else {
+      for (size_t q = 0; q < cnt; ++q) {
+        memcpy(S2 + (x.pbase + q) * nl, bs[k].pdl_s2 + q * x.nl, (size_t)x.nl * 4);
+        memcpy(S1 + (x.pbase + q) * nl, bs[k].rp_s + q * x.nl, (size_t)x.nl * 4);
+      }
+    }
+  }
+  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
+  ModexpJob J1;
+  J1.k32 = nn;
+  for (int which = 0; which < 2; ++which)   // the order prepare's J1 uses
+    for (uint32_t k = 0; k < count; ++k) {
+      const GaPre::Sess& x = ss[k];
+      for (uint32_t q = 0; q < x.R * x.n; ++q) {
+        const size_t p = x.pbase + q, r = x.rbase + q % x.n;
+        J1.add(DI((which == 0 ? o_s2 : o_s) + p * nl * 4), nl, DI(o_rn + r * nl * 4), nl, recvn_max, (uint32_t)r);
+      }
+    }
+  std::vector<uint8_t> desc;
+  J1.pack(desc);
+  memcpy(img.data() + o_desc, desc.data(), desc.size());
+  hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
+  StreamScope scope(c, gs);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, gs), "prestart H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // img is pageable and local
+    return rc;
+  // the lanes launch() would give GA: 32 lanes (KD = 160 constants) for the small
+  // batches of a multi-GPU shard, where GA's chain latency is the critical path
+  const uint32_t group = ga_lanes(2 * P, nn);
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
+                         group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
+    return rc;
+  g.out = reinterpret_cast<uint32_t*>(dev + o_out);
+  if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
+    return rc;
+  (void)hipEventRecord(g.ga_setup, gs);   // GA's constants are ready
+  // issue priority 3 (2 measured 1-2 ms slower per call, profiles/r02x_ab_full.jsonl)
+  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 3, group)))
+    return rc;
+  if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
+  g.nl = nl;
+  g.n = n;
+  g.R = count == 1 ? bs->n_refresh : 0;
+  g.sess = std::move(ss);
+  g.valid = true;
+  *n_out = n;
+  *P_out = P;
+  return FSDKR_OK;
+}
+
+int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
+  uint32_t n = 0, P = 0;
+  int rc = prestart_ga(c, b, 1, &n, &P);
+  if (rc || P == 0) return rc;
+  return prestart_fb_tables(c, b, *reinterpret_cast<GaPre*>(c->ga_pre), n, P);
+}
+
+// does the prestarted GA belong to these sessions (same shapes, same inputs)?
+bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
+  const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
+  if (!g || !g->valid || g->sess.size() != count) return false;
+  uint32_t nl = 0;
+  for (uint32_t k = 0; k < count; ++k) nl = std::max(nl, bs[k].nl);
+  if (g->nl != nl) return false;
+  size_t on = 0, op = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const GaPre::Sess& x = g->sess[k];
+    const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
+    if (x.nl != b->nl || x.n != ns || x.R != b->n_refresh) return false;
+    const size_t rows = (size_t)x.R * x.n * x.nl;
+    if (memcmp(g->recv_n.data() + on, b->recv_n, (size_t)x.n * x.nl * 4) != 0 ||
+        memcmp(g->s2.data() + op, b->pdl_s2, rows * 4) != 0 || memcmp(g->s.data() + op, b->rp_s, rows * 4) != 0)
+      return false;
+    on += (size_t)x.n * x.nl;
+    op += rows;
+  }
+  return true;
+}
+
+}  // namespace fsdkr

@@ -255,4 +255,140 @@ int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t*
   return c->sync();
 }
 
+namespace {
+const uint32_t SECP_Q[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                            0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+const uint32_t SECP_G[16] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u,
+                             0xF9DCBBACu, 0x79BE667Eu, 0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                             0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+
+// curv VerifiableSS::map_share_to_new_params: the Lagrange weight at 0 of point
+// x_j = old_index[j] over the set, prod_{x_k != x_j} x_k / (x_k - x_j) mod q
+// (entries equal to x_j are skipped, as the reference skips index == j)
+hbn::Limbs lagrange(const uint32_t* x, uint32_t cnt, uint32_t j, const hbn::Limbs& Q) {
+  hbn::Limbs num{1}, den{1};
+  for (uint32_t k = 0; k < cnt; ++k) {
+    if (x[k] == x[j]) continue;
+    num = hbn::mulmod(num, hbn::Limbs{x[k]}, Q);
+    const hbn::Limbs d = x[k] > x[j] ? hbn::Limbs{x[k] - x[j]} : hbn::sub(Q, hbn::Limbs{x[j] - x[k]});
+    den = hbn::mulmod(den, d, Q);
+  }
+  hbn::Limbs inv;
+  if (!hbn::modinv(den, Q, &inv)) return hbn::Limbs{};   // unreachable for indices < q
+  return hbn::mulmod(num, inv, Q);
+}
+}  // namespace
+
+int fsdkr_collect_recover(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count, fsdkr_recovered* out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!jobs || !out) {
+    c->fail("fsdkr_collect_recover: null jobs / out");
+    return FSDKR_E_ARG;
+  }
+  for (uint32_t j = 0; j < count; ++j) {
+    const fsdkr_recover_job& J = jobs[j];
+    if (!shape_digits(J.nl) || !J.old_index || !J.cts || !J.p || !J.q || (J.n_new && (!J.points || !out[j].pk_vec))) {
+      c->fail("fsdkr_collect_recover: job %u: bad shape or null array (nl=%u)", j, J.nl);
+      return FSDKR_E_ARG;
+    }
+  }
+  const hbn::Limbs Q = hbn::from(SECP_Q, 8);
+  // Lagrange weights (host; t_vss+1 small integers per job)
+  std::vector<std::vector<hbn::Limbs>> li(count);
+  for (uint32_t j = 0; j < count; ++j) {
+    const uint32_t T = jobs[j].t_vss + 1;
+    li[j].resize(T);
+    for (uint32_t k = 0; k < T; ++k) li[j][k] = lagrange(jobs[j].old_index, T, k, Q);
+    out[j].status = FSDKR_RECOVER_OK;
+  }
+  // decryptions: one batched call per key width; a width whose batch the
+  // decryption refuses (a degenerate key) is retried job by job
+  std::vector<std::vector<uint32_t>> plain(count);
+  for (uint32_t nl : {64u, 96u, 128u, 192u}) {
+    std::vector<uint32_t> cts, kidx, ps, qs, owners;
+    for (uint32_t j = 0; j < count; ++j) {
+      const fsdkr_recover_job& J = jobs[j];
+      if (J.nl != nl) continue;
+      const uint32_t T = J.t_vss + 1;
+      cts.insert(cts.end(), J.cts, J.cts + (size_t)T * 2 * nl);
+      for (uint32_t k = 0; k < T; ++k) kidx.push_back((uint32_t)owners.size());
+      ps.insert(ps.end(), J.p, J.p + nl);
+      qs.insert(qs.end(), J.q, J.q + nl);
+      owners.push_back(j);
+    }
+    if (owners.empty()) continue;
+    const uint32_t total = (uint32_t)kidx.size();
+    std::vector<uint32_t> m((size_t)total * nl);
+    int rc = fsdkr_paillier_decrypt_multi(ctx, nl, total, cts.data(), kidx.data(), ps.data(), qs.data(),
+                                          (uint32_t)owners.size(), m.data());
+    if (rc == FSDKR_OK) {
+      size_t at = 0;
+      for (uint32_t j : owners) {
+        const size_t T = jobs[j].t_vss + 1;
+        plain[j].assign(m.begin() + at * nl, m.begin() + (at + T) * nl);
+        at += T;
+      }
+      continue;
+    }
+    if (rc != FSDKR_E_ARG) return rc;
+    for (uint32_t j : owners) {
+      const fsdkr_recover_job& J = jobs[j];
+      const uint32_t T = J.t_vss + 1;
+      plain[j].resize((size_t)T * nl);
+      if (fsdkr_paillier_decrypt(ctx, nl, T, J.cts, J.p, J.q, plain[j].data()) != FSDKR_OK) {
+        out[j].status = FSDKR_RECOVER_PANIC_DECRYPT;
+        plain[j].clear();
+      }
+    }
+  }
+  // new share = (sum_k l_k m_k mod N) mod q, then one MSM launch for every y and pk_vec row
+  uint32_t terms = 1;
+  for (uint32_t j = 0; j < count; ++j)
+    terms = std::max(terms, std::min(jobs[j].t_key, jobs[j].t_vss) + 1);
+  std::vector<uint32_t> pts, scs;
+  std::vector<uint32_t> row_of(count, ~0u);
+  auto add_row = [&](const uint32_t* p16, size_t n_pts, const std::vector<hbn::Limbs>& sc) {
+    for (size_t k = 0; k < terms; ++k) {
+      const size_t at = pts.size();
+      pts.resize(at + 16, 0u);
+      scs.resize(scs.size() + 8, 0u);
+      if (k < n_pts) {
+        memcpy(pts.data() + at, p16 + k * 16, 64);
+        hbn::store(sc[k], scs.data() + scs.size() - 8, 8);
+      }
+    }
+  };
+  uint32_t rows = 0;
+  for (uint32_t j = 0; j < count; ++j) {
+    const fsdkr_recover_job& J = jobs[j];
+    if (out[j].status == FSDKR_RECOVER_PANIC_DECRYPT) continue;
+    const uint32_t T = J.t_vss + 1, nl = J.nl;
+    const hbn::Limbs N = hbn::mul(hbn::from(J.p, nl), hbn::from(J.q, nl));
+    hbn::Limbs acc;
+    for (uint32_t k = 0; k < T; ++k) acc = hbn::add(acc, hbn::mul(li[j][k], hbn::from(plain[j].data() + (size_t)k * nl, nl)));
+    const hbn::Limbs share = hbn::mod(hbn::mod(acc, N), Q);
+    memset(out[j].share, 0, sizeof out[j].share);
+    hbn::store(share, out[j].share, 8);
+    row_of[j] = rows;
+    add_row(SECP_G, 1, std::vector<hbn::Limbs>{share});
+    const uint32_t tp = std::min(J.t_key, J.t_vss) + 1;
+    for (uint32_t i = 0; i < J.n_new; ++i) add_row(J.points + (size_t)i * tp * 16, tp, li[j]);
+    rows += 1 + J.n_new;
+    if (J.t_key > J.t_vss) out[j].status = FSDKR_RECOVER_PANIC_LI;
+  }
+  if (!rows) return FSDKR_OK;
+  std::vector<uint32_t> res((size_t)rows * 16);
+  int rc = fsdkr_ec_msm(ctx, rows, terms, pts.data(), scs.data(), res.data());
+  if (rc) return rc;
+  for (uint32_t j = 0; j < count; ++j) {
+    if (row_of[j] == ~0u) continue;
+    const uint32_t* r = res.data() + (size_t)row_of[j] * 16;
+    memcpy(out[j].y, r, 64);
+    if (jobs[j].n_new) memcpy(out[j].pk_vec, r + 16, (size_t)jobs[j].n_new * 64);
+  }
+  return FSDKR_OK;
+}
+
 }  // extern "C"

@@ -52,6 +52,20 @@ class VerdictsC(ctypes.Structure):
                [(f, ctypes.c_uint32) for f in ("cap_pairs", "cap_msgs", "cap_joins")]
 
 
+class RecoverJobC(ctypes.Structure):
+    _fields_ = [("nl", ctypes.c_uint32), ("t_vss", ctypes.c_uint32), ("t_key", ctypes.c_uint32),
+                ("n_new", ctypes.c_uint32), ("old_index", u32p), ("cts", u32p), ("p", u32p), ("q", u32p),
+                ("points", u32p)]
+
+
+class RecoveredC(ctypes.Structure):
+    _fields_ = [("share", ctypes.c_uint32 * 8), ("y", ctypes.c_uint32 * 16), ("pk_vec", u32p),
+                ("status", ctypes.c_int32)]
+
+
+RECOVER_OK, RECOVER_PANIC_LI, RECOVER_PANIC_DECRYPT = 0, 1, 2
+
+
 class ErrorC(ctypes.Structure):
     _fields_ = [("variant", ctypes.c_int32), ("panic", ctypes.c_int32), ("f", ctypes.c_uint32 * 4),
                 ("keys_applied", ctypes.c_uint32)]
@@ -71,6 +85,9 @@ def lib():
     vp = ctypes.c_void_p
     L.fsdkr_ctx_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(vp)]
     L.fsdkr_ctx_create.restype = ctypes.c_int
+    L.fsdkr_collect_recover.argtypes = [vp, ctypes.POINTER(RecoverJobC), ctypes.c_uint32,
+                                        ctypes.POINTER(RecoveredC)]
+    L.fsdkr_collect_recover.restype = ctypes.c_int
     L.fsdkr_ctx_destroy.argtypes = [vp]
     L.fsdkr_ctx_destroy.restype = None
     L.fsdkr_last_error.argtypes = [vp]
@@ -404,6 +421,43 @@ class Context:
                                                         _ptr(A), _ptr(Z),
                                                         out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out
+
+    def collect_recover(self, jobs):
+        """fsdkr_collect_recover: jobs = [dict(nl, t_vss, t_key, old_index, cts, p, q, points)],
+        points[i] = the first min(t_key, t_vss)+1 committed points for new party i.
+        Returns per job (status, share, y, pk_vec); a ciphertext wider than N^2
+        raises ValueError (ints_to_limbs)."""
+        from . import _pack
+        keep, cj = [], (RecoverJobC * len(jobs))()
+        outs = (RecoveredC * len(jobs))()
+        for k, j in enumerate(jobs):
+            nl, T = j["nl"], len(j["cts"])
+            tp = min(j["t_key"], j["t_vss"]) + 1
+            idx = np.ascontiguousarray(np.asarray(j["old_index"], dtype=np.uint32))
+            C = ints_to_limbs(j["cts"], 2 * nl)
+            Pp, Qq = ints_to_limbs([j["p"]], nl), ints_to_limbs([j["q"]], nl)
+            n_new = len(j["points"])
+            Pt = np.zeros((max(1, n_new * tp), 16), dtype=np.uint32)
+            if n_new:
+                _pack.points([pt for row in j["points"] for pt in row], None, Pt)
+            PK = np.zeros((max(1, n_new), 16), dtype=np.uint32)
+            keep.append((idx, C, Pp, Qq, Pt, PK))
+            cj[k] = RecoverJobC(nl, j["t_vss"], j["t_key"], n_new, _ptr(idx), _ptr(C), _ptr(Pp), _ptr(Qq), _ptr(Pt))
+            outs[k].pk_vec = _ptr(PK)
+            assert T == j["t_vss"] + 1
+        self.check(self._lib.fsdkr_collect_recover(self._h, cj, len(jobs), outs))
+
+        def point(v):
+            x, y = v & ((1 << 256) - 1), v >> 256
+            return None if (x == 0 and y == 0) else (x, y)
+        res = []
+        for k, j in enumerate(jobs):
+            o = outs[k]
+            share = int.from_bytes(bytes(o.share), "little")
+            y = point(int.from_bytes(bytes(o.y), "little"))
+            pk = [point(v) for v in limbs_to_ints(keep[k][5][:len(j["points"])])] if j["points"] else []
+            res.append((int(o.status), share, y, pk))
+        return res
 
     def ec_msm(self, points, scalars):
         """points/scalars: lists (count) of equal-length lists; points are (x, y) or None."""

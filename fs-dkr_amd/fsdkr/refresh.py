@@ -19,7 +19,7 @@ checks and before any paillier_key_vec write; decryption and the pk_vec loop
 (:439-464) after them.
 collect_many() verifies many independent sessions in one device pass
 (BASELINE configs[4]).  There is no CPU fallback."""
-from ._native import Context, FsdkrError
+from ._native import Context
 from .batch import CollectBatch, SessionSet
 
 Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
@@ -363,78 +363,32 @@ def _dk_limbs(dk):
 
 
 def _speculative(ctx, jobs):
-    """Share recovery of every job (msgs, local_key, n_new) on the recovery stream:
-    one batched decryption per key width + one MSM launch for all of them.  Per
-    job: the 4-tuple of recover_share or the exception the reference raises there."""
-    plans = []
-    for msgs, lk, n_new in jobs:
+    """Share recovery of every job (msgs, local_key, n_new) in one
+    fsdkr_collect_recover call on the recovery stream (GPU decryptions + one MSM
+    launch).  Per job: the 4-tuple (share, y, pk_vec, t_ok) or the exception the
+    reference raises there."""
+    out = [None] * len(jobs)
+    todo, cj = [], []
+    for k, (msgs, lk, n_new) in enumerate(jobs):
         try:
-            plans.append(_recovery_plan(msgs, lk, n_new))
-            if _dk_limbs(lk.paillier_dk) is None:
-                plans[-1] = FsDkrPanic("share recovery: decryption key wider than 6144 bits")
+            plan = _recovery_plan(msgs, lk, n_new)
+            nl = _dk_limbs(lk.paillier_dk)
+            if nl is None:
+                raise FsDkrPanic("share recovery: decryption key wider than 6144 bits")
+            if max(c.bit_length() for c in plan["cts"]) > 64 * nl:
+                raise FsDkrPanic("share recovery: a ciphertext wider than N^2")
         except (FsDkrPanic, IndexError, AttributeError, TypeError) as e:
-            plans.append(e if isinstance(e, FsDkrPanic) else FsDkrPanic(f"share recovery: {e!r}"))
-    sig_of = {}
-    for w in (64, 96, 128, 192):
-        cts, kidx, ps, qs, owners = [], [], [], [], []
-        for j, (p, (msgs, lk, n_new)) in enumerate(zip(plans, jobs)):
-            if isinstance(p, Exception) or _dk_limbs(lk.paillier_dk) != w:
-                continue
-            owners.append((j, len(cts), len(p["cts"])))
-            for c in p["cts"]:
-                cts.append(c)
-                kidx.append(len(ps))
-            ps.append(lk.paillier_dk.p)
-            qs.append(lk.paillier_dk.q)
-        if not cts:
+            out[k] = e if isinstance(e, FsDkrPanic) else FsDkrPanic(f"share recovery: {e!r}")
             continue
-        try:
-            sig = ctx.paillier_decrypt_many(cts, kidx, ps, qs, w)
-        except (ValueError, FsdkrError):
-            # a ciphertext wider than N^2 (ints_to_limbs) or a degenerate key the
-            # batched decryption refuses (p == q, p == 1, even p): decrypt each
-            # job on its own so one bad key fails only its own session
-            for j, at, cnt in owners:
-                lk = jobs[j][1]
-                try:
-                    sig_of[j] = ctx.paillier_decrypt_many(plans[j]["cts"], [0] * cnt, [lk.paillier_dk.p],
-                                                          [lk.paillier_dk.q], w)
-                except (ValueError, FsdkrError) as e:
-                    plans[j] = FsDkrPanic(f"share recovery: Paillier::decrypt ({e})")
-            continue
-        for j, at, cnt in owners:
-            sig_of[j] = sig[at:at + cnt]
-    return _finish_recovery(ctx, plans, sig_of)
-
-
-def _finish_recovery(ctx, plans, sig_of):
-    """new share = sum_j l_j Dec(c_j) mod N mod q; y and pk_vec by one MSM launch."""
-    rows, scs = [], []
-    width = 1
-    for j, p in enumerate(plans):
-        if isinstance(p, Exception):
-            continue
-        m = sig_of[j]
-        new_share = sum(l * s for l, s in zip(p["li"], m)) % p["N"] % Q
-        p["share"] = new_share
-        rows.append([(GX, GY)])
-        scs.append([new_share])
-        for i in range(p["n_new"]):
-            rows.append(p["pts"][i])
-            scs.append(p["li"][:len(p["pts"][i])])
-        width = max([width] + [len(r) for r in p["pts"]])
-    rows = [r + [None] * (width - len(r)) for r in rows]
-    scs = [r + [0] * (width - len(r)) for r in scs]
-    res = ctx.ec_msm(rows, scs) if rows else []
-    out, pos = [], 0
-    for p in plans:
-        if isinstance(p, Exception):
-            out.append(p)
-            continue
-        y = res[pos]
-        pk = res[pos + 1:pos + 1 + p["n_new"]]
-        pos += 1 + p["n_new"]
-        out.append((p["share"], y, pk, p["t_ok"]))
+        todo.append(k)
+        cj.append(dict(nl=nl, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=plan["cts"],
+                       p=lk.paillier_dk.p, q=lk.paillier_dk.q, points=plan["pts"]))
+    if cj:
+        for k, (status, share, y, pk) in zip(todo, ctx.collect_recover(cj)):
+            if status == 2:   # FSDKR_RECOVER_PANIC_DECRYPT
+                out[k] = FsDkrPanic("share recovery: Paillier::decrypt (degenerate decryption key)")
+            else:
+                out[k] = (share, y, pk, status != 1)   # 1: FSDKR_RECOVER_PANIC_LI
     return out
 
 
@@ -464,8 +418,7 @@ def _recovery_plan(msgs, local_key, n_new):
     t_key = local_key.t
     terms = min(t_key, t_vss) + 1
     pts = [[msgs[j].points_committed_vec[i] for j in range(terms)] for i in range(n_new)]
-    dk = local_key.paillier_dk
-    return {"li": li, "cts": cts, "pts": pts, "n_new": n_new, "N": dk.p * dk.q, "t_ok": t_key <= t_vss}
+    return {"t_vss": t_vss, "index": [msgs[j].old_party_index for j in range(t_vss + 1)], "cts": cts, "pts": pts}
 
 
 def recover_share(ctx, msgs, party_index, t, dk, nl, n_new):

@@ -340,6 +340,43 @@ int fsdkr_paillier_decrypt_multi(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, co
 int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t* points, const uint32_t* scalars,
                  uint32_t* out);
 
+/* Share recovery of collect() in one call, for `count` independent jobs (one
+ * party of RefreshMessage::collect, JoinMessage::collect, or one session of a
+ * multi-session batch): refresh_message.rs:367-373 (get_ciphertext_sum) and
+ * :439-464 (Paillier::decrypt, x_i, y, pk_vec), add_party_message.rs:183-213.
+ * Job j: the Lagrange weights l_k of the first t_vss+1 messages' old indices
+ * (curv map_share_to_new_params), the decryption of the party's ciphertext
+ * from each of them under (p, q), new share = (sum_k l_k Dec(c_k) mod N) mod q
+ * (decryption is a homomorphism on units of Z_{N^2}: the reference's decryption
+ * of prod_k c_k^l_k * Enc(0)), y = G*share and pk_vec[i] = sum_{k <= t'}
+ * l_k * points[i][k] for i < n_new, t' = min(t_key, t_vss).  The decryptions and
+ * multi-scalar multiplications run on the GPU on the recovery stream (they
+ * overlap a launched collect batch).  Index checks the reference performs by
+ * indexing its own vectors (the party's ciphertext, t_vss+1 messages) belong to
+ * the caller, which extracts the arrays below. */
+typedef struct fsdkr_recover_job {
+  uint32_t nl;                /* limbs of N = p q: 64, 96, 128 or 192 */
+  uint32_t t_vss;             /* VSS threshold of local_key.vss_scheme: t_vss+1 messages combine */
+  uint32_t t_key;             /* local_key.t: the pk_vec sums run k = 0..t_key (:460) */
+  uint32_t n_new;             /* pk_vec entries to rebuild (refresh + join messages) */
+  const uint32_t* old_index;  /* [t_vss+1] old_party_index of message k (1-based) */
+  const uint32_t* cts;        /* [t_vss+1][2nl] points_encrypted_vec[i-1] of message k */
+  const uint32_t* p;          /* [nl] */
+  const uint32_t* q;          /* [nl] */
+  const uint32_t* points;     /* [n_new][min(t_key,t_vss)+1][16] points_committed_vec[i] of message k */
+} fsdkr_recover_job;
+/* status of a recovered job */
+#define FSDKR_RECOVER_OK 0
+#define FSDKR_RECOVER_PANIC_LI 1       /* t_key > t_vss: li_vec[k] out of bounds in the pk_vec loop (:460-462) */
+#define FSDKR_RECOVER_PANIC_DECRYPT 2  /* the decryption key is degenerate (p == q, even, 1): Paillier::decrypt */
+typedef struct fsdkr_recovered {
+  uint32_t share[8];          /* new x_i, reduced mod q */
+  uint32_t y[16];             /* G * x_i (affine; (0,0) = infinity) */
+  uint32_t* pk_vec;           /* caller's [n_new][16] */
+  int32_t status;             /* FSDKR_RECOVER_* */
+} fsdkr_recovered;
+int fsdkr_collect_recover(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count, fsdkr_recovered* out);
+
 /* Kernel timing (needs FSDKR_CFG_TIMING): accumulated milliseconds and launch
  * count of kernel `name` since the last reset ("modexp", "mod_setup", ...). */
 int fsdkr_kernel_time(const fsdkr_ctx* ctx, const char* name, double* ms, uint32_t* launches);

@@ -77,6 +77,21 @@ class OracleDevice:
     def paillier_decrypt_many(self, cts, key_idx, ps, qs, nl):
         return [paillier.decrypt(paillier.DecryptionKey(ps[k], qs[k]), c) for c, k in zip(cts, key_idx)]
 
+    def collect_recover(self, jobs):
+        """fsdkr_collect_recover restated: Lagrange weights (oracle.vss), the
+        oracle's decryption, share = sum l_k m_k mod N mod q, y and pk_vec."""
+        from oracle.vss import map_share_to_new_params
+        out = []
+        for j in jobs:
+            idx = [x - 1 for x in j["old_index"]]
+            li = [map_share_to_new_params(idx[k], idx) for k in range(len(idx))]
+            dk = paillier.DecryptionKey(j["p"], j["q"])
+            ms = [paillier.decrypt(dk, c) for c in j["cts"]]
+            share = sum(l * m for l, m in zip(li, ms)) % (j["p"] * j["q"]) % ec.Q
+            pk = self.ec_msm(j["points"], [li[:len(row)] for row in j["points"]])
+            out.append((1 if j["t_key"] > j["t_vss"] else 0, share, ec.mul(ec.G, share), pk))
+        return out
+
     def ec_msm(self, rows, scs):
         out = []
         for row, sc in zip(rows, scs):

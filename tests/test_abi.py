@@ -37,7 +37,8 @@ def test_struct_layout(tmp_path):
     import subprocess
     from fsdkr import _native
     pairs = [("fsdkr_collect_batch", _native.CollectBatchC), ("fsdkr_verdicts", _native.VerdictsC),
-             ("fsdkr_error", _native.ErrorC)]
+             ("fsdkr_error", _native.ErrorC), ("fsdkr_recover_job", _native.RecoverJobC),
+             ("fsdkr_recovered", _native.RecoveredC)]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "fsdkr/fsdkr.h"', "int main(void){"]
     for cname, py in pairs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')

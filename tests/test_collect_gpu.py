@@ -291,3 +291,30 @@ def test_prestart_drops_a_plan_that_reads_it(gpu_ctx):
     want = [7] * 9
     want[1] = 7 & ~2
     assert [int(x) & 7 for x in v2.pdl] == want
+
+
+def test_collect_recover_entry(gpu_ctx, dkr5):
+    """fsdkr_collect_recover (share recovery in one C-ABI call, refresh_message.rs:367-373,
+    439-464) against the oracle's collect() for every party of a t=2 n=5 refresh, in one
+    call with a degenerate-key job (p == q: Paillier::decrypt panics) and a job whose
+    local_key.t exceeds the VSS threshold (li_vec index panic) beside them."""
+    from fsdkr.refresh import _dk_limbs
+    keys, msgs, dks, _ = dkr5
+    jobs, want = [], []
+    for party in range(5):
+        lk = keys[party]
+        t = lk.vss_scheme.threshold
+        jobs.append(dict(nl=_dk_limbs(lk.paillier_dk), t_vss=t, t_key=lk.t,
+                         old_index=[m.old_party_index for m in msgs[:t + 1]],
+                         cts=[m.points_encrypted_vec[lk.i - 1] for m in msgs[:t + 1]],
+                         p=lk.paillier_dk.p, q=lk.paillier_dk.q,
+                         points=[[m.points_committed_vec[i] for m in msgs[:t + 1]] for i in range(5)]))
+        ko = lk.clone()
+        protocol.collect(copy.deepcopy(msgs), ko, dks[party], [], Rng("a8"), KB)
+        want.append((0, ko.x_i, ko.y, ko.pk_vec[:5]))
+    bad = dict(jobs[1], q=jobs[1]["p"])
+    over = dict(jobs[2], t_key=jobs[2]["t_vss"] + 1)
+    got = gpu_ctx.collect_recover(jobs + [bad, over])
+    assert got[:5] == want
+    assert got[5][0] == 2                       # FSDKR_RECOVER_PANIC_DECRYPT
+    assert got[6][0] == 1 and got[6][1:3] == want[2][1:3]   # FSDKR_RECOVER_PANIC_LI, share still recovered
