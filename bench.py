@@ -101,11 +101,10 @@ def efficiency(work, issued, seconds, world=1):
 
 def cpu_baseline(batch, verdict_ref, proofs, threads, seconds_budget=12.0):
     """The C++ restatement of collect()'s verification over GMP (oracle/cpu_baseline.cpp,
-    dlopen libgmp.so.10: the reference's own bignum engine) on this host, on a
-    bounded sample of the SAME packed workload (pairs from the start of the
-    batch, whole ring-Pedersen / correct-key / DLog proofs), on 1 thread and on
-    `threads` threads; extrapolated to the full proof mix.  Its verdicts on the
-    sample are checked against the GPU's."""
+    dlopen libgmp.so.10: the reference's own bignum engine) on this host over the
+    SAME packed workload: the whole verification timed on `threads` threads
+    (about 7 s at n = 64), every verdict checked against the GPU's; the
+    single-thread figure is extrapolated from a bounded sample."""
     from oracle import cpu_baseline as cb
     out = cb.measure(batch, verdict_ref, threads=threads, budget_s=seconds_budget)
     out["value"] = proofs / out["collect_s"]

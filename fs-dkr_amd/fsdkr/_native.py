@@ -64,6 +64,8 @@ class RecoveredC(ctypes.Structure):
 
 
 RECOVER_OK, RECOVER_PANIC_LI, RECOVER_PANIC_DECRYPT = 0, 1, 2
+DRAW_BITS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                ctypes.c_uint32)
 
 
 class ErrorC(ctypes.Structure):
@@ -88,6 +90,9 @@ def lib():
     L.fsdkr_collect_recover.argtypes = [vp, ctypes.POINTER(RecoverJobC), ctypes.c_uint32,
                                         ctypes.POINTER(RecoveredC)]
     L.fsdkr_collect_recover.restype = ctypes.c_int
+    L.fsdkr_sample_primes.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                      DRAW_BITS_FN, vp, u32p, ctypes.c_uint32]
+    L.fsdkr_sample_primes.restype = ctypes.c_int
     L.fsdkr_ctx_destroy.argtypes = [vp]
     L.fsdkr_ctx_destroy.restype = None
     L.fsdkr_last_error.argtypes = [vp]
@@ -294,6 +299,29 @@ class Context:
         V = np.zeros(count, dtype=np.uint32)
         self.check(self._lib.fsdkr_miller_rabin(self._h, mod_limbs, count, _ptr(C), _ptr(B), _ptr(V)))
         return V.tolist()
+
+    def sample_primes(self, draw_bits, bits, count, window=0, span=0):
+        """fsdkr_sample_primes: `count` primes of `bits` bits by the batched prime
+        walk; draw_bits(k) supplies the k-bit random starts (the caller's RNG)."""
+        limbs = (bits + 31) // 32
+        errs = []
+
+        def cb(_user, nbits, out, nl):
+            try:
+                v = draw_bits(nbits)
+                for k in range(nl):
+                    out[k] = (v >> (32 * k)) & 0xFFFFFFFF
+                return 0
+            except Exception as e:   # re-raised below, after the C call returns
+                errs.append(e)
+                return 1
+        fn = DRAW_BITS_FN(cb)
+        O = np.zeros((max(1, count), limbs), dtype=np.uint32)
+        rc = self._lib.fsdkr_sample_primes(self._h, bits, count, window, span, fn, None, _ptr(O), limbs)
+        if errs:
+            raise errs[0]
+        self.check(rc)
+        return limbs_to_ints(O[:count])
 
     # ---- collect() verification -------------------------------------------
     def verify_collect(self, batch):

@@ -311,6 +311,24 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
                                const uint32_t* S, const uint32_t* T, const uint32_t* N, const uint32_t* A,
                                const uint32_t* Z, uint8_t* verdict);
 
+/* The prime walk above it (kzen-paillier Paillier::keypair_with_modulus_size's
+ * prime generation, restated: the walk oracle/keygen.py follows).  `count`
+ * probable primes of `bits` bits (bits >= 64; top two bits set) by independent
+ * walks: walk w draws a start s (`draw`: bits uniform random bits, OR-ed with
+ * 3 << (bits-2) | 1) and returns the first of s, s+2, ..., s+2(span-1) that has
+ * no odd prime factor below 2000, passes a Miller-Rabin round to base 2 and
+ * MR rounds 8 more rounds to bases 2 + (SHA-256("fsdkr-mr" | c | j | ctr)
+ * stream mod (c - 3)); a walk with no prime draws a new start after every walk
+ * of its pass is settled.  Draw order: every walk's start first, in walk order.
+ * The base-2 rounds of `window` survivors of every unsettled walk run as one GPU
+ * launch (fsdkr_miller_rabin), then the extra rounds of each walk's first
+ * passer.  span 0 = 4 * bits, window 0 = max(32, bits / 8).  out: [count][limbs],
+ * limbs >= ceil(bits / 32).  `draw` returns 0 on success (non-zero aborts with
+ * FSDKR_E_ARG). */
+typedef int (*fsdkr_draw_bits_fn)(void* user, uint32_t bits, uint32_t* out, uint32_t limbs);
+int fsdkr_sample_primes(fsdkr_ctx* ctx, uint32_t bits, uint32_t count, uint32_t window, uint32_t span,
+                        fsdkr_draw_bits_fn draw, void* user, uint32_t* out, uint32_t limbs);
+
 /* ---- Job 1: Paillier encryption of the shares (refresh_message.rs:72-84) ----
  * out[k] = (1 + m[k] N) * r[k]^N mod N^2, N = ns[n_idx[k]]  (kzen-paillier
  * encrypt_with_chosen_randomness).  m: [count][ml], r: [count][nl] (< N),

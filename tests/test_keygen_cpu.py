@@ -43,38 +43,3 @@ def test_carmichael_and_primes():
         assert ok.is_probable_prime(p)
         assert all(ok.strong_probable_prime(p, b) for b in (2, 3, p - 1, 1))
     assert not ok.is_probable_prime(((1 << 521) - 1) * ((1 << 127) - 1))
-
-
-def test_product_sieve_matches_trial_division():
-    from fsdkr import keygen
-    for s in range(3):
-        st = Rng(("sv", s)).bits(1024) | 1 | (3 << 1022)
-        got = set(keygen.sieve(st, 2048).tolist())
-        want = {i for i in range(2048) if all((st + 2 * i) % p for p in ok.SMALL_PRIMES)}
-        assert got == want
-
-
-def test_product_witness_bases_match_oracle():
-    from fsdkr import keygen
-    for c in ((1 << 521) - 1, Rng("w").prime(512), 2047 * 89 + 2):
-        assert keygen.witness_bases(c) == ok.witness_bases(c)
-        assert all(2 <= b <= c - 2 for b in keygen.witness_bases(c))
-
-
-class _CpuMr:
-    """Host-logic harness: answers fsdkr_miller_rabin with the oracle so the
-    batched walk schedule (windows, passers, redraw passes) is checked without
-    a GPU.  Test infrastructure only; the GPU test runs the real kernel."""
-
-    def miller_rabin(self, cands, bases, mod_limbs):
-        assert all(c.bit_length() <= 32 * mod_limbs for c in cands)
-        return [1 if ok.strong_probable_prime(c, b) else 0 for c, b in zip(cands, bases)]
-
-
-@pytest.mark.parametrize("span,window", [(0, 0), (24, 4), (8, 3)])
-def test_product_walk_schedule_matches_oracle(span, window):
-    """Short walks (span 8/24) fail often, exercising the redraw passes."""
-    from fsdkr import keygen
-    got = keygen.sample_primes(_CpuMr(), Rng(("sched", span)), 192, 10, window=window or None, span=span or None)
-    want = ok.sample_primes(Rng(("sched", span)), 192, 10, span=span)
-    assert got == want

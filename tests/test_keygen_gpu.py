@@ -68,10 +68,35 @@ def test_miller_rabin_rejects_bad_input(gpu_ctx):
 
 @pytest.mark.parametrize("bits,count,span", [(512, 6, 0), (1024, 3, 0), (256, 8, 24)])
 def test_sample_primes_match_oracle(gpu_ctx, bits, count, span):
+    """fsdkr_sample_primes (the C-ABI prime walk) against the oracle's walk for the same draws."""
     from fsdkr import keygen
     got = keygen.sample_primes(gpu_ctx, Rng(("sp", bits)), bits, count, span=span or None)
     want = ok.sample_primes(Rng(("sp", bits)), bits, count, span=span)
     assert got == want
+
+
+@pytest.mark.parametrize("span,window", [(0, 0), (24, 4), (8, 3)])
+def test_walk_schedule_matches_oracle(gpu_ctx, span, window):
+    """Short walks (span 8/24) and small windows fail often, exercising the redraw
+    passes and the passer queue of the C walk; the primes equal the oracle's."""
+    from fsdkr import keygen
+    got = keygen.sample_primes(gpu_ctx, Rng(("sched", span)), 192, 10, window=window or None, span=span or None)
+    want = ok.sample_primes(Rng(("sched", span)), 192, 10, span=span)
+    assert got == want
+
+
+def test_sample_primes_draw_errors(gpu_ctx):
+    """An RNG that raises aborts the walk with that exception; bad widths are refused."""
+    from fsdkr import keygen
+    from fsdkr._native import FsdkrError
+
+    class Broken:
+        def bits(self, k):
+            raise OSError("entropy source gone")
+    with pytest.raises(OSError):
+        keygen.sample_primes(gpu_ctx, Broken(), 512, 2)
+    with pytest.raises(FsdkrError):
+        gpu_ctx.sample_primes(Rng("x").bits, 4096, 1)   # 128-limb candidates: no MR shape
 
 
 def test_single_keypair_matches_oracle_paillier(gpu_ctx):
