@@ -271,6 +271,12 @@ struct CollectPlan {
   // operands read them from the prestart buffer once ga_done has fired
   bool ga_hit = false;
   hipEvent_t ga_done = nullptr;
+  // the prestart's Montgomery constants of the N_i^2 (the same rows launch() needs
+  // for J2 / eq / prod3), ready at ga_setup: launch() reuses them instead of
+  // running its own mod_setup on the main chain
+  const uint32_t* pre_cons_nn = nullptr;
+  bool pre_cons_wide = false;
+  hipEvent_t ga_setup = nullptr;
   // h1 / h2 fixed-base tables built by fsdkr_collect_prestart (fb_hit)
   bool fb_hit = false;
   FbPre fb_pre;
@@ -299,6 +305,8 @@ struct GaPre {
   uint32_t* out = nullptr;               // [2P][nn]: J1 instance order (s2^N rows, then s^N rows)
   hipEvent_t done = nullptr;
   hipEvent_t ga_setup = nullptr;   // GA's Montgomery constants ready (before its chains)
+  const uint32_t* cons = nullptr;   // those constants (KD 160 when `wide`, else the width's KD)
+  bool wide = false;
   // the fixed-base tables of h1_i, h2_i (bases 2i, 2i+1 of prepare's FbJob), built
   // for exponents of up to bits_h1 / bits_h2 bits with window w
   bool fb_valid = false;

@@ -32,16 +32,27 @@ int collect_launch_impl(Ctx* c) {
     return rc;
   // moduli constants
   uint32_t *cons_nn = nullptr, *cons_nl = nullptr, *cons_ck = nullptr;
-  if ((rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn, "collect_nn"))) return rc;
+  const bool reuse_nn = pl.ga_hit && pl.pre_cons_nn && !pl.pre_cons_wide;
+  if (reuse_nn) {   // the prestart's constants of the same N_i^2 rows
+    (void)hipStreamWaitEvent(st, pl.ga_setup, 0);
+    cons_nn = const_cast<uint32_t*>(pl.pre_cons_nn);
+  } else if ((rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn, "collect_nn"))) {
+    return rc;
+  }
   if ((rc = setup_moduli(c, nl, PI(pl.o_mods), pl.n_mods_nl, &cons_nl, "collect_nl"))) return rc;
   if ((rc = setup_moduli(c, pl.ckl, PI(pl.o_ckmods), Mt, &cons_ck, "collect_ck"))) return rc;
   // J2 / J5 (256-bit challenge exponents): 8 lanes per instance
   const uint32_t j2_group = 8, j5_group = 8;
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;
-  if (ga_group == kWideGroup && pl.jcount[0] &&
-      (rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup)))
-    return rc;
+  if (ga_group == kWideGroup && pl.jcount[0]) {
+    if (pl.ga_hit && pl.pre_cons_nn && pl.pre_cons_wide) {
+      (void)hipStreamWaitEvent(st, pl.ga_setup, 0);
+      cons_nn_w = const_cast<uint32_t*>(pl.pre_cons_nn);
+    } else if ((rc = setup_moduli(c, nn, PI(pl.o_NN), n, &cons_nn_w, "collect_nn_w", kWideGroup))) {
+      return rc;
+    }
+  }
   // ---- stream plan (up to thirteen concurrent lanes of work: give HIP >= 12 hardware
   //      queues, GPU_MAX_HW_QUEUES, or streams share queues and serialise):
   //   side 0  : GA (nn, long exponents, priority)               | start after mod_setup

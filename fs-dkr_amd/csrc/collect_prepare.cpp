@@ -99,6 +99,9 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   GaPre* gpre = reinterpret_cast<GaPre*>(c->ga_pre);
   if (pl.ga_hit) {
     pl.ga_done = gpre->done;
+    pl.ga_setup = gpre->ga_setup;
+    pl.pre_cons_nn = gpre->cons;
+    pl.pre_cons_wide = gpre->wide;
     gpre->valid = false;   // consumed (the buffer lives until the next prestart)
   }
   clk.lap("shapes");

@@ -228,6 +228,8 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
                          group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
     return rc;
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
+  g.cons = cons;
+  g.wide = group == kWideGroup;
   if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
     return rc;
   (void)hipEventRecord(g.ga_setup, gs);   // GA's constants are ready

@@ -36,6 +36,9 @@ __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __rest
   const int li = threadIdx.x / G;
   const uint32_t m = blockIdx.x * IPB + li;
   if (m >= n_mod) return;
+  // a few waves at the head of every job's chain: they win issue arbitration
+  // against the exponentiation waves already on the SIMD
+  __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* N = mods + (size_t)m * K32;
   MT M;

@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
   }
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0x00);   // [0,0,0,0]
-  else if constexpr (G == 8) return FSDKR_DPP_BANK(FSDKR_DPP_BANK(v, v, 0x150, 0x3), v, 0x158, 0xC);
+  else if constexpr (G == 8) return FSDKR_DPP_BANK(FSDKR_DPP(v, 0x150), v, 0x158, 0xC);   // lane 0, then lane 8 into 8..15
   else return FSDKR_DPP(v, 0x150);                        // row_newbcast:0
 }
 template <int G>
@@ -84,6 +84,17 @@ __device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0x90);   // [0,0,1,2]
   else return FSDKR_DPP(v, 0x111);                        // row_shr:1
+}
+// value of lane g+1, rotating within the group (the top lane reads lane 0), where
+// one DPP move does it (G = 2, 4: quad_perm; G = 16: row_ror:15); HAS_ROT<G>
+template <int G>
+constexpr bool HAS_ROT = G == 2 || G == 4 || G == 16;
+template <int G>
+__device__ __forceinline__ uint32_t dpp_next_rot(uint32_t v) {
+  static_assert(HAS_ROT<G>, "no single-move rotation for this group size");
+  if constexpr (G == 2) return FSDKR_DPP(v, 0xB1);        // [1,0,3,2]
+  else if constexpr (G == 4) return FSDKR_DPP(v, 0x39);   // [1,2,3,0]
+  else return FSDKR_DPP(v, 0x12F);                        // row_ror:15
 }
 // group-wide max over the G lanes
 template <int G>
@@ -191,30 +202,70 @@ struct Mont29 {
   static constexpr bool sq_raw(int d) { return d == 0 || (L % 2 == 0 && d == L / 2); }
   static constexpr bool sq_dbl(int d) { return d > 0 && (L % 2 == 1 ? d <= L / 2 : d < L / 2); }
 
-  // one CIOS row at rotation R (logical column j lives in slot (j+R)%L)
+  // a_r * b_j into slot (j + R) % L (squaring rows: the tournament slots only)
+  template <int R, bool SQ, int J>
+  __device__ __forceinline__ void mac_ab(uint64_t* acc, const uint32_t* b, uint32_t ai, uint32_t a2) const {
+    if constexpr (SQ) {
+      constexpr int d = (J - R % L + L) % L;
+      if constexpr (sq_raw(d)) mac(acc[(J + R) % L], ai, b[J]);
+      else if constexpr (sq_dbl(d)) mac(acc[(J + R) % L], a2, b[J]);
+    } else {
+      mac(acc[(J + R) % L], ai, b[J]);
+    }
+  }
+  template <int R, bool SQ, int... Js>
+  __device__ __forceinline__ void mac_ab_rest(uint64_t* acc, const uint32_t* b, uint32_t ai, uint32_t a2,
+                                              std::integer_sequence<int, Js...>) const {
+    (mac_ab<R, SQ, Js + 1>(acc, b, ai, a2), ...);
+  }
+
+  // One CIOS row at rotation R (logical column j lives in slot (j+R)%L).  For
+  // the long-lane throughput shapes (ORDERED: L > FSDKR_ROW_FENCE_MIN_L with a
+  // rotating DPP move, i.e. G = 2 / 4) the order is fixed by scheduling barriers
+  // so every dependent step has independent MACs between it and its producer (no
+  // s_nop before the DPP moves, the quotient's v_mul_lo latency hidden):
+  //   a_r*b_0 (the retiring column s0), m = s0 * n' (lane-local), a_r*b_1..L-1,
+  //   broadcast m, m*n_0, carry/digit of s0, m*n_1, carry into s1, m*n_2..L-1,
+  //   the retired digit moves down one lane.
+  // Short lanes (latency shapes) keep the compiler's order, which interleaves
+  // consecutive rows (measured: the fixed order cost 4-8 % at 8 lanes,
+  // profiles/r03d_row_order_ab.txt).
+  static constexpr bool ORDERED = HAS_ROT<G> && L > FSDKR_ROW_FENCE_MIN_L;
   template <int R, bool SQ>
   __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, const uint32_t* n, uint32_t ai) const {
-    if constexpr (SQ) {
-      const uint32_t a2 = ai << 1;
-#pragma unroll
-      for (int j = 0; j < L; ++j) {
-        const int d = (j - R % L + L) % L;
-        if (sq_raw(d)) mac(acc[(j + R) % L], ai, b[j]);
-        else if (sq_dbl(d)) mac(acc[(j + R) % L], a2, b[j]);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], ai, b[j]);
-    }
     constexpr int s0 = R % L, s1 = (R + 1) % L;
-    const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
+    const uint32_t a2 = SQ ? ai << 1 : 0u;
+    if constexpr (ORDERED) {
+      mac_ab<R, SQ, 0>(acc, b, ai, a2);
+      uint32_t m = ((uint32_t)acc[s0] * ninv) & M29;
+      __builtin_amdgcn_sched_barrier(0);
+      mac_ab_rest<R, SQ>(acc, b, ai, a2, std::make_integer_sequence<int, L - 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+      m = bcast_lane0<G>(m);
+      mac(acc[s0], m, n[0]);
+      uint64_t carry = acc[s0] >> 29;
+      uint32_t digit = (uint32_t)acc[s0] & M29;
+      asm volatile("" : "+v"(digit), "+v"(carry));   // computed here, not sunk to their uses
+      __builtin_amdgcn_sched_barrier(0);
+      mac(acc[s1], m, n[1]);
+      acc[s1] += carry;
 #pragma unroll
-    for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
-    // every lane carries its lowest column into the next one (value-preserving;
-    // in lane 0 that column is 0 mod 2^29 after m*n), so the digit that moves
-    // down to lane g-1 fits 29 bits: one 32-bit DPP move, no lane-0 masking
-    acc[s1] += acc[s0] >> 29;
-    acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0] & M29) & m_top);
+      for (int j = 2; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
+      __builtin_amdgcn_sched_barrier(0);
+      acc[s0] = (uint64_t)dpp_next_rot<G>(digit);   // lane 0's digit is 0: the top lane gets the 0 it needs
+    } else {
+      mac_ab<R, SQ, 0>(acc, b, ai, a2);
+      mac_ab_rest<R, SQ>(acc, b, ai, a2, std::make_integer_sequence<int, L - 1>{});
+      const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
+#pragma unroll
+      for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
+      // every lane carries its lowest column into the next one (value-preserving;
+      // in lane 0 that column is 0 mod 2^29 after m*n), so the digit that moves
+      // down to lane g-1 fits 29 bits: one 32-bit DPP move
+      acc[s1] += acc[s0] >> 29;
+      if constexpr (HAS_ROT<G>) acc[s0] = (uint64_t)dpp_next_rot<G>((uint32_t)acc[s0] & M29);
+      else acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0] & M29) & m_top);
+    }
     if constexpr (NORM_IN_CYCLE && (((R + 1) % NSTEP == 0) || (R + 1 == L))) norm_step<(R + 1) % L>(acc);
     if constexpr (ROW_FENCE) __builtin_amdgcn_sched_barrier(0);
   }

@@ -255,6 +255,8 @@ int fsdkr_ec_msm(fsdkr_ctx* ctx, uint32_t count, uint32_t terms, const uint32_t*
   return c->sync();
 }
 
+}  // extern "C"
+
 namespace {
 const uint32_t SECP_Q[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
                             0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -278,6 +280,8 @@ hbn::Limbs lagrange(const uint32_t* x, uint32_t cnt, uint32_t j, const hbn::Limb
   return hbn::mulmod(num, inv, Q);
 }
 }  // namespace
+
+extern "C" {
 
 int fsdkr_collect_recover(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count, fsdkr_recovered* out) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);

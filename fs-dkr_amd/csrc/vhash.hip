@@ -21,6 +21,7 @@ static inline uint32_t blocks_for(uint32_t n, uint32_t per) { return (n + per - 
 __global__ void binom_kernel(const BinomArgs a) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.count) return;
+  __builtin_amdgcn_s_setprio(3);   // on the main chain ahead of J5: short, latency-critical
   const uint32_t* s = P32(a.s_ptr[p]);
   const uint32_t* n = P32(a.n_ptr[p]);
   uint32_t* o = a.out + (size_t)p * a.out_limbs;
