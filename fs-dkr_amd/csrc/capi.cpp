@@ -192,8 +192,9 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   // runs only where the caller asked for it (it prepared KD = 160 constants)
   uint32_t grp = c->modexp_group ? c->modexp_group : group;
   if (grp == kWideGroup && (group != kWideGroup || k32 != 128)) grp = 16;
+  if (grp == kWaveGroup && k32 != 128) grp = 16;
   if (c->ct) grp = 0;   // the regular-access kernels have one shape per width
-  const int KD = shape_digits_g(k32, grp);
+  const int KD = table_digits(k32, grp);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
     return FSDKR_E_UNSUPPORTED;
@@ -380,7 +381,7 @@ const char* fsdkr_last_error(const fsdkr_ctx* ctx) {
 
 int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
-  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32)) return FSDKR_E_ARG;
+  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)) return FSDKR_E_ARG;
   c->modexp_group = lanes;
   return FSDKR_OK;
 }

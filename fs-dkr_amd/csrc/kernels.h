@@ -33,7 +33,11 @@ int shape_digits(uint32_t k32);   // KD for a K32-limb modulus class (0 if unsup
 // Montgomery constants (R = 2^(29 KD)) differ from the 144-digit class: a launch
 // with group kWideGroup needs consts from mod_setup_g(k32, kWideGroup, ...).
 constexpr uint32_t kWideGroup = 32;
-int shape_digits_g(uint32_t k32, uint32_t group);
+// One instance per wave64 (modexp_wave_kernel), 4096-bit class only; it uses the
+// class's own KD = 144 constants (mod_setup), table entries of 192 words.
+constexpr uint32_t kWaveGroup = 64;
+int shape_digits_g(uint32_t k32, uint32_t group);   // digits of the Montgomery constants
+int table_digits(uint32_t k32, uint32_t group);     // words per window-table entry
 hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st);
 hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint32_t n_mod, uint32_t* consts,
                        hipStream_t st);

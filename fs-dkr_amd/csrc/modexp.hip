@@ -213,6 +213,95 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
 }
 
+// One instance per wave64 (the latency shape of small launches, e.g. a
+// multi-GPU rank's GA chains): lane g holds digits gL..gL+L-1 of every operand,
+// KR digits in the first KR/L lanes and zeros above; the streamed operand of each
+// Montgomery product is read from registers with v_readlane (Mont29::product_w),
+// so the row digit and the quotient digit are wave-uniform and the quotient is
+// computed on the scalar unit.  Constants are the KR-digit class's (mod_setup).
+// Same exponentiation schedule as modexp_kernel; the window table is a global
+// slab of KD-word entries; no LDS except the final limb conversion.
+template <int KR, int L, int K32>
+__global__ __launch_bounds__(64) void modexp_wave_kernel(const ModexpArgs a) {
+  constexpr int KD = 64 * L;
+  using MT = Mont29<KD, 64, KR>;
+  constexpr int STRIDE = 3 * KR + 4;
+  __shared__ uint32_t lds[KD];
+  const int g = threadIdx.x;
+  const uint32_t inst = blockIdx.x;
+  if (inst >= a.count) return;
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  const bool live = g * L < KR;   // lanes holding digits of the KR-digit class
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = live ? C[g * L + j] : 0u;
+  M.ninv = (uint32_t)__builtin_amdgcn_readfirstlane((int)C[3 * KR]);
+  const uint32_t w = a.window;
+  const uint32_t tsize = 1u << w;
+  uint32_t* T = a.table + (size_t)inst * tsize * KD;
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[inst]);
+  const uint32_t exp_limbs = a.exp_len[inst];
+  uint32_t acc[L], opnd[L];
+  const uint32_t* B = reinterpret_cast<const uint32_t*>(a.base_ptr[inst]);
+  const int blen = (int)min(a.base_len[inst], (uint32_t)K32);
+#pragma unroll
+  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);   // 0 past the class's digits
+#pragma unroll
+  for (int j = 0; j < L; ++j) T[g * L + j] = live ? C[KR + g * L + j] : 0u;   // T[0] = R mod N
+  const uint32_t nwin = a.nwin_i ? max(1u, a.nwin_i[inst]) : a.nwin;
+  auto digit = [&](uint32_t k) -> uint32_t {
+    const uint32_t p = (nwin - 1 - k) * w;
+    const uint32_t lo = p >> 5, sh = p & 31;
+    const uint32_t v0 = (lo < exp_limbs) ? E[lo] : 0u;
+    const uint32_t v1 = (lo + 1 < exp_limbs) ? E[lo + 1] : 0u;
+    return (uint32_t)(mk64(v0, v1) >> sh) & (tsize - 1);
+  };
+  // the schedule of modexp_kernel: R^2, table build, nwin-1 windows, exit by 1
+  const uint32_t n_build = tsize - 1;
+  const uint32_t n_steps = n_build + (nwin - 1) * (w + 1) + 1;
+  uint32_t k = 1, sub = 0;
+  for (uint32_t st = 0; st < n_steps; ++st) {
+    if (st == n_build) {
+      const uint32_t d0 = digit(0);
+#pragma unroll
+      for (int j = 0; j < L; ++j) acc[j] = T[(size_t)d0 * KD + g * L + j];
+    }
+    if (st >= n_build && st < n_steps - 1 && sub < w) {
+      M.sqr_w(acc, acc);   // the ladder's squarings
+    } else {
+      const uint32_t* src = (st == 0) ? nullptr : (st < n_build) ? T + KD : (st == n_steps - 1) ? nullptr
+                                                                            : T + (size_t)digit(k) * KD;
+      if (st == 0) {
+#pragma unroll
+        for (int j = 0; j < L; ++j) opnd[j] = live ? C[2 * KR + g * L + j] : 0u;   // R^2 mod N
+      } else if (!src) {
+#pragma unroll
+        for (int j = 0; j < L; ++j) opnd[j] = (g == 0 && j == 0) ? 1u : 0u;
+      } else {
+#pragma unroll
+        for (int j = 0; j < L; ++j) opnd[j] = src[g * L + j];
+      }
+      M.mul_w(acc, acc, opnd);
+    }
+    if (st < n_build) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) T[(size_t)(st + 1) * KD + g * L + j] = acc[j];
+    } else if (st < n_steps - 1) {
+      if (++sub == w + 1) { sub = 0; ++k; }
+    }
+  }
+  M.carry_exact(acc);
+  M.sub_if_ge(acc);
+  lds_put<KD, 64>(lds, acc, g);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* O = a.out + (size_t)inst * K32;
+  for (int q = g; q < K32; q += 64) O[q] = limb_of(lds, KR, q);
+}
+
 // ---- host-side launchers -------------------------------------------------------
 template <int KD, int G, int K32>
 static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
@@ -238,6 +327,13 @@ static hipError_t launch_modexp(const ModexpArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int KR, int L, int K32>
+static hipError_t launch_modexp_wave(const ModexpArgs& a, hipStream_t st) {
+  if (a.count == 0) return hipSuccess;
+  hipLaunchKernelGGL((modexp_wave_kernel<KR, L, K32>), dim3(a.count), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
 int shape_digits(uint32_t k32) {
   switch (k32) {
     case 64: return 72;
@@ -251,6 +347,11 @@ int shape_digits(uint32_t k32) {
 int shape_digits_g(uint32_t k32, uint32_t group) {
   if (k32 == kPrimeLimbs) return 36;   // key generation only (1024-bit primes)
   return (k32 == 128 && group == kWideGroup) ? 160 : shape_digits(k32);
+}
+
+int table_digits(uint32_t k32, uint32_t group) {
+  if (k32 == 128 && group == kWaveGroup) return 192;   // 64 lanes x 3 slots
+  return shape_digits_g(k32, group);
 }
 
 hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint32_t n_mod, uint32_t* consts,
@@ -319,6 +420,7 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
     case 128:
       // 32 lanes only on explicit request: it needs KD = 160 constants (mod_setup_g)
       if (a.group == kWideGroup) return launch_modexp<160, 32, 128>(a, st);
+      if (a.group == kWaveGroup) return launch_modexp_wave<144, 3, 128>(a, st);
       // a launch past the resident-lane capacity: 4 lanes (L = 36, squaring rows
       // with 19 + 36 MACs per row) beat 8 (L = 18) by 4% (profiles/r02h_modexp_sqr.jsonl)
       switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {

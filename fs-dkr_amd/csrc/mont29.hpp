@@ -38,7 +38,10 @@ constexpr uint32_t M29 = (1u << 29) - 1;
 // G <= 4: quad_perm inside one DPP quad.  G = 8/16: row_shr/row_shl:1 inside a
 // 16-lane row (group boundaries masked by the caller), row_newbcast:n for the
 // broadcasts (two bank-masked moves for the two 8-lane groups of a row).
-#define FSDKR_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_mov_dpp((int)(v), (ctrl), 0xF, 0xF, false))
+// bound_ctrl set: a lane whose source is outside the row reads 0 (the old value
+// is undefined for these moves anyway), and the DPP-combine pass may then fold
+// the move into the VALU op that consumes it (`dpp(x) & y` as one v_and_b32_dpp)
+#define FSDKR_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_mov_dpp((int)(v), (ctrl), 0xF, 0xF, true))
 #define FSDKR_DPP_BANK(old, v, ctrl, bank) \
   ((uint32_t)__builtin_amdgcn_update_dpp((int)(old), (int)(v), (ctrl), 0xF, (bank), false))
 
@@ -49,6 +52,7 @@ constexpr uint32_t M29 = (1u << 29) - 1;
 template <int G>
 __device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
   if constexpr (G == 1) return v;
+  else if constexpr (G == 64) return (uint32_t)__builtin_amdgcn_readlane((int)v, 0);   // wave-uniform (SGPR)
   else if constexpr (G == 32) {
     const uint32_t t = FSDKR_DPP(v, 0x150);                                   // row_newbcast:0
     return (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)t, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
@@ -61,6 +65,7 @@ __device__ __forceinline__ uint32_t bcast_lane0(uint32_t v) {
 template <int G>
 __device__ __forceinline__ uint32_t bcast_top(uint32_t v) {
   if constexpr (G == 1) return v;
+  else if constexpr (G == 64) return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
   else if constexpr (G == 32) return (uint32_t)__shfl((int)v, (int)((__lane_id() & ~31u) + 31u));   // rare: once per modexp
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xF5);   // [1,1,3,3]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0xFF);   // [3,3,3,3]
@@ -71,7 +76,7 @@ __device__ __forceinline__ uint32_t bcast_top(uint32_t v) {
 template <int G>
 __device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
   if constexpr (G == 1) return v;
-  else if constexpr (G == 32) return FSDKR_DPP(v, 0x130);   // wave_shl:1
+  else if constexpr (G == 32 || G == 64) return FSDKR_DPP(v, 0x130);   // wave_shl:1 (lane 63 reads 0)
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xF5);   // [1,1,3,3]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0xF9);   // [1,2,3,3]
   else return FSDKR_DPP(v, 0x101);                        // row_shl:1
@@ -80,7 +85,7 @@ __device__ __forceinline__ uint32_t dpp_next(uint32_t v) {
 template <int G>
 __device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {
   if constexpr (G == 1) return v;
-  else if constexpr (G == 32) return FSDKR_DPP(v, 0x138);   // wave_shr:1
+  else if constexpr (G == 32 || G == 64) return FSDKR_DPP(v, 0x138);   // wave_shr:1 (lane 0 reads 0)
   else if constexpr (G == 2) return FSDKR_DPP(v, 0xA0);   // [0,0,2,2]
   else if constexpr (G == 4) return FSDKR_DPP(v, 0x90);   // [0,0,1,2]
   else return FSDKR_DPP(v, 0x111);                        // row_shr:1
@@ -104,6 +109,7 @@ __device__ __forceinline__ int group_max(int v) {
   if constexpr (G >= 8) v = max(v, (int)FSDKR_DPP(v, 0x141));  // row_half_mirror
   if constexpr (G >= 16) v = max(v, (int)FSDKR_DPP(v, 0x140)); // row_mirror
   if constexpr (G >= 32) v = max(v, __shfl_xor(v, 16));
+  if constexpr (G >= 64) v = max(v, __shfl_xor(v, 32));
   return v;
 }
 
@@ -127,17 +133,26 @@ __device__ __forceinline__ void opaque(uint32_t* v) {
   for (int j = N - N % 4; j < N; ++j) asm volatile("" : "+v"(v[j]));
 }
 
-template <int KD, int G>
+// KR: digits of the modulus class (rows of a product, R = 2^(29 KR)); KD >= KR
+// register slots over the G lanes.  KD > KR only for G = 64 (one instance per
+// wave), whose top lanes hold zero digits.
+template <int KD, int G, int KR = KD>
 struct Mont29 {
   static constexpr int L = KD / G;
   static_assert(KD % G == 0, "KD must split evenly over the group");
-  // normalisation points inside one L-row cycle: at most 18 rows apart (bound: 31)
-  static constexpr int NSTEP = L <= 18 ? L : (L + 1) / 2 <= 18 ? (L + 1) / 2 : (L + 2) / 3;
+  static_assert(KR == KD || (G == 64 && KR % L == 0 && KR < KD), "spare slots only in the wave shape");
   // A column spends exactly L rows in a lane and leaves it as a 29-bit digit
-  // (row(): the retired column's carry stays behind), gaining < 2^59.01 per row:
-  // for L <= 24 it cannot reach 2^64 before it moves on, so only the final carry
-  // passes of mul() are needed.  Longer lanes normalise every NSTEP rows.
+  // (row(): the retired column's carry stays behind), gaining < 2^59.01 per row
+  // (< 2^59.6 in squaring rows): for L <= 24 it cannot reach 2^64 before it
+  // moves on, so only the final carry passes of mul() are needed.
   static constexpr bool NORM_IN_CYCLE = L > 24;
+  // Longer lanes fold the column at logical position P_k into P_k + 1 once per
+  // row (rolling normalisation, roll_norm), so every column is folded once per
+  // fold point during its L-row stay and accumulates at most 18 rows between
+  // folds (bound: 21 squaring rows).  That is NROLL column folds per row
+  // instead of a full L-column carry pass every 18 rows (2L per 36 rows).
+  static constexpr int NROLL = NORM_IN_CYCLE ? (L + 17) / 18 - 1 : 0;
+  static constexpr int roll_pos(int k) { return (k + 1) * L / (NROLL + 1); }
   // Scheduling fence at the end of each row.  Long lanes (throughput shapes,
   // 3 waves/SIMD) need it to hold VGPRs down; short lanes (latency shapes, one
   // wave per SIMD) drop it so the next row's a*b products can fill the m-digit
@@ -150,6 +165,9 @@ struct Mont29 {
   uint32_t m_lane0;   // ~0 in group lane 0
   uint32_t m_first;   // ~0 unless lane 0   (masks dpp_prev)
   uint32_t m_top;     // ~0 unless top lane (masks dpp_next)
+  uint32_t eight;     // 8 in an SGPR (roll_fold)
+  uint32_t m29;       // M29 in a VGPR: DPP-combined v_and_b32 needs a VGPR operand
+  uint32_t m_top29;   // M29 unless top lane (the digit moving down, masked in one v_and_b32_dpp)
 
   __device__ __forceinline__ void init_lane(int g_) {
     g = g_;
@@ -159,6 +177,10 @@ struct Mont29 {
     // keep the masks as plain values so `x & mask` stays one full-rate v_and
     // (the optimiser otherwise rewrites it into v_cndmask on a lane predicate)
     asm volatile("" : "+v"(m_lane0), "+v"(m_first), "+v"(m_top));
+    eight = 8u;
+    m29 = M29;
+    m_top29 = m_top & M29;
+    asm volatile("" : "+s"(eight), "+v"(m29), "+v"(m_top29));
   }
 
   __device__ __forceinline__ uint64_t prev64(uint64_t v) const {
@@ -183,6 +205,24 @@ struct Mont29 {
     }
     acc[RHO % L] = (uint64_t)((uint32_t)acc[RHO % L] & M29) + cin;
     __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // Rolling normalisation at rotation R: the column at logical position P moves
+  // its high word into position P + 1 (same lane: P + 1 < L), one v_mad_u64_u32
+  // by 8 (2^32 = 8 * 2^29) and one move that clears the high word.  The folded
+  // column keeps < 2^32, the receiving one gains < 2^35; values are unchanged.
+  template <int R, int K>
+  __device__ __forceinline__ void roll_fold(uint64_t* acc) const {
+    constexpr int P = roll_pos(K);
+    static_assert(P >= 2 && P + 1 < L, "fold points stay inside the lane, clear of the retiring column");
+    constexpr int sp = (P + R) % L, sn = (P + 1 + R) % L;
+    const uint32_t hi = (uint32_t)(acc[sp] >> 32);
+    acc[sp] = (uint64_t)(uint32_t)acc[sp];
+    mac(acc[sn], hi, eight);   // a v_mad_u64_u32 by an opaque 8, not a 64-bit shift-add
+  }
+  template <int R, int... Ks>
+  __device__ __forceinline__ void roll_norm(uint64_t* acc, std::integer_sequence<int, Ks...>) const {
+    (roll_fold<R, Ks>(acc), ...);
   }
 
   // Squaring rows (SQ): of the pair products a_r a_p (p = g L + j) a row issues
@@ -237,36 +277,40 @@ struct Mont29 {
     const uint32_t a2 = SQ ? ai << 1 : 0u;
     if constexpr (ORDERED) {
       mac_ab<R, SQ, 0>(acc, b, ai, a2);
-      uint32_t m = ((uint32_t)acc[s0] * ninv) & M29;
+      uint32_t m = (uint32_t)acc[s0] * ninv;
       __builtin_amdgcn_sched_barrier(0);
       mac_ab_rest<R, SQ>(acc, b, ai, a2, std::make_integer_sequence<int, L - 1>{});
       __builtin_amdgcn_sched_barrier(0);
-      m = bcast_lane0<G>(m);
+      m = bcast_lane0<G>(m) & m29;   // one v_and_b32 with the DPP broadcast folded in
       mac(acc[s0], m, n[0]);
       uint64_t carry = acc[s0] >> 29;
-      uint32_t digit = (uint32_t)acc[s0] & M29;
+      uint32_t digit = (uint32_t)acc[s0];
       asm volatile("" : "+v"(digit), "+v"(carry));   // computed here, not sunk to their uses
       __builtin_amdgcn_sched_barrier(0);
       mac(acc[s1], m, n[1]);
       acc[s1] += carry;
 #pragma unroll
       for (int j = 2; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
+      roll_norm<R>(acc, std::make_integer_sequence<int, NROLL>{});
       __builtin_amdgcn_sched_barrier(0);
-      acc[s0] = (uint64_t)dpp_next_rot<G>(digit);   // lane 0's digit is 0: the top lane gets the 0 it needs
+      acc[s0] = (uint64_t)(dpp_next_rot<G>(digit) & m29);   // lane 0's digit is 0: the top lane gets the 0 it needs
     } else {
       mac_ab<R, SQ, 0>(acc, b, ai, a2);
       mac_ab_rest<R, SQ>(acc, b, ai, a2, std::make_integer_sequence<int, L - 1>{});
-      const uint32_t m = bcast_lane0<G>(((uint32_t)acc[s0] * ninv) & M29);
+      // G = 64: the instance is the wave, so m is computed on the scalar unit
+      // from lane 0's column (ninv is an SGPR there)
+      const uint32_t m = (G == 64) ? ((bcast_lane0<G>((uint32_t)acc[s0]) * ninv) & M29)
+                                   : (bcast_lane0<G>((uint32_t)acc[s0] * ninv) & m29);
 #pragma unroll
       for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
+      roll_norm<R>(acc, std::make_integer_sequence<int, NROLL>{});
       // every lane carries its lowest column into the next one (value-preserving;
       // in lane 0 that column is 0 mod 2^29 after m*n), so the digit that moves
       // down to lane g-1 fits 29 bits: one 32-bit DPP move
       acc[s1] += acc[s0] >> 29;
-      if constexpr (HAS_ROT<G>) acc[s0] = (uint64_t)dpp_next_rot<G>((uint32_t)acc[s0] & M29);
-      else acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0] & M29) & m_top);
+      if constexpr (HAS_ROT<G>) acc[s0] = (uint64_t)(dpp_next_rot<G>((uint32_t)acc[s0]) & m29);
+      else acc[s0] = (uint64_t)(dpp_next<G>((uint32_t)acc[s0]) & m_top29);
     }
-    if constexpr (NORM_IN_CYCLE && (((R + 1) % NSTEP == 0) || (R + 1 == L))) norm_step<(R + 1) % L>(acc);
     if constexpr (ROW_FENCE) __builtin_amdgcn_sched_barrier(0);
   }
 
@@ -299,6 +343,7 @@ struct Mont29 {
   template <bool SQ>
   __device__ __forceinline__ void product(uint32_t* out, uint32_t* b, const uint32_t* a_lds) {
     static_assert(!SQ || NORM_IN_CYCLE || L <= 21, "squaring rows: column bound");
+    static_assert(G != 64, "the wave shape streams from registers: product_w");
     uint64_t acc[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) acc[j] = 0;
@@ -310,6 +355,48 @@ struct Mont29 {
       opaque<L>(n);
       cycle<SQ>(acc, b, n, a_lds + cyc * L, cur, cyc + 1 < G ? (uint32_t)L : 0u, std::make_integer_sequence<int, L>{});
     }
+    finish(out, acc);
+  }
+
+  // G = 64 (one instance per wave): the streamed operand is held in registers
+  // like b (lane g: digits gL..gL+L-1) and each row's digit is read with
+  // v_readlane, so it is wave-uniform: the a*b MACs take it from an SGPR and
+  // the quotient digit is computed on the scalar unit (row()).  No LDS.  Only
+  // the first KR/L lanes' digits are streamed (R = 2^(29 KR)).  a may alias b.
+  __device__ __forceinline__ void mul_w(uint32_t* out, uint32_t* b, const uint32_t* a) { product_w<false>(out, b, a); }
+  __device__ __forceinline__ void sqr_w(uint32_t* out, uint32_t* b) { product_w<true>(out, b, b); }
+
+  template <int R, bool SQ>
+  __device__ __forceinline__ void row_w(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* a,
+                                        uint32_t& cur, int cyc) const {
+    const uint32_t ai = cur;   // next row's digit first: the readlane latency hides behind this row
+    cur = (R + 1 < L) ? (uint32_t)__builtin_amdgcn_readlane((int)a[R + 1], cyc)
+                      : (uint32_t)__builtin_amdgcn_readlane((int)a[0], cyc + 1);   // lane KR/L past the end: unused
+    row<R, SQ>(acc, b, n, ai);
+  }
+  template <bool SQ, int... Rs>
+  __device__ __forceinline__ void cycle_w(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* a,
+                                          uint32_t& cur, int cyc, std::integer_sequence<int, Rs...>) const {
+    (row_w<Rs, SQ>(acc, b, n, a, cur, cyc), ...);
+  }
+  template <bool SQ>
+  __device__ __forceinline__ void product_w(uint32_t* out, uint32_t* b, const uint32_t* a) {
+    static_assert(G == 64 && (!SQ || L <= 21), "wave shape");
+    uint64_t acc[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[j] = 0;
+    uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)a[0], 0);
+#pragma unroll 1
+    for (int cyc = 0; cyc < KR / L; ++cyc) {
+      opaque<L>(b);
+      opaque<L>(n);
+      cycle_w<SQ>(acc, b, n, a, cur, cyc, std::make_integer_sequence<int, L>{});
+    }
+    finish(out, acc);
+  }
+
+  // carries of a finished product: digits <= 2^29+127
+  __device__ __forceinline__ void finish(uint32_t* out, uint64_t* acc) const {
     // rotation is back to identity; two more carry steps give digits <= 2^29+127
     norm_step<0>(acc);
     const uint32_t cin = dpp_prev<G>((uint32_t)(acc[L - 1] >> 29)) & m_first;

@@ -48,9 +48,10 @@ typedef struct fsdkr_cfg {
 int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out);
 void fsdkr_ctx_destroy(fsdkr_ctx* ctx);
 const char* fsdkr_last_error(const fsdkr_ctx* ctx);
-/* Lanes cooperating on one modexp instance (2, 4, 8, 16, and 32 for the
- * 4096-bit generic modexp; unsupported values for a width fall back to the
- * automatic choice); 0 = choose by batch size. */
+/* Lanes cooperating on one modexp instance (2, 4, 8, 16, and 32 or 64 for the
+ * 4096-bit generic modexp, 64 being one instance per wavefront; unsupported
+ * values for a width fall back to the automatic choice); 0 = choose by batch
+ * size. */
 int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes);
 /* Switch per-kernel HIP-event timing (FSDKR_CFG_TIMING) on or off after
  * creation.  The events cost ~9 ms per n = 64 collect (eight streams, one

@@ -57,9 +57,11 @@ def test_modexp_paillier_shape(gpu_ctx):
     assert got == [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
 
 
-@pytest.mark.parametrize("limbs,group", [(64, 2), (64, 4), (64, 8), (128, 4), (128, 8), (128, 16), (192, 4), (192, 8)])
+@pytest.mark.parametrize("limbs,group", [(64, 2), (64, 4), (64, 8), (128, 4), (128, 8), (128, 16), (128, 32), (128, 64),
+                                         (192, 4), (192, 8)])
 def test_modexp_every_group_size(gpu_ctx, limbs, group):
-    """Each lanes-per-instance variant (mont29.hpp DPP paths for G = 2..16) is exact,
+    """Each lanes-per-instance variant (mont29.hpp DPP paths for G = 2..32; G = 64 the
+    one-instance-per-wave kernel with v_readlane rows) is exact,
     including the all-ones modulus and exponent-length spread in one launch."""
     rnd = random.Random(1000 * limbs + group)
     bits = 32 * limbs
