@@ -357,13 +357,15 @@ inline void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, ui
 // GA lanes per instance: GA shares the chip with the other streams, so it takes
 // the largest group that keeps it within about half the resident lanes
 // (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
-// (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants) for latency.
+// (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants), and at most one
+// wave per SIMD (1024 chains) one wave per chain (modexp_wave_kernel), for latency.
 // Used by the prestart and by launch().
 inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
   uint32_t g = 8;
   for (uint32_t x : {16u, kWideGroup})
     if ((uint64_t)count * x <= 65536u) g = x;
   if (g == kWideGroup && nn != 128) g = 16;
+  if (nn == 128 && count <= 1024) g = kWaveGroup;
   return g;
 }
 

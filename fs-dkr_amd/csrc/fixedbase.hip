@@ -79,6 +79,53 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   }
 }
 
+// The same chain with one base per wave64 (Mont29 wave shape, product_w): lane g
+// holds digits gL..gL+L-1, KR digits in the first KR/L lanes; the row digit and
+// the quotient are wave-uniform (v_readlane, scalar-unit quotient).  For launches
+// of at most one wave per SIMD, where the chain's latency is the critical path.
+template <int KR, int L, int K32>
+__global__ __launch_bounds__(64) void fb_table_wave_kernel(const FbTableArgs a) {
+  constexpr int KD = 64 * L;
+  using MT = Mont29<KD, 64, KR>;
+  constexpr int STRIDE = 3 * KR + 4;
+  const int g = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  if (b >= a.count) return;
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[b] * STRIDE;
+  const bool live = g * L < KR;
+  MT M;
+  M.init_lane(g);
+  uint32_t acc[L], r2[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    M.n[j] = live ? C[g * L + j] : 0u;
+    r2[j] = live ? C[2 * KR + g * L + j] : 0u;
+  }
+  M.ninv = (uint32_t)__builtin_amdgcn_readfirstlane((int)C[3 * KR]);
+  const uint32_t* B = reinterpret_cast<const uint32_t*>(a.base_ptr[b]);
+  const int blen = (int)min(a.base_len[b], (uint32_t)K32);
+#pragma unroll
+  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);   // 0 past the class's digits
+  uint32_t* T = a.table + (size_t)a.toff[b] * KR;
+  const uint32_t h = a.h[b];
+  const uint32_t n_steps = 1 + (h > 0 ? (h - 1) * a.w : 0);
+  uint32_t entry = 0;
+  for (uint32_t st = 0; st < n_steps; ++st) {
+    if (st == 0) M.mul_w(acc, acc, r2);   // Montgomery form of the base
+    else M.sqr_w(acc, acc);
+    if (st == 0 || (st % a.w) == 0) {
+      if (live) {
+#pragma unroll
+        for (int j = 0; j < L; ++j) T[(size_t)entry * KR + g * L + j] = acc[j];
+      }
+      ++entry;
+    }
+  }
+}
+
 // One thread per instance: the BGMW product schedule of its exponent, by a
 // counting sort of its w-bit digits (O(h + 2^w)): for d = max digit .. 1 the
 // windows j with e_j = d (ascending j), then one A-step.
@@ -216,12 +263,22 @@ static hipError_t exp_launch(const FbExpArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int KR, int L, int K32>
+static hipError_t table_launch_wave(const FbTableArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((fb_table_wave_kernel<KR, L, K32>), dim3(a.count), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+// Bases whose chains fit one wave per SIMD (n = 64: 192 chains) run one per wave;
+// more (many sessions) the 8- / 4-lane group shapes.
+constexpr uint32_t kFbWaveMax = 1024;
+
 hipError_t launch_fb_table(uint32_t k32, const FbTableArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
-  // few bases, long chains: the most lanes per instance the width allows
+  const bool wave = a.count <= kFbWaveMax;
   switch (k32) {
-    case 64: return table_launch<72, 8, 64>(a, st);
-    case 96: return table_launch<108, 4, 96>(a, st);
+    case 64: return wave ? table_launch_wave<72, 2, 64>(a, st) : table_launch<72, 8, 64>(a, st);
+    case 96: return wave ? table_launch_wave<108, 2, 96>(a, st) : table_launch<108, 4, 96>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

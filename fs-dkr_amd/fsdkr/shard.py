@@ -11,13 +11,15 @@ No other data crosses the interconnect.  collect() then maps the merged
 verdicts to the reference's first error on a header-only batch of the whole
 message set (threshold, sizes, party indices, ek.n) and applies collect()'s
 side effects and share recovery (refresh_message.rs:330-464) on every rank."""
+import os
+
 import numpy as np
 
 from .batch import CollectBatch, Verdicts
 
 
 # GA split of a small slice (measured: profiles/r02zd_ga_lanes_cus_ab.jsonl, r02zn_ga_split_size_ab.jsonl)
-GA_SPLIT_CUS = 160
+GA_SPLIT_CUS = int(os.environ.get("FSDKR_SHARD_GA_CUS", "160"))   # env: tuning runs only
 GA_SPLIT_MAX_CHAINS = 1024
 
 
