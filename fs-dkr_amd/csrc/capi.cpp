@@ -371,6 +371,7 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   fsdkr::free_collect_plan(c);
   fsdkr::free_ga_pre(c);
+  fsdkr::free_recover(c);
   delete c;
 }
 

@@ -41,8 +41,10 @@ int collect_launch_impl(Ctx* c) {
   }
   if ((rc = setup_moduli(c, nl, PI(pl.o_mods), pl.n_mods_nl, &cons_nl, "collect_nl"))) return rc;
   if ((rc = setup_moduli(c, pl.ckl, PI(pl.o_ckmods), Mt, &cons_ck, "collect_ck"))) return rc;
-  // J2 / J5 (256-bit challenge exponents): 8 lanes per instance
-  const uint32_t j2_group = 8, j5_group = 8;
+  // J2 / J5 (256-bit challenge exponents): 8 lanes per instance; a small 4096-bit
+  // J2 (a multi-GPU rank's slice) one instance per wave: its chain is on the
+  // critical path of the rank (J2 -> inverses -> equalities)
+  const uint32_t j2_group = (nn == 128 && pl.jcount[2] <= 1024) ? kWaveGroup : 8, j5_group = 8;
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;
   if (ga_group == kWideGroup && pl.jcount[0]) {

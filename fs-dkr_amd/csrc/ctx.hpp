@@ -38,6 +38,7 @@ struct Ctx {
   hipStream_t side[NSIDE] = {};   // concurrent streams for independent jobs (lazily created)
   void* plan = nullptr;           // prepared collect() batch (collect.cpp)
   void* ga_pre = nullptr;         // prestarted s^N mod N^2 job (fsdkr_collect_prestart)
+  void* recover = nullptr;        // launched share recovery (fsdkr_collect_recover_launch)
   // pinned host arena for the collect() image (grow-only; one H2D copy per prepare)
   uint8_t* pinned = nullptr;
   size_t pinned_bytes = 0;
@@ -154,6 +155,7 @@ inline uint8_t ped_verdict(const uint32_t* eq, uint32_t M, uint32_t panic_word) 
   return panic_word ? 2 : 1;
 }
 void free_collect_plan(Ctx* c);
+void free_recover(Ctx* c);
 void free_ga_pre(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
                       uint32_t group = 0);

@@ -4,8 +4,13 @@
 // exponentiation and EC work run on the GPU; the O(1) L-function / mu
 // arithmetic of kzen-paillier decrypt runs on the host.
 #include <hip/hip_runtime.h>
+#include <openssl/bn.h>
+#include <openssl/crypto.h>
+#include <openssl/ec.h>
+#include <openssl/obj_mac.h>
 
 #include <algorithm>
+#include <string>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -279,9 +284,408 @@ hbn::Limbs lagrange(const uint32_t* x, uint32_t cnt, uint32_t j, const hbn::Limb
   if (!hbn::modinv(den, Q, &inv)) return hbn::Limbs{};   // unreachable for indices < q
   return hbn::mulmod(num, inv, Q);
 }
+
+// secp256k1 group of the host-side y = G * share (OpenSSL; one scalar
+// multiplication per job, off the GPU's latency-bound MSM path)
+const EC_GROUP* secp_group() {
+  static const EC_GROUP* g = EC_GROUP_new_by_curve_name(NID_secp256k1);
+  return g;
+}
+
+// out16 = G * k (affine x | y as 8 little-endian u32 limbs each; (0, 0) = infinity)
+bool g_mul(const hbn::Limbs& k, uint32_t* out16) {
+  std::memset(out16, 0, 64);
+  uint8_t kb[32] = {0};
+  for (size_t i = 0; i < k.size() && i < 8; ++i)
+    for (int b = 0; b < 4; ++b) kb[4 * i + b] = (uint8_t)(k[i] >> (8 * b));
+  BN_CTX* bc = BN_CTX_new();
+  BIGNUM* bk = BN_lebin2bn(kb, 32, nullptr);
+  BIGNUM *x = BN_new(), *y = BN_new();
+  EC_POINT* R = EC_POINT_new(secp_group());
+  bool ok = bc && bk && x && y && R;
+  if (ok) BN_set_flags(bk, BN_FLG_CONSTTIME);
+  ok = ok && EC_POINT_mul(secp_group(), R, bk, nullptr, nullptr, bc) == 1;
+  if (ok && !EC_POINT_is_at_infinity(secp_group(), R)) {
+    ok = EC_POINT_get_affine_coordinates(secp_group(), R, x, y, bc) == 1;
+    uint8_t xb[32], yb[32];
+    ok = ok && BN_bn2lebinpad(x, xb, 32) == 32 && BN_bn2lebinpad(y, yb, 32) == 32;
+    if (ok) {
+      std::memcpy(out16, xb, 32);
+      std::memcpy(out16 + 8, yb, 32);
+    }
+  }
+  EC_POINT_free(R);
+  BN_free(x);
+  BN_free(y);
+  BN_clear_free(bk);
+  BN_CTX_free(bc);
+  OPENSSL_cleanse(kb, sizeof kb);
+  return ok;
+}
+
+// a^-1 mod m for a secret odd m (OpenSSL, constant-time flag); false if not a unit
+bool inv_secret(const hbn::Limbs& a, const hbn::Limbs& m, hbn::Limbs* out) {
+  auto to_bn = [](const hbn::Limbs& v) {
+    std::vector<uint8_t> b(4 * std::max<size_t>(v.size(), 1), 0);
+    for (size_t i = 0; i < v.size(); ++i)
+      for (int k = 0; k < 4; ++k) b[4 * i + k] = (uint8_t)(v[i] >> (8 * k));
+    BIGNUM* r = BN_lebin2bn(b.data(), (int)b.size(), nullptr);
+    OPENSSL_cleanse(b.data(), b.size());
+    return r;
+  };
+  BN_CTX* bc = BN_CTX_new();
+  BIGNUM *ba = to_bn(a), *bm = to_bn(m), *br = BN_new();
+  bool ok = bc && ba && bm && br;
+  if (ok) {
+    BN_set_flags(ba, BN_FLG_CONSTTIME);
+    BN_set_flags(bm, BN_FLG_CONSTTIME);
+    ok = BN_mod_inverse(br, ba, bm, bc) != nullptr;
+  }
+  if (ok) {
+    const int nb = BN_num_bytes(br);
+    std::vector<uint8_t> b((size_t)std::max(nb, 1) + 3, 0);
+    BN_bn2lebinpad(br, b.data(), (int)b.size());
+    hbn::Limbs r((b.size() + 3) / 4, 0u);
+    for (size_t i = 0; i < b.size(); ++i) r[i / 4] |= (uint32_t)b[i] << (8 * (i % 4));
+    hbn::trim(r);
+    *out = r;
+    OPENSSL_cleanse(b.data(), b.size());
+  }
+  BN_clear_free(ba);
+  BN_clear_free(bm);
+  BN_clear_free(br);
+  BN_CTX_free(bc);
+  return ok;
+}
+
+// grow-only pinned host buffer (the async D2H targets of a launched recovery)
+struct Pinned {
+  void* p = nullptr;
+  size_t bytes = 0;
+  uint32_t* get(size_t want) {
+    if (want > bytes) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      bytes = 0;
+      if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+      bytes = want;
+    }
+    return reinterpret_cast<uint32_t*>(p);
+  }
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+};
 }  // namespace
 
+namespace fsdkr {
+
+// A launched share recovery (fsdkr_collect_recover_launch): the GPU work (CRT
+// decryption exponentiations, the pk_vec MSM) is enqueued on the recovery
+// stream; finish() waits for it and does the O(1) host arithmetic.  Every input
+// is copied at launch, so the caller's arrays may go away in between.
+struct RecoverPending {
+  struct Job {
+    uint32_t nl = 0, T = 0, t_key = 0, t_vss = 0, n_new = 0, tp = 0;
+    std::vector<hbn::Limbs> li;
+    hbn::Limbs P, Q, qinv, pinv;
+    bool dec_ok = false;
+    uint32_t width = 0;      // decryption batch (index into widths)
+    size_t dec_at = 0;       // its first decryption in that batch
+    size_t row = ~(size_t)0; // its first pk_vec row of the MSM
+  };
+  struct Width {
+    uint32_t nl = 0, total = 0, keys = 0, exp_bits = 0;
+    std::vector<uint32_t> base, ex, idx, mods;
+    std::vector<uint8_t> desc;
+    Pinned out;
+  };
+  std::vector<Job> jobs;
+  std::vector<Width> widths;
+  uint32_t rows = 0, terms = 1;
+  std::vector<uint32_t> pts, scs;
+  std::vector<uint64_t> ptrs;
+  Pinned msm_out;
+  hipEvent_t done = nullptr;
+  bool in_flight = false;
+
+  ~RecoverPending() {
+    if (done) (void)hipEventDestroy(done);
+  }
+  int launch(Ctx* c, const fsdkr_recover_job* in, uint32_t count);
+  int finish(Ctx* c, fsdkr_recovered* out);
+};
+
+RecoverPending* recover_state(Ctx* c) {
+  if (!c->recover) c->recover = new RecoverPending();
+  return reinterpret_cast<RecoverPending*>(c->recover);
+}
+
+void free_recover(Ctx* c) {
+  delete reinterpret_cast<RecoverPending*>(c->recover);
+  c->recover = nullptr;
+}
+
+int RecoverPending::launch(Ctx* c, const fsdkr_recover_job* in, uint32_t count) {
+  const hbn::Limbs Qs = hbn::from(SECP_Q, 8);
+  jobs.assign(count, Job{});
+  widths.clear();
+  rows = 0;
+  terms = 1;
+  pts.clear();
+  scs.clear();
+  // per job: Lagrange weights, the key's CRT constants (a degenerate key panics in
+  // Paillier::decrypt: p or q even or 1, p == q, p^2 / q^2 / N wider than the class)
+  parallel_for_host(count, 1, [&](size_t b0, size_t b1) {
+    for (size_t j = b0; j < b1; ++j) {
+      const fsdkr_recover_job& J = in[j];
+      Job& X = jobs[j];
+      X.nl = J.nl;
+      X.T = J.t_vss + 1;
+      X.t_key = J.t_key;
+      X.t_vss = J.t_vss;
+      X.n_new = J.n_new;
+      X.tp = std::min(J.t_key, J.t_vss) + 1;
+      X.li.resize(X.T);
+      for (uint32_t k = 0; k < X.T; ++k) X.li[k] = lagrange(J.old_index, X.T, k, Qs);
+      X.P = hbn::from(J.p, J.nl);
+      X.Q = hbn::from(J.q, J.nl);
+      const hbn::Limbs PP = hbn::mul(X.P, X.P), QQ = hbn::mul(X.Q, X.Q), N = hbn::mul(X.P, X.Q);
+      X.dec_ok = !hbn::is_even(X.P) && !hbn::is_even(X.Q) && hbn::bitlen(PP) <= 32 * J.nl &&
+                 hbn::bitlen(QQ) <= 32 * J.nl && hbn::bitlen(N) <= 32 * J.nl && !hbn::is_one(X.P) &&
+                 !hbn::is_one(X.Q) && inv_secret(hbn::mod(X.Q, X.P), X.P, &X.qinv) &&
+                 inv_secret(hbn::mod(X.P, X.Q), X.Q, &X.pinv);
+    }
+  });
+  // decryption batches, one per key width: (c mod p^2)^(p-1), (c mod q^2)^(q-1)
+  for (uint32_t nl : {64u, 96u, 128u, 192u}) {
+    Width W;
+    W.nl = nl;
+    std::vector<uint32_t> owners;
+    for (uint32_t j = 0; j < count; ++j)
+      if (jobs[j].nl == nl && jobs[j].dec_ok) {
+        jobs[j].width = (uint32_t)widths.size();
+        jobs[j].dec_at = W.total;
+        W.total += jobs[j].T;
+        owners.push_back(j);
+      }
+    if (!W.total) continue;
+    W.keys = (uint32_t)owners.size();
+    W.base.assign((size_t)2 * W.total * nl, 0u);
+    W.ex.assign((size_t)2 * W.total * nl, 0u);
+    W.idx.resize(2 * (size_t)W.total);
+    W.mods.assign((size_t)2 * W.keys * nl, 0u);
+    parallel_for_host(owners.size(), 1, [&](size_t b0, size_t b1) {
+      for (size_t o = b0; o < b1; ++o) {
+        const uint32_t j = owners[o];
+        const Job& X = jobs[j];
+        const hbn::Limbs PP = hbn::mul(X.P, X.P), QQ = hbn::mul(X.Q, X.Q);
+        const hbn::Limbs pm1 = hbn::sub(X.P, hbn::Limbs{1}), qm1 = hbn::sub(X.Q, hbn::Limbs{1});
+        hbn::store(PP, W.mods.data() + (2 * o) * nl, nl);
+        hbn::store(QQ, W.mods.data() + (2 * o + 1) * nl, nl);
+        for (uint32_t k = 0; k < X.T; ++k) {
+          const size_t i = X.dec_at + k;
+          const hbn::Limbs ck = hbn::from(in[j].cts + (size_t)k * 2 * nl, 2 * nl);
+          hbn::store(hbn::mod(ck, PP), W.base.data() + (2 * i) * nl, nl);
+          hbn::store(hbn::mod(ck, QQ), W.base.data() + (2 * i + 1) * nl, nl);
+          hbn::store(pm1, W.ex.data() + (2 * i) * nl, nl);
+          hbn::store(qm1, W.ex.data() + (2 * i + 1) * nl, nl);
+          W.idx[2 * i] = (uint32_t)(2 * o);
+          W.idx[2 * i + 1] = (uint32_t)(2 * o + 1);
+        }
+      }
+    });
+    for (uint32_t j : owners) W.exp_bits = std::max({W.exp_bits, hbn::bitlen(jobs[j].P), hbn::bitlen(jobs[j].Q)});
+    widths.push_back(std::move(W));
+  }
+  // pk_vec rows: new party i's sum over k < tp of li[k] * points_committed_vec[i] of message k
+  for (uint32_t j = 0; j < count; ++j)
+    if (jobs[j].dec_ok && jobs[j].n_new) terms = std::max(terms, jobs[j].tp);
+  for (uint32_t j = 0; j < count; ++j) {
+    Job& X = jobs[j];
+    if (!X.dec_ok || !X.n_new) continue;
+    X.row = rows;
+    for (uint32_t i = 0; i < X.n_new; ++i)
+      for (uint32_t k = 0; k < terms; ++k) {
+        const size_t at = pts.size();
+        pts.resize(at + 16, 0u);
+        scs.resize(scs.size() + 8, 0u);
+        if (k < X.tp) {
+          std::memcpy(pts.data() + at, in[j].points + ((size_t)i * X.tp + k) * 16, 64);
+          hbn::store(X.li[k], scs.data() + scs.size() - 8, 8);
+        }
+      }
+    rows += X.n_new;
+  }
+  // enqueue: recovery stream, issue priority 3 (few waves beside a launched pipeline)
+  StreamScope scope(c, c->aux_stream());
+  PrioScope prio(c, 3);
+  int rc;
+  for (Width& W : widths) {
+    const uint32_t nl = W.nl, n = 2 * W.total, nm = 2 * W.keys;
+    const std::string tag = "rc" + std::to_string(nl);
+    const size_t nb = (size_t)n * nl * 4;
+    uint8_t* d = (uint8_t*)c->buf((tag + "_io").c_str(), 3 * nb + (size_t)nm * nl * 4 + 1024);
+    uint32_t* h_out = W.out.get(nb);
+    if (!d || !h_out) {
+      c->fail("fsdkr_collect_recover: allocation failed");
+      return FSDKR_E_OOM;
+    }
+    uint32_t *d_base = (uint32_t*)d, *d_ex = d_base + (size_t)n * nl, *d_out = d_ex + (size_t)n * nl;
+    uint32_t* d_mods = d_out + (size_t)n * nl;
+    if ((rc = c->hip_check(hipMemcpyAsync(d_base, W.base.data(), nb, hipMemcpyHostToDevice, c->stream), "H2D rc")) ||
+        (rc = c->hip_check(hipMemcpyAsync(d_ex, W.ex.data(), nb, hipMemcpyHostToDevice, c->stream), "H2D rc")) ||
+        (rc = c->hip_check(hipMemcpyAsync(d_mods, W.mods.data(), (size_t)nm * nl * 4, hipMemcpyHostToDevice, c->stream),
+                           "H2D rc")))
+      return rc;
+    uint32_t* consts = nullptr;
+    if ((rc = setup_moduli(c, nl, d_mods, nm, &consts, tag.c_str()))) return rc;
+    ModexpJob job;
+    job.k32 = nl;
+    for (uint32_t i = 0; i < n; ++i)
+      job.add((uint64_t)(uintptr_t)(d_base + (size_t)i * nl), nl, (uint64_t)(uintptr_t)(d_ex + (size_t)i * nl), nl,
+              W.exp_bits, W.idx[i]);
+    W.desc.clear();
+    job.pack(W.desc);
+    uint8_t* d_desc = (uint8_t*)c->buf((tag + "_desc").c_str(), W.desc.size());
+    if (!d_desc) return FSDKR_E_OOM;
+    if ((rc = c->hip_check(hipMemcpyAsync(d_desc, W.desc.data(), W.desc.size(), hipMemcpyHostToDevice, c->stream),
+                           "H2D rc desc")))
+      return rc;
+    {
+      CtScope ct(c);   // secret exponents p - 1, q - 1: regular-access modexp
+      if ((rc = launch_modexp_desc(c, nl, n, W.exp_bits, d_desc, consts, d_out, c->stream, (tag + "_tab").c_str(),
+                                   c->prio, 0)))
+        return rc;
+    }
+    if ((rc = c->hip_check(hipMemcpyAsync(h_out, d_out, nb, hipMemcpyDeviceToHost, c->stream), "D2H rc"))) return rc;
+  }
+  if (rows) {
+    const size_t np = (size_t)rows * terms;
+    uint8_t* d = (uint8_t*)c->buf("rc_msm", np * 16 * 4 + np * 8 * 4 + np * 8 + (size_t)rows * 16 * 4 + np * 96 + 1024);
+    uint32_t* h_out = msm_out.get((size_t)rows * 64);
+    if (!d || !h_out) return FSDKR_E_OOM;
+    uint32_t* d_pts = (uint32_t*)d;
+    uint32_t* d_sc = d_pts + np * 16;
+    uint64_t* d_ptr = (uint64_t*)(d_sc + np * 8);
+    uint32_t* d_o = (uint32_t*)(d_ptr + np);
+    uint32_t* d_scr = d_o + (size_t)rows * 16;
+    ptrs.resize(np);
+    for (size_t k = 0; k < np; ++k) ptrs[k] = (uint64_t)(uintptr_t)(d_pts + k * 16);
+    if ((rc = c->hip_check(hipMemcpyAsync(d_pts, pts.data(), np * 64, hipMemcpyHostToDevice, c->stream), "H2D pts")) ||
+        (rc = c->hip_check(hipMemcpyAsync(d_sc, scs.data(), np * 32, hipMemcpyHostToDevice, c->stream), "H2D sc")) ||
+        (rc = c->hip_check(hipMemcpyAsync(d_ptr, ptrs.data(), np * 8, hipMemcpyHostToDevice, c->stream), "H2D ptr")))
+      return rc;
+    EcMsmArgs a{d_ptr, d_sc, terms, d_o, rows, d_scr, c->prio};
+    c->mark("ec", true);
+    rc = c->hip_check(launch_ec_msm(a, c->stream), "ec_msm");
+    c->mark("ec", false);
+    if (rc) return rc;
+    if ((rc = c->hip_check(hipMemcpyAsync(h_out, d_o, (size_t)rows * 64, hipMemcpyDeviceToHost, c->stream), "D2H msm")))
+      return rc;
+  }
+  if (!done && (rc = c->hip_check(hipEventCreateWithFlags(&done, hipEventDisableTiming), "event"))) return rc;
+  if ((rc = c->hip_check(hipEventRecord(done, c->stream), "event record"))) return rc;
+  in_flight = true;
+  return FSDKR_OK;
+}
+
+int RecoverPending::finish(Ctx* c, fsdkr_recovered* out) {
+  in_flight = false;
+  int rc = c->hip_check(hipEventSynchronize(done), "recovery wait");
+  if (rc) return rc;
+  const hbn::Limbs Qs = hbn::from(SECP_Q, 8), one{1};
+  bool ec_ok = true;
+  parallel_for_host(jobs.size(), 1, [&](size_t b0, size_t b1) {
+    for (size_t j = b0; j < b1; ++j) {
+      const Job& X = jobs[j];
+      fsdkr_recovered& O = out[j];
+      std::memset(O.share, 0, sizeof O.share);
+      std::memset(O.y, 0, sizeof O.y);
+      if (!X.dec_ok) {
+        O.status = FSDKR_RECOVER_PANIC_DECRYPT;
+        continue;
+      }
+      const uint32_t nl = X.nl;
+      const uint32_t* h = reinterpret_cast<const uint32_t*>(widths[X.width].out.p);
+      // kzen-paillier CRT decryption with g = N + 1: h_p = L_p(g^(p-1) mod p^2)^-1 = p - q^-1 mod p
+      const hbn::Limbs hp = hbn::sub(X.P, X.qinv), hq = hbn::sub(X.Q, X.pinv);
+      const hbn::Limbs N = hbn::mul(X.P, X.Q);
+      hbn::Limbs acc;
+      for (uint32_t k = 0; k < X.T; ++k) {
+        const size_t i = X.dec_at + k;
+        const hbn::Limbs up = hbn::from(h + (2 * i) * nl, nl), uq = hbn::from(h + (2 * i + 1) * nl, nl);
+        const hbn::Limbs mp = hbn::mulmod(hbn::div_exact(hbn::sub(up.empty() ? one : up, one), X.P), hp, X.P);
+        const hbn::Limbs mq = hbn::mulmod(hbn::div_exact(hbn::sub(uq.empty() ? one : uq, one), X.Q), hq, X.Q);
+        // m = mq + q * ((mp - mq) q^-1 mod p)
+        const hbn::Limbs mqp = hbn::mod(mq, X.P);
+        const hbn::Limbs d = hbn::cmp(mp, mqp) >= 0 ? hbn::sub(mp, mqp) : hbn::sub(hbn::add(mp, X.P), mqp);
+        const hbn::Limbs m = hbn::add(mq, hbn::mul(X.Q, hbn::mulmod(d, X.qinv, X.P)));
+        acc = hbn::add(acc, hbn::mul(X.li[k], m));
+      }
+      // new share = (sum_k l_k m_k mod N) mod q (one decryption of the summed ciphertext)
+      const hbn::Limbs share = hbn::mod(hbn::mod(acc, N), Qs);
+      hbn::store(share, O.share, 8);
+      if (!g_mul(share, O.y)) ec_ok = false;
+      if (X.n_new) {
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(msm_out.p) + X.row * 16;
+        std::memcpy(O.pk_vec, r, (size_t)X.n_new * 64);
+      }
+      O.status = X.t_key > X.t_vss ? FSDKR_RECOVER_PANIC_LI : FSDKR_RECOVER_OK;
+    }
+  });
+  if (!ec_ok) {
+    c->fail("fsdkr_collect_recover: OpenSSL secp256k1 scalar multiplication failed");
+    return FSDKR_E_ARG;
+  }
+  return FSDKR_OK;
+}
+
+}  // namespace fsdkr
+
 extern "C" {
+
+int fsdkr_collect_recover_launch(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count && !jobs) {
+    c->fail("fsdkr_collect_recover: null jobs");
+    return FSDKR_E_ARG;
+  }
+  for (uint32_t j = 0; j < count; ++j) {
+    const fsdkr_recover_job& J = jobs[j];
+    if (!shape_digits(J.nl) || !J.old_index || !J.cts || !J.p || !J.q || (J.n_new && !J.points)) {
+      c->fail("fsdkr_collect_recover: job %u: bad shape or null array (nl=%u)", j, J.nl);
+      return FSDKR_E_ARG;
+    }
+  }
+  RecoverPending* R = recover_state(c);
+  if (R->in_flight) {
+    c->fail("fsdkr_collect_recover_launch: a recovery is in flight (call fsdkr_collect_recover_finish)");
+    return FSDKR_E_ARG;
+  }
+  return R->launch(c, jobs, count);
+}
+
+int fsdkr_collect_recover_finish(fsdkr_ctx* ctx, fsdkr_recovered* out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  RecoverPending* R = reinterpret_cast<RecoverPending*>(c->recover);
+  if (!R || !R->in_flight) {
+    c->fail("fsdkr_collect_recover_finish: no recovery launched");
+    return FSDKR_E_ARG;
+  }
+  if (!out && !R->jobs.empty()) {
+    c->fail("fsdkr_collect_recover_finish: null out");
+    return FSDKR_E_ARG;
+  }
+  for (size_t j = 0; j < R->jobs.size(); ++j)
+    if (R->jobs[j].n_new && !out[j].pk_vec) {
+      c->fail("fsdkr_collect_recover_finish: job %zu: null pk_vec", j);
+      return FSDKR_E_ARG;
+    }
+  return R->finish(c, out);
+}
 
 int fsdkr_collect_recover(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count, fsdkr_recovered* out) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
@@ -291,108 +695,8 @@ int fsdkr_collect_recover(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_
     c->fail("fsdkr_collect_recover: null jobs / out");
     return FSDKR_E_ARG;
   }
-  for (uint32_t j = 0; j < count; ++j) {
-    const fsdkr_recover_job& J = jobs[j];
-    if (!shape_digits(J.nl) || !J.old_index || !J.cts || !J.p || !J.q || (J.n_new && (!J.points || !out[j].pk_vec))) {
-      c->fail("fsdkr_collect_recover: job %u: bad shape or null array (nl=%u)", j, J.nl);
-      return FSDKR_E_ARG;
-    }
-  }
-  const hbn::Limbs Q = hbn::from(SECP_Q, 8);
-  // Lagrange weights (host; t_vss+1 small integers per job)
-  std::vector<std::vector<hbn::Limbs>> li(count);
-  for (uint32_t j = 0; j < count; ++j) {
-    const uint32_t T = jobs[j].t_vss + 1;
-    li[j].resize(T);
-    for (uint32_t k = 0; k < T; ++k) li[j][k] = lagrange(jobs[j].old_index, T, k, Q);
-    out[j].status = FSDKR_RECOVER_OK;
-  }
-  // decryptions: one batched call per key width; a width whose batch the
-  // decryption refuses (a degenerate key) is retried job by job
-  std::vector<std::vector<uint32_t>> plain(count);
-  for (uint32_t nl : {64u, 96u, 128u, 192u}) {
-    std::vector<uint32_t> cts, kidx, ps, qs, owners;
-    for (uint32_t j = 0; j < count; ++j) {
-      const fsdkr_recover_job& J = jobs[j];
-      if (J.nl != nl) continue;
-      const uint32_t T = J.t_vss + 1;
-      cts.insert(cts.end(), J.cts, J.cts + (size_t)T * 2 * nl);
-      for (uint32_t k = 0; k < T; ++k) kidx.push_back((uint32_t)owners.size());
-      ps.insert(ps.end(), J.p, J.p + nl);
-      qs.insert(qs.end(), J.q, J.q + nl);
-      owners.push_back(j);
-    }
-    if (owners.empty()) continue;
-    const uint32_t total = (uint32_t)kidx.size();
-    std::vector<uint32_t> m((size_t)total * nl);
-    int rc = fsdkr_paillier_decrypt_multi(ctx, nl, total, cts.data(), kidx.data(), ps.data(), qs.data(),
-                                          (uint32_t)owners.size(), m.data());
-    if (rc == FSDKR_OK) {
-      size_t at = 0;
-      for (uint32_t j : owners) {
-        const size_t T = jobs[j].t_vss + 1;
-        plain[j].assign(m.begin() + at * nl, m.begin() + (at + T) * nl);
-        at += T;
-      }
-      continue;
-    }
-    if (rc != FSDKR_E_ARG) return rc;
-    for (uint32_t j : owners) {
-      const fsdkr_recover_job& J = jobs[j];
-      const uint32_t T = J.t_vss + 1;
-      plain[j].resize((size_t)T * nl);
-      if (fsdkr_paillier_decrypt(ctx, nl, T, J.cts, J.p, J.q, plain[j].data()) != FSDKR_OK) {
-        out[j].status = FSDKR_RECOVER_PANIC_DECRYPT;
-        plain[j].clear();
-      }
-    }
-  }
-  // new share = (sum_k l_k m_k mod N) mod q, then one MSM launch for every y and pk_vec row
-  uint32_t terms = 1;
-  for (uint32_t j = 0; j < count; ++j)
-    terms = std::max(terms, std::min(jobs[j].t_key, jobs[j].t_vss) + 1);
-  std::vector<uint32_t> pts, scs;
-  std::vector<uint32_t> row_of(count, ~0u);
-  auto add_row = [&](const uint32_t* p16, size_t n_pts, const std::vector<hbn::Limbs>& sc) {
-    for (size_t k = 0; k < terms; ++k) {
-      const size_t at = pts.size();
-      pts.resize(at + 16, 0u);
-      scs.resize(scs.size() + 8, 0u);
-      if (k < n_pts) {
-        memcpy(pts.data() + at, p16 + k * 16, 64);
-        hbn::store(sc[k], scs.data() + scs.size() - 8, 8);
-      }
-    }
-  };
-  uint32_t rows = 0;
-  for (uint32_t j = 0; j < count; ++j) {
-    const fsdkr_recover_job& J = jobs[j];
-    if (out[j].status == FSDKR_RECOVER_PANIC_DECRYPT) continue;
-    const uint32_t T = J.t_vss + 1, nl = J.nl;
-    const hbn::Limbs N = hbn::mul(hbn::from(J.p, nl), hbn::from(J.q, nl));
-    hbn::Limbs acc;
-    for (uint32_t k = 0; k < T; ++k) acc = hbn::add(acc, hbn::mul(li[j][k], hbn::from(plain[j].data() + (size_t)k * nl, nl)));
-    const hbn::Limbs share = hbn::mod(hbn::mod(acc, N), Q);
-    memset(out[j].share, 0, sizeof out[j].share);
-    hbn::store(share, out[j].share, 8);
-    row_of[j] = rows;
-    add_row(SECP_G, 1, std::vector<hbn::Limbs>{share});
-    const uint32_t tp = std::min(J.t_key, J.t_vss) + 1;
-    for (uint32_t i = 0; i < J.n_new; ++i) add_row(J.points + (size_t)i * tp * 16, tp, li[j]);
-    rows += 1 + J.n_new;
-    if (J.t_key > J.t_vss) out[j].status = FSDKR_RECOVER_PANIC_LI;
-  }
-  if (!rows) return FSDKR_OK;
-  std::vector<uint32_t> res((size_t)rows * 16);
-  int rc = fsdkr_ec_msm(ctx, rows, terms, pts.data(), scs.data(), res.data());
-  if (rc) return rc;
-  for (uint32_t j = 0; j < count; ++j) {
-    if (row_of[j] == ~0u) continue;
-    const uint32_t* r = res.data() + (size_t)row_of[j] * 16;
-    memcpy(out[j].y, r, 64);
-    if (jobs[j].n_new) memcpy(out[j].pk_vec, r + 16, (size_t)jobs[j].n_new * 64);
-  }
-  return FSDKR_OK;
+  int rc = fsdkr_collect_recover_launch(ctx, jobs, count);
+  return rc ? rc : fsdkr_collect_recover_finish(ctx, out);
 }
 
 }  // extern "C"

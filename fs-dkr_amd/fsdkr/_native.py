@@ -90,6 +90,10 @@ def lib():
     L.fsdkr_collect_recover.argtypes = [vp, ctypes.POINTER(RecoverJobC), ctypes.c_uint32,
                                         ctypes.POINTER(RecoveredC)]
     L.fsdkr_collect_recover.restype = ctypes.c_int
+    L.fsdkr_collect_recover_launch.argtypes = [vp, ctypes.POINTER(RecoverJobC), ctypes.c_uint32]
+    L.fsdkr_collect_recover_launch.restype = ctypes.c_int
+    L.fsdkr_collect_recover_finish.argtypes = [vp, ctypes.POINTER(RecoveredC)]
+    L.fsdkr_collect_recover_finish.restype = ctypes.c_int
     L.fsdkr_sample_primes.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                       DRAW_BITS_FN, vp, u32p, ctypes.c_uint32]
     L.fsdkr_sample_primes.restype = ctypes.c_int
@@ -455,9 +459,13 @@ class Context:
         points[i] = the first min(t_key, t_vss)+1 committed points for new party i.
         Returns per job (status, share, y, pk_vec); a ciphertext wider than N^2
         raises ValueError (ints_to_limbs)."""
+        return self.collect_recover_finish(self.collect_recover_launch(jobs))
+
+    def collect_recover_launch(self, jobs):
+        """fsdkr_collect_recover_launch: the recovery's GPU work is enqueued and
+        runs while the caller goes on; returns the handle collect_recover_finish takes."""
         from . import _pack
         keep, cj = [], (RecoverJobC * len(jobs))()
-        outs = (RecoveredC * len(jobs))()
         for k, j in enumerate(jobs):
             nl, T = j["nl"], len(j["cts"])
             tp = min(j["t_key"], j["t_vss"]) + 1
@@ -468,22 +476,31 @@ class Context:
             Pt = np.zeros((max(1, n_new * tp), 16), dtype=np.uint32)
             if n_new:
                 _pack.points([pt for row in j["points"] for pt in row], None, Pt)
-            PK = np.zeros((max(1, n_new), 16), dtype=np.uint32)
-            keep.append((idx, C, Pp, Qq, Pt, PK))
+            keep.append((idx, C, Pp, Qq, Pt))
             cj[k] = RecoverJobC(nl, j["t_vss"], j["t_key"], n_new, _ptr(idx), _ptr(C), _ptr(Pp), _ptr(Qq), _ptr(Pt))
-            outs[k].pk_vec = _ptr(PK)
             assert T == j["t_vss"] + 1
-        self.check(self._lib.fsdkr_collect_recover(self._h, cj, len(jobs), outs))
+        self.check(self._lib.fsdkr_collect_recover_launch(self._h, cj, len(jobs)))
+        return [len(j["points"]) for j in jobs]
+
+    def collect_recover_finish(self, handle):
+        n_new = handle
+        outs = (RecoveredC * len(n_new))()
+        pks = []
+        for k, n in enumerate(n_new):
+            PK = np.zeros((max(1, n), 16), dtype=np.uint32)
+            pks.append(PK)
+            outs[k].pk_vec = _ptr(PK)
+        self.check(self._lib.fsdkr_collect_recover_finish(self._h, outs))
 
         def point(v):
             x, y = v & ((1 << 256) - 1), v >> 256
             return None if (x == 0 and y == 0) else (x, y)
         res = []
-        for k, j in enumerate(jobs):
+        for k, n in enumerate(n_new):
             o = outs[k]
             share = int.from_bytes(bytes(o.share), "little")
             y = point(int.from_bytes(bytes(o.y), "little"))
-            pk = [point(v) for v in limbs_to_ints(keep[k][5][:len(j["points"])])] if j["points"] else []
+            pk = [point(v) for v in limbs_to_ints(pks[k][:n])] if n else []
             res.append((int(o.status), share, y, pk))
         return res
 

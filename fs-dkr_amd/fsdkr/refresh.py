@@ -238,18 +238,18 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     batch = CollectBatch(msgs, local_key, joins, m_security, key_bits, staged=True)
     if batch.ga_ready:
         ctx.collect_prestart(batch)
-    batch.complete()
-    spec = None
-    if batch.header_only:
-        verdicts = None
-    else:
-        ctx.collect_prepare(batch)
-        ctx.collect_launch()
-        try:
-            if recovery == "speculative":
-                spec = _speculative(ctx, [job])[0]
-        finally:   # the batch never stays in flight
+    spec, verdicts = None, None
+    # the share recovery's GPU work runs beside the whole verification
+    pend = _speculative_launch(ctx, [job]) if recovery == "speculative" and not batch.header_only else None
+    try:
+        batch.complete()
+        if not batch.header_only:
+            ctx.collect_prepare(batch)
+            ctx.collect_launch()
             verdicts = ctx.collect_finish(batch)
+    finally:   # the recovery never stays in flight
+        if pend is not None:
+            spec = _speculative_finish(ctx, pend)[0]
     err, applied = _mapped(ctx, batch, msgs, verdicts)
     if recovery == "after" or batch.header_only:
         spec = _recover_after(ctx, [job], [err])[0]
@@ -275,19 +275,21 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="sp
     sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits, staged=True)
     if sset.n_prestart:   # every session's s2^N, s^N mod N^2 chains start while the rest is packed
         ctx.collect_prestart_set(sset)
-    sset.complete()
-    live = sset.live
     specs = [None] * len(sess)
     verdicts = None
-    if live:
-        ctx.collect_prepare_set(sset)
-        ctx.collect_launch()
-        try:
-            if recovery == "speculative":
-                for i, r in zip(live, _speculative(ctx, [jobs[i] for i in live])):
-                    specs[i] = r
-        finally:   # the batch never stays in flight
+    early = sorted(sset.row) if recovery == "speculative" else []
+    pend = _speculative_launch(ctx, [jobs[i] for i in early]) if early else None
+    try:
+        sset.complete()
+        live = sset.live
+        if live:
+            ctx.collect_prepare_set(sset)
+            ctx.collect_launch()
             verdicts = ctx.collect_finish_set(sset)
+    finally:   # the recovery never stays in flight
+        if pend is not None:
+            for i, r in zip(early, _speculative_finish(ctx, pend)):
+                specs[i] = r
     errs = []
     for i, (msgs, lk, dk, joins) in enumerate(sess):
         if i in sset.row:
@@ -332,18 +334,19 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
         batch = CollectBatch(msgs, lk0, joins, m_security, key_bits, staged=True)
         if batch.ga_ready:
             ctx.collect_prestart(batch)
-        batch.complete()
         jobs = [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members]
         specs = [None] * len(members)
         verdicts = None
-        if not batch.header_only:
-            ctx.collect_prepare(batch)
-            ctx.collect_launch()
-            try:
-                if recovery == "speculative":
-                    specs = _speculative(ctx, jobs)
-            finally:   # the batch never stays in flight
+        pend = _speculative_launch(ctx, jobs) if recovery == "speculative" and not batch.header_only else None
+        try:
+            batch.complete()
+            if not batch.header_only:
+                ctx.collect_prepare(batch)
+                ctx.collect_launch()
                 verdicts = ctx.collect_finish(batch)
+        finally:   # the recovery never stays in flight
+            if pend is not None:
+                specs = _speculative_finish(ctx, pend)
         err, applied = _mapped(ctx, batch, msgs, verdicts)
         if recovery == "after" or batch.header_only:
             specs = _recover_after(ctx, jobs, [err] * len(jobs))
@@ -367,6 +370,14 @@ def _speculative(ctx, jobs):
     fsdkr_collect_recover call on the recovery stream (GPU decryptions + one MSM
     launch).  Per job: the 4-tuple (share, y, pk_vec, t_ok) or the exception the
     reference raises there."""
+    return _speculative_finish(ctx, _speculative_launch(ctx, jobs))
+
+
+def _speculative_launch(ctx, jobs):
+    """The host pre-pass of _speculative and the launch of its GPU work
+    (fsdkr_collect_recover_launch); _speculative_finish collects the results.
+    collect() launches it before its own pipeline: it reads only the messages
+    and the local key, which the caller holds before any proof is checked."""
     out = [None] * len(jobs)
     todo, cj = [], []
     for k, (msgs, lk, n_new) in enumerate(jobs):
@@ -383,8 +394,13 @@ def _speculative(ctx, jobs):
         todo.append(k)
         cj.append(dict(nl=nl, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=plan["cts"],
                        p=lk.paillier_dk.p, q=lk.paillier_dk.q, points=plan["pts"]))
-    if cj:
-        for k, (status, share, y, pk) in zip(todo, ctx.collect_recover(cj)):
+    return out, todo, (ctx.collect_recover_launch(cj) if cj else None)
+
+
+def _speculative_finish(ctx, pending):
+    out, todo, handle = pending
+    if handle is not None:
+        for k, (status, share, y, pk) in zip(todo, ctx.collect_recover_finish(handle)):
             if status == 2:   # FSDKR_RECOVER_PANIC_DECRYPT
                 out[k] = FsDkrPanic("share recovery: Paillier::decrypt (degenerate decryption key)")
             else:

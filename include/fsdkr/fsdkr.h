@@ -395,6 +395,16 @@ typedef struct fsdkr_recovered {
   int32_t status;             /* FSDKR_RECOVER_* */
 } fsdkr_recovered;
 int fsdkr_collect_recover(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count, fsdkr_recovered* out);
+/* The same as two calls, so the recovery overlaps the caller's other work: _launch
+ * copies every input, does the host pre-pass (Lagrange weights, CRT constants,
+ * ciphertext reductions) and enqueues the GPU work (the decryption
+ * exponentiations, the pk_vec MSM) on the recovery stream, then returns;
+ * _finish waits for it and fills `out` as fsdkr_collect_recover does.  One
+ * recovery in flight per context; collect() launches it before its own
+ * pipeline (refresh_message.rs:439-464 only reads inputs the caller holds
+ * before verification). */
+int fsdkr_collect_recover_launch(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, uint32_t count);
+int fsdkr_collect_recover_finish(fsdkr_ctx* ctx, fsdkr_recovered* out);
 
 /* Kernel timing (needs FSDKR_CFG_TIMING): accumulated milliseconds and launch
  * count of kernel `name` since the last reset ("modexp", "mod_setup", ...). */

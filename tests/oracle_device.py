@@ -92,6 +92,12 @@ class OracleDevice:
             out.append((1 if j["t_key"] > j["t_vss"] else 0, share, ec.mul(ec.G, share), pk))
         return out
 
+    def collect_recover_launch(self, jobs):
+        return list(jobs)
+
+    def collect_recover_finish(self, handle):
+        return self.collect_recover(handle)
+
     def ec_msm(self, rows, scs):
         out = []
         for row, sc in zip(rows, scs):
