@@ -398,14 +398,16 @@ struct RecoverPending {
     uint32_t nl = 0, total = 0, keys = 0, exp_bits = 0;
     std::vector<uint32_t> base, ex, idx, mods;
     std::vector<uint8_t> desc;
-    Pinned out;
+    uint32_t* out = nullptr;   // pinned, dec_out[class]
   };
   std::vector<Job> jobs;
   std::vector<Width> widths;
   uint32_t rows = 0, terms = 1;
   std::vector<uint32_t> pts, scs;
   std::vector<uint64_t> ptrs;
-  Pinned msm_out;
+  // pinned D2H targets, kept across calls (allocating or freeing pinned memory
+  // synchronises the device, which would wait for a running pipeline)
+  Pinned dec_out[4], msm_out;
   hipEvent_t done = nullptr;
   bool in_flight = false;
 
@@ -458,7 +460,8 @@ int RecoverPending::launch(Ctx* c, const fsdkr_recover_job* in, uint32_t count) 
     }
   });
   // decryption batches, one per key width: (c mod p^2)^(p-1), (c mod q^2)^(q-1)
-  for (uint32_t nl : {64u, 96u, 128u, 192u}) {
+  for (uint32_t wc = 0; wc < 4; ++wc) {
+    const uint32_t nl = 64u + 32u * wc + (wc == 3 ? 32u : 0u);   // 64, 96, 128, 192
     Width W;
     W.nl = nl;
     std::vector<uint32_t> owners;
@@ -526,7 +529,8 @@ int RecoverPending::launch(Ctx* c, const fsdkr_recover_job* in, uint32_t count) 
     const std::string tag = "rc" + std::to_string(nl);
     const size_t nb = (size_t)n * nl * 4;
     uint8_t* d = (uint8_t*)c->buf((tag + "_io").c_str(), 3 * nb + (size_t)nm * nl * 4 + 1024);
-    uint32_t* h_out = W.out.get(nb);
+    const uint32_t wc = nl == 64 ? 0 : nl == 96 ? 1 : nl == 128 ? 2 : 3;
+    uint32_t* h_out = W.out = dec_out[wc].get(nb);
     if (!d || !h_out) {
       c->fail("fsdkr_collect_recover: allocation failed");
       return FSDKR_E_OOM;
@@ -607,7 +611,7 @@ int RecoverPending::finish(Ctx* c, fsdkr_recovered* out) {
         continue;
       }
       const uint32_t nl = X.nl;
-      const uint32_t* h = reinterpret_cast<const uint32_t*>(widths[X.width].out.p);
+      const uint32_t* h = widths[X.width].out;
       // kzen-paillier CRT decryption with g = N + 1: h_p = L_p(g^(p-1) mod p^2)^-1 = p - q^-1 mod p
       const hbn::Limbs hp = hbn::sub(X.P, X.qinv), hq = hbn::sub(X.Q, X.pinv);
       const hbn::Limbs N = hbn::mul(X.P, X.Q);
