@@ -243,9 +243,9 @@ def pmc_traffic(count):
 
 def phases(ctx, msgs, lk, joins, key_bits):
     """One instrumented collect, in refresh.collect's order: where the host time
-    of a step goes (stage-1 pack, GA prestart, share-recovery launch, stage-2
-    pack overlapping the prestarted chains, prepare, pipeline launch, finish
-    wait, recovery finish, first error)."""
+    of a step goes (stage-1 pack, GA prestart, stage-2 pack overlapping the
+    prestarted chains, prepare, pipeline launch, share-recovery launch (its host
+    pre-pass overlaps the pipeline), finish wait, recovery finish, first error)."""
     from fsdkr.batch import CollectBatch
     from fsdkr.refresh import _speculative_finish, _speculative_launch
     t0 = time.perf_counter()
@@ -253,14 +253,14 @@ def phases(ctx, msgs, lk, joins, key_bits):
     ts = time.perf_counter()
     ctx.collect_prestart(b)
     tp = time.perf_counter()
-    pend = _speculative_launch(ctx, [(msgs, lk, len(msgs) + len(joins))])
-    tr = time.perf_counter()
     b.complete()
     t1 = time.perf_counter()
     ctx.collect_prepare(b)
     t2 = time.perf_counter()
     ctx.collect_launch()
     t3 = time.perf_counter()
+    pend = _speculative_launch(ctx, [(msgs, lk, len(msgs) + len(joins))])
+    tr = time.perf_counter()
     v = ctx.collect_finish(b)
     t4 = time.perf_counter()
     _speculative_finish(ctx, pend)
@@ -275,8 +275,8 @@ def phases(ctx, msgs, lk, joins, key_bits):
         ctx.collect_run(b)
         runs.append((time.perf_counter() - a) * 1e3)
     return b, v, {"pack_stage1_ms": (ts - t0) * 1e3, "prestart_ms": (tp - ts) * 1e3,
-                  "recovery_launch_ms": (tr - tp) * 1e3, "pack_stage2_ms": (t1 - tr) * 1e3,
-                  "prepare_ms": (t2 - t1) * 1e3, "launch_ms": (t3 - t2) * 1e3, "finish_wait_ms": (t4 - t3) * 1e3,
+                  "pack_stage2_ms": (t1 - tp) * 1e3, "prepare_ms": (t2 - t1) * 1e3, "launch_ms": (t3 - t2) * 1e3,
+                  "recovery_launch_ms": (tr - t3) * 1e3, "finish_wait_ms": (t4 - tr) * 1e3,
                   "recovery_finish_ms": (t45 - t4) * 1e3, "first_error_ms": (t5 - t45) * 1e3,
                   "device_pipeline_ms": min(runs)}
 

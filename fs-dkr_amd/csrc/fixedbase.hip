@@ -269,9 +269,11 @@ static hipError_t table_launch_wave(const FbTableArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Bases whose chains fit one wave per SIMD (n = 64: 192 chains) run one per wave;
-// more (many sessions) the 8- / 4-lane group shapes.
-constexpr uint32_t kFbWaveMax = 1024;
+// Few bases (n = 64: 192 chains; a multi-GPU rank's receivers) run one per wave,
+// latency first; more (n = 256: 768 chains, many sessions) the 8- / 4-lane group
+// shapes, whose MACs per issued instruction are higher (the wave shape at n = 256
+// measured 606 -> 728 ms per collect, profiles/r03o_bench.json config3).
+constexpr uint32_t kFbWaveMax = 256;
 
 hipError_t launch_fb_table(uint32_t k32, const FbTableArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;

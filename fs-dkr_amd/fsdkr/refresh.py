@@ -238,18 +238,18 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     batch = CollectBatch(msgs, local_key, joins, m_security, key_bits, staged=True)
     if batch.ga_ready:
         ctx.collect_prestart(batch)
-    spec, verdicts = None, None
-    # the share recovery's GPU work runs beside the whole verification
-    pend = _speculative_launch(ctx, [job]) if recovery == "speculative" and not batch.header_only else None
-    try:
-        batch.complete()
-        if not batch.header_only:
-            ctx.collect_prepare(batch)
-            ctx.collect_launch()
+    spec, verdicts, pend = None, None, None
+    batch.complete()
+    if not batch.header_only:
+        ctx.collect_prepare(batch)
+        ctx.collect_launch()
+        try:   # the share recovery's host pre-pass and GPU work overlap the pipeline
+            if recovery == "speculative":
+                pend = _speculative_launch(ctx, [job])
+        finally:   # the batch never stays in flight
             verdicts = ctx.collect_finish(batch)
-    finally:   # the recovery never stays in flight
-        if pend is not None:
-            spec = _speculative_finish(ctx, pend)[0]
+            if pend is not None:   # nor does the recovery
+                spec = _speculative_finish(ctx, pend)[0]
     err, applied = _mapped(ctx, batch, msgs, verdicts)
     if recovery == "after" or batch.header_only:
         spec = _recover_after(ctx, [job], [err])[0]
@@ -275,21 +275,21 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="sp
     sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits, staged=True)
     if sset.n_prestart:   # every session's s2^N, s^N mod N^2 chains start while the rest is packed
         ctx.collect_prestart_set(sset)
+    sset.complete()
+    live = sset.live
     specs = [None] * len(sess)
-    verdicts = None
-    early = sorted(sset.row) if recovery == "speculative" else []
-    pend = _speculative_launch(ctx, [jobs[i] for i in early]) if early else None
-    try:
-        sset.complete()
-        live = sset.live
-        if live:
-            ctx.collect_prepare_set(sset)
-            ctx.collect_launch()
+    verdicts, pend = None, None
+    if live:
+        ctx.collect_prepare_set(sset)
+        ctx.collect_launch()
+        try:   # the share recovery's host pre-pass and GPU work overlap the pipeline
+            if recovery == "speculative":
+                pend = _speculative_launch(ctx, [jobs[i] for i in live])
+        finally:   # the batch never stays in flight
             verdicts = ctx.collect_finish_set(sset)
-    finally:   # the recovery never stays in flight
-        if pend is not None:
-            for i, r in zip(early, _speculative_finish(ctx, pend)):
-                specs[i] = r
+            if pend is not None:   # nor does the recovery
+                for i, r in zip(live, _speculative_finish(ctx, pend)):
+                    specs[i] = r
     errs = []
     for i, (msgs, lk, dk, joins) in enumerate(sess):
         if i in sset.row:
@@ -336,17 +336,18 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
             ctx.collect_prestart(batch)
         jobs = [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members]
         specs = [None] * len(members)
-        verdicts = None
-        pend = _speculative_launch(ctx, jobs) if recovery == "speculative" and not batch.header_only else None
-        try:
-            batch.complete()
-            if not batch.header_only:
-                ctx.collect_prepare(batch)
-                ctx.collect_launch()
+        verdicts, pend = None, None
+        batch.complete()
+        if not batch.header_only:
+            ctx.collect_prepare(batch)
+            ctx.collect_launch()
+            try:   # the share recovery's host pre-pass and GPU work overlap the pipeline
+                if recovery == "speculative":
+                    pend = _speculative_launch(ctx, jobs)
+            finally:   # the batch never stays in flight
                 verdicts = ctx.collect_finish(batch)
-        finally:   # the recovery never stays in flight
-            if pend is not None:
-                specs = _speculative_finish(ctx, pend)
+                if pend is not None:   # nor does the recovery
+                    specs = _speculative_finish(ctx, pend)
         err, applied = _mapped(ctx, batch, msgs, verdicts)
         if recovery == "after" or batch.header_only:
             specs = _recover_after(ctx, jobs, [err] * len(jobs))
@@ -376,8 +377,8 @@ def _speculative(ctx, jobs):
 def _speculative_launch(ctx, jobs):
     """The host pre-pass of _speculative and the launch of its GPU work
     (fsdkr_collect_recover_launch); _speculative_finish collects the results.
-    collect() launches it before its own pipeline: it reads only the messages
-    and the local key, which the caller holds before any proof is checked."""
+    collect() launches it right after its pipeline, so the host pre-pass (the
+    Lagrange weights: O(t^2) products at n = 256) overlaps the device work."""
     out = [None] * len(jobs)
     todo, cj = [], []
     for k, (msgs, lk, n_new) in enumerate(jobs):

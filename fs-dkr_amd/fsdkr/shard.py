@@ -82,13 +82,10 @@ def merge(dist, local_vec, device=None):
     return t.cpu().numpy()
 
 
-def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=2048, launch_only=False,
-                 after_prestart=None):
+def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=2048, launch_only=False):
     """This rank's slice as a CollectBatch (n_recv = n); launched on the GPU.
     Returns (batch or None, verdicts or None); with launch_only the caller
-    finishes it (ctx.collect_finish).  after_prestart() runs once the longest
-    chains are on the GPU, before the rest of the slice is packed (shard.collect
-    launches the share recovery there)."""
+    finishes it (ctx.collect_finish) after overlapping host work."""
     R, J = len(msgs), len(joins)
     n = R + J
     r0, r1 = shard_range(R, world, rank)
@@ -106,8 +103,6 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
         return None, None
     if b.ga_ready and hasattr(ctx, "collect_prestart"):   # the long chains start while stage 2 packs
         ctx.collect_prestart(b)
-    if after_prestart is not None:
-        after_prestart()
     b.complete()
     ctx.collect_prepare(b)
     ctx.collect_launch()
@@ -137,23 +132,16 @@ def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, devic
     if header.size_fail:
         merged = None
     else:
-        # the share recovery's GPU work runs on the recovery stream beside the slice's
-        # verification, launched as soon as the slice's longest chains are on the GPU
-        pend = []
-
-        def launch_recovery():
-            if recovery == "speculative" and not pend:
-                pend.append(_speculative_launch(ctx, [job]))
-        v = None
-        try:
-            b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True,
-                                after_prestart=launch_recovery)
-            launch_recovery()   # an empty slice: no prestart hook ran
-            if b is not None:   # the slice never stays in flight
+        b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True)
+        v, pend = None, None
+        try:   # the share recovery overlaps the slice's pipeline on the recovery stream
+            if recovery == "speculative":
+                pend = _speculative_launch(ctx, [job])
+        finally:   # the slice never stays in flight
+            if b is not None:
                 v = ctx.collect_finish(b)
-        finally:   # nor does the recovery
-            if pend:
-                spec = _speculative_finish(ctx, pend[0])[0]
+            if pend is not None:   # nor does the recovery
+                spec = _speculative_finish(ctx, pend)[0]
         merged = MergedVerdicts(merge(dist, scatter(v, R, J, n, world, rank), device), R, J, n)
     err, applied = _mapped(ctx, header, msgs, merged)
     if recovery == "after" or header.size_fail:
