@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <openssl/evp.h>
 
+#include "evp_sha.hpp"
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -124,7 +126,7 @@ struct HostSha {
   bool digest(uint32_t* e8) {
     uint8_t d[32];
     unsigned int len = 0;
-    const bool ok = ctx && EVP_DigestInit_ex(ctx, EVP_sha256(), nullptr) == 1 &&
+    const bool ok = ctx && EVP_DigestInit_ex(ctx, sha256_md(), nullptr) == 1 &&
                     EVP_DigestUpdate(ctx, buf.data(), buf.size()) == 1 && EVP_DigestFinal_ex(ctx, d, &len) == 1 &&
                     len == 32;
     if (ok) digest_le(d, e8);

@@ -203,6 +203,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     if (x.b->ck_lens && x.b->ck_lens[lm] < CK_M2) pl.ck_short[m] = 1;
   }
   parallel_for(Mt, 4, [&](size_t b0, size_t b1) {
+    HostSha sha;
     for (size_t m = b0; m < b1; ++m) {
       const Sess& x = pl.ss[sess_of_msg[m]];
       const fsdkr_collect_batch* b = x.b;
@@ -223,19 +224,18 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
         const hbn::Limbs Nl = hbn::from(ckn, x.ckl);
         std::vector<uint32_t> mask((size_t)msklen * 8, 0);
         for (uint32_t j = 0; j < CK_M2; ++j) {
-          Sha256 h;
-          h.init();
-          h.bigint(ckn, x.ckl);
-          absorb_u32(h, salt_v);
-          absorb_u32(h, j);
+          // seed = H(n, salt, j), mask block k = H(seed, k): each value as curv to_bytes
+          sha.buf.clear();
+          put_bigint(sha.buf, ckn, x.ckl);
+          put_bigint(sha.buf, &salt_v, 1);
+          put_bigint(sha.buf, &j, 1);
           uint32_t seed[8];
-          h.finish_le(seed);
+          if (!sha.digest(seed)) sha_fail = true;
           for (uint32_t k = 0; k < msklen; ++k) {
-            Sha256 hk;
-            hk.init();
-            hk.bigint(seed, 8);
-            absorb_u32(hk, k);
-            hk.finish_le(mask.data() + (size_t)k * 8);
+            sha.buf.clear();
+            put_bigint(sha.buf, seed, 8);
+            put_bigint(sha.buf, &k, 1);
+            if (!sha.digest(mask.data() + (size_t)k * 8)) sha_fail = true;
           }
           hbn::store(hbn::mod(hbn::from(mask.data(), mask.size()), Nl), RHO.data() + (m * CK_M2 + j) * ckl, ckl);
         }
@@ -270,6 +270,10 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     }
   });
   clk.lap("ck rho+primes");
+  if (sha_fail) {
+    c->fail("fsdkr_collect_prepare: SHA-256 (OpenSSL EVP) failed");
+    return FSDKR_E_ARG;
+  }
   // DLog statements: N > 2^128, gcd(g, N) = gcd(ni, N) = 1, x < N; challenges e = H(x, g, N, ni)
   pl.dlog_pre.assign(J, 0);
   pl.dlog_trivial.assign(J, 0);

@@ -233,8 +233,11 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
     return rc;
   (void)hipEventRecord(g.ga_setup, gs);   // GA's constants are ready
-  // issue priority 3 (2 measured 1-2 ms slower per call, profiles/r02x_ab_full.jsonl)
-  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 3, group)))
+  // issue priority 2: GA ends ~13 ms before the pipeline's last jobs, which need
+  // the issue slots more (n = 64 median of 7 interleaved calls 56.4 -> 55.3 ms vs
+  // priority 3, profiles/r03s_ga_prio_ab.jsonl; round 2, with the PDL hash on the
+  // GPU's critical path, measured 3 faster)
+  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 2, group)))
     return rc;
   if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;

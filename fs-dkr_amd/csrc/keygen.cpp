@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "evp_sha.hpp"
 #include "hostbn.hpp"
 #include "kernels.h"
 
@@ -172,7 +173,7 @@ bool witness_bases(const hbn::Limbs& c, std::vector<hbn::Limbs>* out) {
                        (uint8_t)ctr, (uint8_t)(ctr >> 8), (uint8_t)(ctr >> 16), (uint8_t)(ctr >> 24)};
       uint8_t d[32];
       unsigned int len = 0;
-      ok = ok && EVP_DigestInit_ex(md, EVP_sha256(), nullptr) == 1 &&
+      ok = ok && EVP_DigestInit_ex(md, sha256_md(), nullptr) == 1 &&
            EVP_DigestUpdate(md, "fsdkr-mr", 8) == 1 && EVP_DigestUpdate(md, cb.data(), nb) == 1 &&
            EVP_DigestUpdate(md, le, 8) == 1 && EVP_DigestFinal_ex(md, d, &len) == 1;
       stream.insert(stream.end(), d, d + 32);
