@@ -10,6 +10,7 @@
 #include <openssl/obj_mac.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <cstring>
 #include <thread>
@@ -599,7 +600,7 @@ int RecoverPending::finish(Ctx* c, fsdkr_recovered* out) {
   int rc = c->hip_check(hipEventSynchronize(done), "recovery wait");
   if (rc) return rc;
   const hbn::Limbs Qs = hbn::from(SECP_Q, 8), one{1};
-  bool ec_ok = true;
+  std::atomic<bool> ec_ok{true};
   parallel_for_host(jobs.size(), 1, [&](size_t b0, size_t b1) {
     for (size_t j = b0; j < b1; ++j) {
       const Job& X = jobs[j];

@@ -318,3 +318,36 @@ def test_collect_recover_entry(gpu_ctx, dkr5):
     assert got[:5] == want
     assert got[5][0] == 2                       # FSDKR_RECOVER_PANIC_DECRYPT
     assert got[6][0] == 1 and got[6][1:3] == want[2][1:3]   # FSDKR_RECOVER_PANIC_LI, share still recovered
+
+
+def test_collect_recover_launch_finish(gpu_ctx, dkr5):
+    """fsdkr_collect_recover_launch / _finish: the same results as the one-call
+    form while a collect batch runs beside it, inputs copied at launch (the
+    caller's arrays may go away), one recovery in flight per context, and a
+    finish without a launch refused."""
+    from fsdkr._native import FsdkrError
+    from fsdkr.batch import CollectBatch
+    from fsdkr.refresh import _dk_limbs
+    keys, msgs, dks, _ = dkr5
+    jobs = []
+    for party in range(5):
+        lk = keys[party]
+        t = lk.vss_scheme.threshold
+        jobs.append(dict(nl=_dk_limbs(lk.paillier_dk), t_vss=t, t_key=lk.t,
+                         old_index=[m.old_party_index for m in msgs[:t + 1]],
+                         cts=[m.points_encrypted_vec[lk.i - 1] for m in msgs[:t + 1]],
+                         p=lk.paillier_dk.p, q=lk.paillier_dk.q,
+                         points=[[m.points_committed_vec[i] for m in msgs[:t + 1]] for i in range(5)]))
+    want = gpu_ctx.collect_recover(jobs)
+    b = CollectBatch(msgs, keys[0], [], 256, KB)
+    gpu_ctx.collect_prepare(b)
+    gpu_ctx.collect_launch()
+    h = gpu_ctx.collect_recover_launch(jobs)
+    with pytest.raises(FsdkrError):
+        gpu_ctx.collect_recover_launch(jobs)     # one in flight
+    v = gpu_ctx.collect_finish(b)
+    assert gpu_ctx.collect_recover_finish(h) == want
+    assert (v.pdl & 7 == 7).all()
+    with pytest.raises(FsdkrError):
+        gpu_ctx.collect_recover_finish(h)        # nothing launched any more
+    assert gpu_ctx.collect_recover(jobs) == want  # the context is usable again
