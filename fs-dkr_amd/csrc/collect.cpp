@@ -195,14 +195,13 @@ int fsdkr_collect_prepare(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
 int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch) {
   fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
   if (!c) return FSDKR_E_ARG;
-  return fsdkr::collect_prestart_impl(c, batch);
+  return fsdkr::collect_prestart_impl(c, batch, 1);
 }
 
 int fsdkr_collect_prestart_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count) {
   fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
   if (!c) return FSDKR_E_ARG;
-  uint32_t n = 0, P = 0;
-  return fsdkr::prestart_ga(c, batches, count, &n, &P);
+  return fsdkr::collect_prestart_impl(c, batches, count);
 }
 
 int fsdkr_collect_launch(fsdkr_ctx* ctx) {

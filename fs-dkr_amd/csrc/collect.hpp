@@ -373,7 +373,7 @@ inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
 
 // collect_prestart.cpp
 int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t* n_out, uint32_t* P_out);
-int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b);
+int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_prepare.cpp
 int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);

@@ -614,14 +614,29 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   // the h1_i / h2_i tables of a prestart: sized for the prestart's exponent bounds
   // (taller tables only add unused entries), used if the layout then agrees
   const GaPre* gp = reinterpret_cast<const GaPre*>(c->ga_pre);
-  const bool fb_cand = count == 1 && gp && gp->fb_valid && gp->nl == nl && gp->n == n && gp->Mt == Mt &&
-                       memcmp(gp->ntilde.data(), bs->recv_ntilde, (size_t)n * nl * 4) == 0 &&
-                       memcmp(gp->h1.data(), bs->recv_h1, (size_t)n * nl * 4) == 0 &&
-                       memcmp(gp->h2.data(), bs->recv_h2, (size_t)n * nl * 4) == 0 &&
-                       memcmp(gp->T.data(), bs->ped_T, (size_t)Mt * nl * 4) == 0 &&
-                       memcmp(gp->pedmod.data(), PEDN.data(), (size_t)Mt * nl * 4) == 0 &&
-                       std::max(mx.s1, mx.as1) <= gp->bits_h1 && std::max(mx.s3, mx.as2) <= gp->bits_h2 &&
-                       z_max <= gp->bits_z;
+  // the prestart's rows are global (session s after s-1) at width nl, zero-extended
+  auto same_rows = [&](const std::vector<uint32_t>& pre, size_t base, const uint32_t* src, size_t rows,
+                       uint32_t ws) {
+    if (pre.size() < (base + rows) * nl) return false;
+    for (size_t r = 0; r < rows; ++r) {
+      const uint32_t* a = pre.data() + (base + r) * nl;
+      if (memcmp(a, src + r * ws, (size_t)ws * 4) != 0) return false;
+      for (uint32_t k = ws; k < nl; ++k)
+        if (a[k]) return false;
+    }
+    return true;
+  };
+  bool fb_cand = gp && gp->fb_valid && gp->nl == nl && gp->n == n && gp->Mt == Mt &&
+                 memcmp(gp->pedmod.data(), PEDN.data(), (size_t)Mt * nl * 4) == 0 &&
+                 std::max(mx.s1, mx.as1) <= gp->bits_h1 && std::max(mx.s3, mx.as2) <= gp->bits_h2 &&
+                 z_max <= gp->bits_z;
+  for (const Sess& x : pl.ss) {
+    if (!fb_cand) break;
+    fb_cand = same_rows(gp->ntilde, x.rbase, x.b->recv_ntilde, x.n, x.b->nl) &&
+              same_rows(gp->h1, x.rbase, x.b->recv_h1, x.n, x.b->nl) &&
+              same_rows(gp->h2, x.rbase, x.b->recv_h2, x.n, x.b->nl) &&
+              same_rows(gp->T, x.mbase, x.b->ped_T, x.Mt, x.b->nl);
+  }
   if (fb_cand) {
     for (uint32_t r = 0; r < n; ++r) {
       FB.b_bits[fb_h1[r]] = gp->bits_h1;

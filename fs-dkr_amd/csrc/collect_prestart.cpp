@@ -12,31 +12,55 @@ namespace fsdkr {
 // of every receiver's DLogStatement (h2: one squaring per exponent bit of s3,
 // ~2816 at 2048-bit keys), then every message's ring-Pedersen T, sized by the
 // bit lengths of the exponents they serve (PDL / Alice s1, s3|s2; RP Z), on the
-// table chain's stream.
-static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, uint32_t n, uint32_t P) {
-  if (!b->recv_ntilde || !b->recv_h1 || !b->recv_h2 || !b->s1l || !b->s3l || !b->ped_T || !b->ped_N || !b->zl ||
-      !b->m_security)
-    return FSDKR_OK;   // stage 1 did not pack them: prepare builds every table
+// table chain's stream.  `count` sessions in prepare's global order (session
+// s's receivers and messages after session s-1's, rows at the widest nl); the
+// sessions' row bases come from the GA prestart (g.sess).  A stage 1 without
+// the exponents sizes the tables by the slots' widths (s1l, s3l, zl): honest
+// exponents fit (s1 < 2^770, s3 < 2^770 N~, Z < phi(N)), and prepare rebuilds
+// the tables if one does not.
+static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, GaPre& g, uint32_t n, uint32_t P) {
+  if (g.sess.size() != count) return FSDKR_OK;
+  const uint32_t M = bs[0].m_security;
+  bool exact_s = true, exact_z = true;
+  uint32_t nl = 0, Mt = 0, s1l = 0, s3l = 0, zl = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (!b->recv_ntilde || !b->recv_h1 || !b->recv_h2 || !b->s1l || !b->s3l || !b->ped_T || !b->ped_N || !b->zl ||
+        !b->m_security || b->m_security != M)
+      return FSDKR_OK;   // stage 1 did not pack them: prepare builds every table
+    exact_s = exact_s && b->pdl_s1 && b->pdl_s3 && b->rp_s1 && b->rp_s2;
+    exact_z = exact_z && b->ped_Z;
+    nl = std::max(nl, b->nl);
+    Mt += b->n_refresh + b->n_join;
+    s1l = std::max(s1l, b->s1l);
+    s3l = std::max(s3l, b->s3l);
+    zl = std::max(zl, b->zl);
+    for (uint32_t i = 0; i < g.sess[k].n; ++i)
+      if (!is_odd(b->recv_ntilde + (size_t)i * b->nl)) return FSDKR_OK;
+  }
   // exponent bit bounds: exact from the packed exponents, else their slot widths
-  // (a slim stage 1 leaves s1 / s3 / Z to stage 2; tables at most 31 bits longer)
-  const bool exact_s = b->pdl_s1 && b->pdl_s3 && b->rp_s1 && b->rp_s2;
-  const uint32_t nl = b->nl, Mt = b->n_refresh + b->n_join, M = b->m_security;
-  for (uint32_t i = 0; i < n; ++i)
-    if (!is_odd(b->recv_ntilde + (size_t)i * nl)) return FSDKR_OK;
   uint32_t bh1 = 1, bh2 = 1, bz = 1;
   if (exact_s) {
-    for (size_t p = 0; p < P; ++p) {
-      bh1 = std::max(bh1, std::max(hbn::bitlen(b->pdl_s1 + p * b->s1l, b->s1l), hbn::bitlen(b->rp_s1 + p * b->s1l, b->s1l)));
-      bh2 = std::max(bh2, std::max(hbn::bitlen(b->pdl_s3 + p * b->s3l, b->s3l), hbn::bitlen(b->rp_s2 + p * b->s3l, b->s3l)));
+    for (uint32_t k = 0; k < count; ++k) {
+      const fsdkr_collect_batch* b = bs + k;
+      for (size_t p = 0; p < (size_t)g.sess[k].R * g.sess[k].n; ++p) {
+        bh1 = std::max(bh1, std::max(hbn::bitlen(b->pdl_s1 + p * b->s1l, b->s1l), hbn::bitlen(b->rp_s1 + p * b->s1l, b->s1l)));
+        bh2 = std::max(bh2, std::max(hbn::bitlen(b->pdl_s3 + p * b->s3l, b->s3l), hbn::bitlen(b->rp_s2 + p * b->s3l, b->s3l)));
+      }
     }
   } else {
-    bh1 = 32 * b->s1l;
-    bh2 = 32 * b->s3l;
+    bh1 = 32 * s1l;
+    bh2 = 32 * s3l;
   }
-  if (b->ped_Z)
-    for (size_t k = 0; k < (size_t)Mt * M; ++k) bz = std::max(bz, hbn::bitlen(b->ped_Z + k * b->zl, b->zl));
-  else
-    bz = 32 * b->zl;
+  if (exact_z) {
+    for (uint32_t k = 0; k < count; ++k) {
+      const fsdkr_collect_batch* b = bs + k;
+      const size_t rows = (size_t)(b->n_refresh + b->n_join) * M;
+      for (size_t q = 0; q < rows; ++q) bz = std::max(bz, hbn::bitlen(b->ped_Z + q * b->zl, b->zl));
+    }
+  } else {
+    bz = 32 * zl;
+  }
   const uint32_t w = fb_window(std::max(std::max(bh1, bh2), bz));
   const FbLayout L = fb_layout(n, Mt, w, bh1, bh2, bz);
   const uint32_t nb = 2 * n + Mt, entries = L.entries, nmod = n + Mt;
@@ -54,11 +78,23 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   }
   std::vector<uint8_t> img(o_tab, 0);
   uint32_t* mods = reinterpret_cast<uint32_t*>(img.data() + o_mod);   // [Ntilde_i | RP modulus_m]
-  memcpy(mods, b->recv_ntilde, (size_t)n * nl * 4);
-  for (uint32_t m = 0; m < Mt; ++m) ped_modulus(b, m, M, nl, mods + (size_t)(n + m) * nl);
-  memcpy(img.data() + o_h1, b->recv_h1, (size_t)n * nl * 4);
-  memcpy(img.data() + o_h2, b->recv_h2, (size_t)n * nl * 4);
-  memcpy(img.data() + o_T, b->ped_T, (size_t)Mt * nl * 4);
+  uint32_t* H1 = reinterpret_cast<uint32_t*>(img.data() + o_h1);
+  uint32_t* H2 = reinterpret_cast<uint32_t*>(img.data() + o_h2);
+  uint32_t* TT = reinterpret_cast<uint32_t*>(img.data() + o_T);
+  auto rows_to = [&](uint32_t* dst, const uint32_t* src, size_t rows, uint32_t ws) {   // zero-extended to nl
+    for (size_t r = 0; r < rows; ++r) memcpy(dst + r * nl, src + r * ws, (size_t)ws * 4);
+  };
+  for (uint32_t k = 0, mb = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const size_t rb = g.sess[k].rbase, ns = g.sess[k].n;
+    const uint32_t mt = b->n_refresh + b->n_join;
+    rows_to(mods + rb * nl, b->recv_ntilde, ns, b->nl);
+    rows_to(H1 + rb * nl, b->recv_h1, ns, b->nl);
+    rows_to(H2 + rb * nl, b->recv_h2, ns, b->nl);
+    rows_to(TT + (size_t)mb * nl, b->ped_T, mt, b->nl);
+    for (uint32_t m = 0; m < mt; ++m) ped_modulus(b, m, M, nl, mods + (size_t)(n + mb + m) * nl);
+    mb += mt;
+  }
   auto* bp = reinterpret_cast<uint64_t*>(img.data() + o_bp);
   for (uint32_t r = 0; r < n; ++r) {   // prepare's base order [h1_i | T_m | h2_i]
     bp[r] = (uint64_t)(uintptr_t)(dev + o_h1 + (size_t)r * nl * 4);
@@ -89,10 +125,10 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
   if ((rc = c->hip_check(launch_fb_table(nl, tall, ts), "prestart fb_table"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.fb_done, ts), "event record"))) return rc;
-  g.ntilde.assign(b->recv_ntilde, b->recv_ntilde + (size_t)n * nl);
-  g.h1.assign(b->recv_h1, b->recv_h1 + (size_t)n * nl);
-  g.h2.assign(b->recv_h2, b->recv_h2 + (size_t)n * nl);
-  g.T.assign(b->ped_T, b->ped_T + (size_t)Mt * nl);
+  g.ntilde.assign(mods, mods + (size_t)n * nl);
+  g.h1.assign(H1, H1 + (size_t)n * nl);
+  g.h2.assign(H2, H2 + (size_t)n * nl);
+  g.T.assign(TT, TT + (size_t)Mt * nl);
   g.pedmod.assign(mods + (size_t)n * nl, mods + (size_t)nmod * nl);
   g.Mt = Mt;
   g.fb_w = w;
@@ -101,6 +137,7 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* b, GaPre& g, ui
   g.bits_z = bz;
   g.fb_entries = entries;
   g.fb_valid = true;
+  (void)P;
   return FSDKR_OK;
 }
 
@@ -251,11 +288,11 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   return FSDKR_OK;
 }
 
-int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* b) {
+int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
   uint32_t n = 0, P = 0;
-  int rc = prestart_ga(c, b, 1, &n, &P);
+  int rc = prestart_ga(c, bs, count, &n, &P);
   if (rc || P == 0) return rc;
-  return prestart_fb_tables(c, b, *reinterpret_cast<GaPre*>(c->ga_pre), n, P);
+  return prestart_fb_tables(c, bs, count, *reinterpret_cast<GaPre*>(c->ga_pre), n, P);
 }
 
 // does the prestarted GA belong to these sessions (same shapes, same inputs)?

@@ -404,7 +404,7 @@ class SessionSet:
         # the prestart covers the set only when every prepared session is regular
         # (prepare_multi's session list must equal the prestart's)
         if staged and reg and len(reg) == len(self.live):
-            self._stage1(sessions, reg)
+            self._stage1(sessions, reg, M)
         if not staged:
             self.complete()
 
@@ -424,7 +424,12 @@ class SessionSet:
                                                           dtype=_BATCH_DT)[0]
         return self
 
-    def _stage1(self, sessions, reg):
+    def _stage1(self, sessions, reg, M):
+        """The fields fsdkr_collect_prestart_multi reads: the GA chains' (receivers'
+        N, PDL s2, range-proof s) and the fixed-base tables' bases (receivers' N~,
+        h1, h2; ring-Pedersen T and N).  The exponents stay in stage 2: the tables
+        are sized by honest bounds (s1 < 2^770, s3 | s2 < 2^770 N~, Z < phi(N)),
+        which prepare checks against the packed exponents."""
         ses = [sessions[s] for s in reg]
         R = np.array([len(m) for m, lk, j in ses], dtype=np.int64)
         n = R + np.array([len(j) for m, lk, j in ses], dtype=np.int64)
@@ -434,11 +439,19 @@ class SessionSet:
         f_rn = G.field([k for (ms, lk, js), nn in zip(ses, n) for k in lk.paillier_key_vec[:nn]], "n")
         f_s2 = G.field([m.pdl_proof_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s2")
         f_s = G.field([m.range_proofs[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s")
-        bits = max(1, f_rn[1], f_s2[1], f_s[1])
+        sts = [st for (ms, lk, js), nn in zip(ses, n) for st in lk.h1_h2_n_tilde_vec[:nn]]
+        if len(sts) != int(n.sum()):
+            return
+        f_nt, f_h1, f_h2 = G.field(sts, "N"), G.field(sts, "g"), G.field(sts, "ni")
+        rps = [m.ring_pedersen_statement for ms, lk, js in ses for m in ms + js]
+        f_T, f_N = G.field(rps, "T"), G.field(rps, "N")
+        bits = max(1, f_rn[1], f_s2[1], f_s[1], f_nt[1], f_h1[1], f_h2[1], f_T[1], f_N[1])
         nl = 64 if bits <= 2048 else 96 if bits <= 3072 else None
         if nl is None:
             return
         a_rn, a_s2, a_s = G.slot(f_rn, nl), G.slot(f_s2, nl), G.slot(f_s, nl)
+        a_nt, a_h1, a_h2 = G.slot(f_nt, nl), G.slot(f_h1, nl), G.slot(f_h2, nl)
+        a_T, a_N = G.slot(f_T, nl), G.slot(f_N, nl)
         G.run()
 
         def starts(counts):
@@ -450,6 +463,12 @@ class SessionSet:
         st["recv_n"] = np.uint64(self._k(a_rn)) + starts(n) * np.uint64(nl * 4)
         st["pdl_s2"] = np.uint64(self._k(a_s2)) + starts(R * n) * np.uint64(nl * 4)
         st["rp_s"] = np.uint64(self._k(a_s)) + starts(R * n) * np.uint64(nl * 4)
+        for name, arr in (("recv_ntilde", a_nt), ("recv_h1", a_h1), ("recv_h2", a_h2)):
+            st[name] = np.uint64(self._k(arr)) + starts(n) * np.uint64(nl * 4)
+        for name, arr in (("ped_T", a_T), ("ped_N", a_N)):
+            st[name] = np.uint64(self._k(arr)) + starts(n) * np.uint64(nl * 4)   # R + J messages per session
+        st["m_security"] = M
+        st["s1l"], st["s3l"], st["zl"] = _limbs_for(770), nl + _limbs_for(770), nl
         self._pre, self.n_prestart = st, len(reg)
 
     def prestart_array(self):
