@@ -126,52 +126,75 @@ __global__ __launch_bounds__(64) void fb_table_wave_kernel(const FbTableArgs a) 
   }
 }
 
-// One thread per instance: the BGMW product schedule of its exponent, by a
+// One wave64 per instance: the BGMW product schedule of its exponent, by a
 // counting sort of its w-bit digits (O(h + 2^w)): for d = max digit .. 1 the
-// windows j with e_j = d (ascending j), then one A-step.
-constexpr int FB_SCHED_BLOCK = 64;
+// windows j with e_j = d, then one A-step.  The lanes read the exponent's digits
+// coalesced (lane l: windows l, l + 64, ...), count them with LDS atomics, scan
+// the 2^w bins across the wave and scatter the window indices into the
+// instance's own schedule row.  Within one digit value the windows come in LDS
+// atomic order: B_d is a product of P_j, so any order gives the same residue
+// (fb_exp_kernel's result is reduced exactly).  Round 2 ran one thread per
+// instance (uncoalesced digit reads, 2-byte scatters over 64 rows per wave,
+// 32 KB of LDS per 64 instances): 3.8 ms on the n = 64 critical chain.
+constexpr int FB_SCHED_IPB = 4;   // instances (waves) per block
 constexpr int FB_MAX_W = 8;
-__global__ __launch_bounds__(FB_SCHED_BLOCK) void fb_sched_kernel(const FbSchedArgs a) {
-  __shared__ uint16_t cnt_lds[FB_SCHED_BLOCK * (1 << FB_MAX_W)];
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64 * FB_SCHED_IPB) void fb_sched_kernel(const FbSchedArgs a) {
+  __shared__ uint32_t cnt_lds[FB_SCHED_IPB][1 << FB_MAX_W];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.x * FB_SCHED_IPB + wv;   // wave-uniform
   if (i >= a.count) return;
+  // a short job at the head of the fixed-base chain: ahead of the long modexp waves
+  __builtin_amdgcn_s_setprio(3);
   const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[i]);
   const uint32_t elen = a.exp_len[i];
   const uint32_t h = a.h[i], w = a.w, nd = 1u << w, mask = nd - 1;
-  uint16_t* cnt = cnt_lds + threadIdx.x * (1 << FB_MAX_W);
+  uint32_t* cnt = cnt_lds[wv];
   auto digit = [&](uint32_t j) -> uint32_t {
     const uint32_t p = j * w, lo = p >> 5, sh = p & 31;
     const uint32_t v0 = (lo < elen) ? E[lo] : 0u;
     const uint32_t v1 = (lo + 1 < elen) ? E[lo + 1] : 0u;
     return (uint32_t)((((uint64_t)v1 << 32) | v0) >> sh) & mask;
   };
-  for (uint32_t d = 0; d < nd; ++d) cnt[d] = 0;
+  for (uint32_t d = lane; d < nd; d += 64) cnt[d] = 0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   uint32_t dmax = 0;
-  for (uint32_t j = 0; j < h; ++j) {
+  for (uint32_t j = lane; j < h; j += 64) {
     const uint32_t d = digit(j);
-    cnt[d] = (uint16_t)(cnt[d] + 1);
+    if (d) atomicAdd(&cnt[d], 1u);
     dmax = max(dmax, d);
   }
-  // start offset of digit d's windows: digits above d first, one A-step after each digit value
-  uint32_t pos = 0;
-  for (uint32_t d = dmax; d >= 1; --d) {
-    const uint32_t c = cnt[d];
-    cnt[d] = (uint16_t)pos;
-    pos += c + 1;
-  }
+  for (int off = 32; off > 0; off >>= 1) dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, off));
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // start of digit d's group: sum over d' in (d, dmax] of (cnt[d'] + 1), one A-step
+  // slot closing every group (empty ones too: A <- A * B once per digit value)
   uint16_t* S = a.sched + (size_t)i * a.stride;
-  for (uint32_t d = dmax; d >= 1; --d) {          // A-step slots (the position after each group)
-    const uint32_t end = (d > 1) ? cnt[d - 1] : pos;
-    S[end - 1] = FB_A_STEP;
-  }
-  for (uint32_t j = 0; j < h; ++j) {
-    const uint32_t d = digit(j);
-    if (d) {
-      S[cnt[d]] = (uint16_t)j;
-      cnt[d] = (uint16_t)(cnt[d] + 1);
+  uint32_t base = 0;
+  for (uint32_t top = dmax; top >= 1;) {   // 64 digit values per pass, descending
+    const uint32_t d = top >= lane ? top - lane : 0u;
+    const uint32_t c = d ? cnt[d] : 0u;
+    const uint32_t v = d ? c + 1 : 0u;
+    uint32_t incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= (uint32_t)off) incl += u;
     }
+    if (d) {
+      const uint32_t start = base + incl - v;
+      S[start + c] = FB_A_STEP;
+      cnt[d] = start;   // becomes the group's write cursor
+    }
+    base += (uint32_t)__shfl((int)incl, 63);
+    top = top > 64 ? top - 64 : 0u;
   }
-  a.nsteps[i] = pos;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t j = lane; j < h; j += 64) {
+    const uint32_t d = digit(j);
+    if (d) S[atomicAdd(&cnt[d], 1u)] = (uint16_t)j;
+  }
+  if (lane == 0) a.nsteps[i] = base;
 }
 
 template <int KD, int G, int K32>
@@ -288,7 +311,7 @@ hipError_t launch_fb_table(uint32_t k32, const FbTableArgs& a, hipStream_t st) {
 hipError_t launch_fb_sched(const FbSchedArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
   if (a.w > FB_MAX_W) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fb_sched_kernel, dim3((a.count + FB_SCHED_BLOCK - 1) / FB_SCHED_BLOCK), dim3(FB_SCHED_BLOCK), 0,
+  hipLaunchKernelGGL(fb_sched_kernel, dim3((a.count + FB_SCHED_IPB - 1) / FB_SCHED_IPB), dim3(64 * FB_SCHED_IPB), 0,
                      st, a);
   return hipGetLastError();
 }

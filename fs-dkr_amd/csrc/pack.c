@@ -10,6 +10,10 @@
  *   gather(objs, attr)        -> (handle, maxbits): holds a reference to getattr(o, attr)
  *                                (attr None: o itself) of every object, max bit length;
  *                                ValueError on a negative value, TypeError on a non-int
+ *   gather_rows(objs, attr, take) -> (handle, maxbits) of the first `take` items of every
+ *                                getattr(o, attr) sequence, flattened (the ring-Pedersen
+ *                                A / Z and sigma vectors without a Python list per call);
+ *                                IndexError when a sequence is shorter than `take`
  *   convert(jobs, threads)    -> jobs = [(handle, buffer, limbs), ...]: fills every
  *                                buffer[len][limbs] (uint32, little-endian) with the GIL
  *                                released, `threads` workers; OverflowError if a value
@@ -138,6 +142,86 @@ static Gathered* do_gather(PyObject* seq, PyObject* attr, size_t* best) {
   g->n = n;
   Py_DECREF(fast);
   return g;
+fail:
+  for (Py_ssize_t i = 0; i < g->n; ++i) Py_XDECREF(v[i]);
+  free(v);
+  free(g);
+  Py_DECREF(fast);
+  return NULL;
+}
+
+/* one value of a gather: owned reference stored in v[i], checked, bit length folded into *best */
+static int take_value(PyObject* x, PyObject** slot, size_t* best) {
+  *slot = x;
+  if (!PyLong_Check(x)) {
+    PyErr_SetString(PyExc_TypeError, "big integer field is not an int");
+    return -1;
+  }
+  if (Py_SIZE(x) < 0) {
+    PyErr_SetString(PyExc_ValueError, "negative big integer in a proof field");
+    return -1;
+  }
+  const size_t b = _PyLong_NumBits(x);
+  if (b == (size_t)-1 && PyErr_Occurred()) return -1;
+  if (b > *best) *best = b;
+  return 0;
+}
+
+static PyObject* py_gather_rows(PyObject* self, PyObject* args) {
+  PyObject *seq, *attr;
+  Py_ssize_t take;
+  if (!PyArg_ParseTuple(args, "OOn", &seq, &attr, &take)) return NULL;
+  if (take < 0) {
+    PyErr_SetString(PyExc_ValueError, "take < 0");
+    return NULL;
+  }
+  PyObject* fast = PySequence_Fast(seq, "objs must be a sequence");
+  if (!fast) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+  PyObject** items = PySequence_Fast_ITEMS(fast);
+  const size_t total = (size_t)n * (size_t)take;
+  Gathered* g = (Gathered*)calloc(1, sizeof(Gathered));
+  PyObject** v = (PyObject**)calloc(total ? total : 1, sizeof(PyObject*));
+  size_t best = 0;
+  if (!g || !v) {
+    free(g);
+    free(v);
+    Py_DECREF(fast);
+    return PyErr_NoMemory();
+  }
+  g->v = v;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* row = item_value(items[i], attr);
+    if (!row) goto fail;
+    PyObject* rf = PySequence_Fast(row, "row must be a sequence");
+    Py_DECREF(row);
+    if (!rf) goto fail;
+    if (PySequence_Fast_GET_SIZE(rf) < take) {
+      PyErr_Format(PyExc_IndexError, "row %zd holds %zd values, %zd needed", i, PySequence_Fast_GET_SIZE(rf), take);
+      Py_DECREF(rf);
+      goto fail;
+    }
+    PyObject** ri = PySequence_Fast_ITEMS(rf);
+    for (Py_ssize_t k = 0; k < take; ++k) {
+      PyObject* x = ri[k];
+      Py_INCREF(x);
+      g->n += 1;
+      if (take_value(x, &v[g->n - 1], &best)) {
+        Py_DECREF(rf);
+        goto fail;
+      }
+    }
+    Py_DECREF(rf);
+  }
+  Py_DECREF(fast);
+  PyObject* cap = PyCapsule_New(g, CAP, gathered_free);
+  if (!cap) {
+    for (Py_ssize_t i = 0; i < g->n; ++i) Py_XDECREF(g->v[i]);
+    free(g->v);
+    free(g);
+    return NULL;
+  }
+  return Py_BuildValue("(Nn)", cap, (Py_ssize_t)best);
 fail:
   for (Py_ssize_t i = 0; i < g->n; ++i) Py_XDECREF(v[i]);
   free(v);
@@ -378,6 +462,7 @@ out:
 
 static PyMethodDef methods[] = {
     {"gather", py_gather, METH_VARARGS, "(handle, maxbits) of getattr(o, attr) over objs"},
+    {"gather_rows", py_gather_rows, METH_VARARGS, "(handle, maxbits) of getattr(o, attr)[:take] over objs, flattened"},
     {"convert", py_convert, METH_VARARGS, "fill [(handle, buffer, limbs), ...] on `threads` workers"},
     {"points", py_points, METH_VARARGS, "affine points (or None) -> [len][16] uint32"},
     {"maxbits", py_maxbits, METH_VARARGS, "max bit length of getattr(o, attr) over objs"},

@@ -63,6 +63,17 @@ class RecoveredC(ctypes.Structure):
                 ("status", ctypes.c_int32)]
 
 
+def _struct_dtype(cls):
+    """numpy structured dtype with the exact layout of a ctypes Structure (pointers as u8)."""
+    names, formats, offsets = [], [], []
+    for name, typ in cls._fields_:
+        names.append(name)
+        formats.append(np.uint64 if ctypes.sizeof(typ) == 8 else np.uint32)
+        offsets.append(getattr(cls, name).offset)
+    return np.dtype({"names": names, "formats": formats, "offsets": offsets, "itemsize": ctypes.sizeof(cls)})
+
+
+_RECOVER_DT = _struct_dtype(RecoverJobC)
 RECOVER_OK, RECOVER_PANIC_LI, RECOVER_PANIC_DECRYPT = 0, 1, 2
 DRAW_BITS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                 ctypes.c_uint32)
@@ -463,24 +474,59 @@ class Context:
 
     def collect_recover_launch(self, jobs):
         """fsdkr_collect_recover_launch: the recovery's GPU work is enqueued and
-        runs while the caller goes on; returns the handle collect_recover_finish takes."""
+        runs while the caller goes on; returns the handle collect_recover_finish takes.
+        Every job's ciphertexts, keys, indices and points are packed into one array
+        per field (one conversion each, however many jobs; the rows of job k at
+        its offsets), and the fsdkr_recover_job rows are filled vectorised."""
         from . import _pack
-        keep, cj = [], (RecoverJobC * len(jobs))()
-        for k, j in enumerate(jobs):
-            nl, T = j["nl"], len(j["cts"])
-            tp = min(j["t_key"], j["t_vss"]) + 1
-            idx = np.ascontiguousarray(np.asarray(j["old_index"], dtype=np.uint32))
-            C = ints_to_limbs(j["cts"], 2 * nl)
-            Pp, Qq = ints_to_limbs([j["p"]], nl), ints_to_limbs([j["q"]], nl)
-            n_new = len(j["points"])
-            Pt = np.zeros((max(1, n_new * tp), 16), dtype=np.uint32)
-            if n_new:
-                _pack.points([pt for row in j["points"] for pt in row], None, Pt)
-            keep.append((idx, C, Pp, Qq, Pt))
-            cj[k] = RecoverJobC(nl, j["t_vss"], j["t_key"], n_new, _ptr(idx), _ptr(C), _ptr(Pp), _ptr(Qq), _ptr(Pt))
-            assert T == j["t_vss"] + 1
-        self.check(self._lib.fsdkr_collect_recover_launch(self._h, cj, len(jobs)))
-        return [len(j["points"]) for j in jobs]
+        J = len(jobs)
+        nls = np.array([j["nl"] for j in jobs], dtype=np.int64)
+        T = np.array([len(j["cts"]) for j in jobs], dtype=np.int64)
+        tp = np.array([min(j["t_key"], j["t_vss"]) + 1 for j in jobs], dtype=np.int64)
+        n_new = np.array([len(j["points"]) for j in jobs], dtype=np.int64)
+        for j, t in zip(jobs, T):
+            assert t == j["t_vss"] + 1
+        idx = np.ascontiguousarray(np.fromiter((i for j in jobs for i in j["old_index"]), dtype=np.uint32,
+                                               count=int(T.sum())))
+        Pt = np.zeros((max(1, int((n_new * tp).sum())), 16), dtype=np.uint32)
+        pts = [pt for j in jobs for row in j["points"] for pt in row]
+        if pts:
+            _pack.points(pts, None, Pt)
+        if J and (nls != nls[0]).any():   # rows at each job's own width
+            C2, PQ2 = [], []
+            for k, j in enumerate(jobs):
+                C2.append(ints_to_limbs(j["cts"], 2 * j["nl"]))
+                PQ2.append(ints_to_limbs([j["p"], j["q"]], j["nl"]))
+            c_ptr = np.array([a.ctypes.data for a in C2], dtype=np.uint64)
+            p_ptr = np.array([a.ctypes.data for a in PQ2], dtype=np.uint64)
+            q_ptr = p_ptr + (nls * 4).astype(np.uint64)
+            keep = (C2, PQ2)
+        else:   # one width: one array per field
+            W = int(nls[0]) if J else 1
+            C = ints_to_limbs([c for j in jobs for c in j["cts"]], 2 * W)
+            PQ = ints_to_limbs([v for j in jobs for v in (j["p"], j["q"])], W)
+
+            def starts(c):
+                return np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.uint64)
+            c_ptr = np.uint64(C.ctypes.data) + starts(T) * np.uint64(2 * W * 4)
+            p_ptr = np.uint64(PQ.ctypes.data) + np.arange(J, dtype=np.uint64) * np.uint64(2 * W * 4)
+            q_ptr = p_ptr + np.uint64(W * 4)
+            keep = (C, PQ)
+        rows = np.zeros(J, dtype=_RECOVER_DT)
+        rows["nl"] = nls
+        rows["t_vss"] = [j["t_vss"] for j in jobs]
+        rows["t_key"] = [j["t_key"] for j in jobs]
+        rows["n_new"] = n_new
+        off = np.concatenate([[0], np.cumsum(T)[:-1]]).astype(np.uint64)
+        rows["old_index"] = np.uint64(idx.ctypes.data) + off * np.uint64(4)
+        rows["cts"], rows["p"], rows["q"] = c_ptr, p_ptr, q_ptr
+        poff = np.concatenate([[0], np.cumsum(n_new * tp)[:-1]]).astype(np.uint64)
+        rows["points"] = np.uint64(Pt.ctypes.data) + poff * np.uint64(64)
+        # the launch reads every host array before it returns (keep, idx, Pt, rows live until then)
+        self.check(self._lib.fsdkr_collect_recover_launch(
+            self._h, ctypes.cast(rows.ctypes.data, ctypes.POINTER(RecoverJobC)), J))
+        del keep
+        return [int(x) for x in n_new]
 
     def collect_recover_finish(self, handle):
         n_new = handle

@@ -19,6 +19,8 @@ the representable set (UnsupportedInput): negative BigInts and values wider
 than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
 import ctypes
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -90,18 +92,70 @@ def pack_points(points, attr=None):
     return arr
 
 
-class _Gather:
-    """Every big-integer field of one batch: gathered once (max bit lengths for the
-    slot widths), converted together on host_threads() workers."""
+class _HostPool:
+    """Recycled host arrays for the large SoA slots of a SessionSet.  A configs[4]
+    step converts ~0.6 GB of 3072-bit values; writing them into fresh arrays pays
+    a first-touch page fault per 4 KiB, a quarter of the conversion on the GPU
+    box (31 -> 23 ms, profiles/r03z_pack_host_only.jsonl).  A set's arrays return
+    when the set is collected (weakref.finalize), keyed by exact shape, so the
+    next call of the same shape reuses them; at most CAP_BYTES are kept."""
+    MIN_BYTES = 1 << 20
+    CAP_BYTES = 4 << 30
 
     def __init__(self):
+        self._free = {}
+        self._bytes = 0
+        self._lock = threading.Lock()
+
+    def empty(self, shape):
+        shape = tuple(int(x) for x in shape)
+        nbytes = int(np.prod(shape)) * 4
+        if nbytes >= self.MIN_BYTES:
+            with self._lock:
+                lst = self._free.get(shape)
+                if lst:
+                    self._bytes -= nbytes
+                    return lst.pop()
+        return np.empty(shape, dtype=np.uint32)
+
+    def give(self, arrays):
+        with self._lock:
+            for a in arrays:
+                if a.dtype == np.uint32 and a.nbytes >= self.MIN_BYTES and a.flags.owndata and \
+                        self._bytes + a.nbytes <= self.CAP_BYTES:
+                    self._free.setdefault(a.shape, []).append(a)
+                    self._bytes += a.nbytes
+
+
+_POOL = _HostPool()
+
+
+class _Gather:
+    """Every big-integer field of one batch: gathered once (max bit lengths for the
+    slot widths), converted together on host_threads() workers.  With `owned`
+    (a list), the slots come from _POOL and are recorded there for its return."""
+
+    def __init__(self, owned=None):
         self.jobs = []
+        self.owned = owned
 
     def field(self, objs, attr=None):
         return _gather(objs, attr) + (len(objs),)
 
+    def rows(self, objs, attr, take):
+        """the first `take` values of every getattr(o, attr), flattened"""
+        try:
+            h, bits = _pack.gather_rows(objs, attr, take)
+        except ValueError as e:
+            raise UnsupportedInput(str(e)) from None
+        return h, bits, len(objs) * take
+
     def slot(self, f, limbs):
-        arr = np.empty((f[2], limbs), dtype=np.uint32)
+        if self.owned is None:
+            arr = np.empty((f[2], limbs), dtype=np.uint32)
+        else:
+            arr = _POOL.empty((f[2], limbs))
+            self.owned.append(arr)
         self.jobs.append((f[0], arr, limbs))
         return arr
 
@@ -397,6 +451,8 @@ class SessionSet:
         self.J = np.array([len(sessions[s][2]) for s in range(S)], dtype=np.int64)
         self.n = self.R + self.J
         self._keep = []
+        self._owned = []   # pooled slot arrays, back to _POOL when the set is collected
+        weakref.finalize(self, _POOL.give, self._owned)
         self.structs = np.zeros(len(self.live), dtype=_BATCH_DT)
         self.row = {s: r for r, s in enumerate(self.live)}
         self._pre, self.n_prestart = None, 0
@@ -435,7 +491,7 @@ class SessionSet:
         n = R + np.array([len(j) for m, lk, j in ses], dtype=np.int64)
         if any(len(lk.paillier_key_vec) < nn for (m, lk, j), nn in zip(ses, n)):
             return
-        G = _Gather()
+        G = _Gather(self._owned)
         f_rn = G.field([k for (ms, lk, js), nn in zip(ses, n) for k in lk.paillier_key_vec[:nn]], "n")
         f_s2 = G.field([m.pdl_proof_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s2")
         f_s = G.field([m.range_proofs[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s")
@@ -483,7 +539,7 @@ class SessionSet:
         return arr.ctypes.data
 
     def _pack_regular(self, sessions, reg, M, key_bits):
-        G = _Gather()
+        G = _Gather(self._owned)
         ses = [sessions[s] for s in reg]
         R = np.array([len(m) for m, lk, j in ses], dtype=np.int64)
         J = np.array([len(j) for m, lk, j in ses], dtype=np.int64)
@@ -509,10 +565,12 @@ class SessionSet:
             F["rp_" + a] = G.field(rng, a)
         for a in ("S", "T", "N"):
             F["ped_" + a] = G.field([m.ring_pedersen_statement for m in am], a)
-        F["ped_A"] = G.field([v for m in am for v in m.ring_pedersen_proof.A[:M]])
-        F["ped_Z"] = G.field([v for m in am for v in m.ring_pedersen_proof.Z[:M]])
+        # regular sessions hold full-length vectors (_regular): flattened in C
+        rpp = [m.ring_pedersen_proof for m in am]
+        F["ped_A"] = G.rows(rpp, "A", M)
+        F["ped_Z"] = G.rows(rpp, "Z", M)
         f_ckn = G.field([m.ek.n for m in am])
-        f_sig = G.field([v for m in am for v in m.dk_correctness_proof.sigma_vec[:M2]])
+        f_sig = G.rows([m.dk_correctness_proof for m in am], "sigma_vec", M2)
         if joins:
             for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
                 F["dlog_" + name] = G.field([j.dlog_statement for j in joins], attr)

@@ -56,3 +56,25 @@ def test_fixed_base_large_batch(gpu_ctx):
     out = gpu_ctx.fixed_base_modexp(bases, list(range(16)), mods, bidx, exps, 64)
     for k in range(0, len(exps), 97):
         assert out[k] == pow(bases[bidx[k]], exps[k], mods[bidx[k]])
+
+
+@pytest.mark.parametrize("top_bits", [3, 40, 256, 8200])
+def test_fixed_base_window_widths(gpu_ctx, top_bits):
+    """Every window width of fb_window (w = 1 .. 8 by the largest exponent): the
+    schedule's 2^w digit bins span one to four 64-lane scan passes of fb_sched."""
+    rnd = random.Random(top_bits)
+    mods = [rnd.getrandbits(2048) | 1 | (1 << 2047) for _ in range(2)]
+    bases = [rnd.getrandbits(2048) % mods[k % 2] for k in range(3)]
+    bidx, exps = [], []
+    for k in range(96):
+        b = k % 3
+        bits = [0, 1, top_bits // 2, top_bits][k % 4]
+        e = rnd.getrandbits(bits) if bits > 1 else bits
+        if k % 7 == 3:
+            e = (1 << top_bits) - 1                         # every digit at its maximum
+        bidx.append(b)
+        exps.append(e)
+    out = gpu_ctx.fixed_base_modexp(bases, [0, 1, 0], mods, bidx, exps, 64)
+    want = [pow(bases[b], e, mods[[0, 1, 0][b]]) for b, e in zip(bidx, exps)]
+    bad = [k for k in range(len(want)) if out[k] != want[k]]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"

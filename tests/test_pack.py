@@ -189,3 +189,44 @@ def test_session_set_equals_per_session_batches():
             assert getattr(one.c, f) == getattr(row.c, f), (s, f)
         pi = np.ctypeslib.as_array(row.c.party_index, shape=(one.R + one.J,))
         assert list(pi) == [m.party_index for m in sessions[s][0]] + [j.party_index or 0 for j in sessions[s][2]]
+
+
+def test_gather_rows_flattens_prefixes():
+    """_pack.gather_rows(objs, attr, take) == gather of [v for o in objs for v in getattr(o, attr)[:take]]."""
+    rnd = random.Random(5)
+    objs = [NS(A=tuple(rnd.getrandbits(rnd.randint(1, 3072)) for _ in range(9))) for _ in range(40)]
+    G = _Gather()
+    f_rows = G.rows(objs, "A", 7)
+    flat = [v for o in objs for v in o.A[:7]]
+    assert f_rows[1] == max(v.bit_length() for v in flat) and f_rows[2] == len(flat)
+    a = G.slot(f_rows, 96)
+    G.run()
+    assert np.array_equal(a, _expect(flat, 96))
+    with pytest.raises(IndexError):
+        _pack.gather_rows(objs, "A", 10)          # a row shorter than `take`
+    with pytest.raises(UnsupportedInput):
+        _Gather().rows([NS(A=(1, -2))], "A", 2)   # negative value
+    with pytest.raises(TypeError):
+        _pack.gather_rows([NS(A=(1, 2.0))], "A", 2)
+
+
+def test_session_set_pool_reuse():
+    """A collected SessionSet's large slot arrays are reused by the next set of
+    the same shape, and the packed contents do not depend on the recycling."""
+    import gc
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from pack_many_cpu import fake_sessions
+    from fsdkr.batch import SessionSet, _POOL
+    sess = fake_sessions(24, seed=3)
+    first = SessionSet(sess, 256, 3072)
+    snap = {k: np.array(v, copy=True) for k, v in enumerate(first._owned)}
+    ids = {id(a) for a in first._owned if a.nbytes >= _POOL.MIN_BYTES}
+    assert ids, "the fake sessions must produce pooled slots"
+    del first
+    gc.collect()
+    second = SessionSet(sess, 256, 3072)
+    assert ids & {id(a) for a in second._owned}
+    for k, a in enumerate(second._owned):
+        assert np.array_equal(a, snap[k])

@@ -51,16 +51,35 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sessions", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--split", action="store_true", help="time gather / convert / points separately")
     a = ap.parse_args()
     sess = fake_sessions(a.sessions)
+    acc = {}
+    if a.split:
+        from fsdkr import batch as B
+
+        def wrap(name):
+            f = getattr(B, name)
+
+            def g(*x, **k):
+                t = time.perf_counter()
+                r = f(*x, **k)
+                acc[name] = acc.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+                return r
+            setattr(B, name, g)
+        for name in ("_gather", "_convert", "pack_points"):
+            wrap(name)
     for _ in range(a.reps):
+        acc.clear()
         t0 = time.perf_counter()
         sset = SessionSet(sess, 256, 3072, staged=True)
         t1 = time.perf_counter()
         sset.complete()
         t2 = time.perf_counter()
-        print(json.dumps({"sessions": a.sessions, "stage1_ms": (t1 - t0) * 1e3, "stage2_ms": (t2 - t1) * 1e3}),
-              flush=True)
+        out = {"sessions": a.sessions, "stage1_ms": (t1 - t0) * 1e3, "stage2_ms": (t2 - t1) * 1e3}
+        out.update({k.strip("_") + "_ms": v for k, v in acc.items()})
+        print(json.dumps(out), flush=True)
+        del sset
 
 
 if __name__ == "__main__":
