@@ -56,6 +56,12 @@ inline const std::vector<uint32_t>& small_primes() {
   return ps;
 }
 
+// the primorial check of the correct-key proof over keys of up to 192 limbs
+inline const hbn::SmallFactorSieve& small_factor_sieve() {
+  static const hbn::SmallFactorSieve sv(small_primes(), 192);
+  return sv;
+}
+
 // q^3 (the Alice s1 bound, range_proofs.rs:125) as limbs
 inline const hbn::Limbs& q_cubed() {
   static hbn::Limbs q3 = [] {

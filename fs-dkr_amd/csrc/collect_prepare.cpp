@@ -215,7 +215,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       ck_bits[m] = hbn::bitlen(ckn, x.ckl);
       if (ck_bits[m] == 0) pl.ck_short[m] = 1;                  // rho = mask % 0: division by zero panics
       const bool one = ck_bits[m] == 1;                          // n = 1: every value is 0 mod 1 -> Ok
-      const bool ok = !one && ck_bits[m] != 0 && is_odd(ckn) && !hbn::has_small_factor(ckn, x.ckl, small_primes());
+      const bool ok = !one && ck_bits[m] != 0 && is_odd(ckn) && !small_factor_sieve().divides(ckn, x.ckl);
       if (one) pl.ck_one[m] = 1;
       if (ok) {
         const uint32_t msklen = ck_bits[m] / 256 + 1;

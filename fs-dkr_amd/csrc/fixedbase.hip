@@ -128,14 +128,19 @@ __global__ __launch_bounds__(64) void fb_table_wave_kernel(const FbTableArgs a) 
 
 // One wave64 per instance: the BGMW product schedule of its exponent, by a
 // counting sort of its w-bit digits (O(h + 2^w)): for d = max digit .. 1 the
-// windows j with e_j = d, then one A-step.  The lanes read the exponent's digits
-// coalesced (lane l: windows l, l + 64, ...), count them with LDS atomics, scan
-// the 2^w bins across the wave and scatter the window indices into the
-// instance's own schedule row.  Within one digit value the windows come in LDS
-// atomic order: B_d is a product of P_j, so any order gives the same residue
-// (fb_exp_kernel's result is reduced exactly).  Round 2 ran one thread per
-// instance (uncoalesced digit reads, 2-byte scatters over 64 rows per wave,
-// 32 KB of LDS per 64 instances): 3.8 ms on the n = 64 critical chain.
+// windows j with e_j = d in ascending j, then one A-step.  The lanes read the
+// exponent's digits coalesced (lane l: windows l, l + 64, ...) and count them
+// with LDS atomics; the 2^w bins are scanned across the wave; then one uniform
+// pass over the windows (scalar digit reads) appends window j to its digit's
+// group, the lane owning bin d holding that group's cursor in a register, so
+// every group lists its windows in ascending order.  That order matters to
+// fb_exp_kernel: the 16 instances of a wave then walk their base's table
+// roughly in step (L2 locality); an atomic-order scatter left the results
+// unchanged but made the n = 64 fixed-base launch ~8 ms slower
+// (profiles/r03za_ab_fbsched_n64.jsonl).  Round 2 ran one thread per instance
+// (uncoalesced digit reads, 2-byte scatters over 64 rows per wave, 32 KB of LDS
+// per 64 instances): 3.8 ms on the n = 64 critical chain and ~110 ms ahead of
+// the configs[4] fixed-base exponents.
 constexpr int FB_SCHED_IPB = 4;   // instances (waves) per block
 constexpr int FB_MAX_W = 8;
 __global__ __launch_bounds__(64 * FB_SCHED_IPB) void fb_sched_kernel(const FbSchedArgs a) {
@@ -190,9 +195,28 @@ __global__ __launch_bounds__(64 * FB_SCHED_IPB) void fb_sched_kernel(const FbSch
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t j = lane; j < h; j += 64) {
-    const uint32_t d = digit(j);
-    if (d) S[atomicAdd(&cnt[d], 1u)] = (uint16_t)j;
+  // ordered scatter: lane l owns bins l, l + 64, l + 128, l + 192
+  uint32_t cur[(1 << FB_MAX_W) / 64];
+#pragma unroll
+  for (int k = 0; k < (1 << FB_MAX_W) / 64; ++k) {
+    const uint32_t d = lane + 64u * k;
+    cur[k] = d < nd ? cnt[d] : 0u;
+  }
+  const uint32_t* Es = reinterpret_cast<const uint32_t*>(
+      ((uint64_t)__builtin_amdgcn_readfirstlane((int)(a.exp_ptr[i] >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a.exp_ptr[i]));
+  const uint32_t hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)h);
+  const uint32_t els = (uint32_t)__builtin_amdgcn_readfirstlane((int)elen);
+  for (uint32_t j = 0; j < hs; ++j) {   // wave-uniform loop and digit
+    const uint32_t p = j * w, lo = p >> 5, sh = p & 31;
+    const uint32_t v0 = (lo < els) ? Es[lo] : 0u;
+    const uint32_t v1 = (lo + 1 < els) ? Es[lo + 1] : 0u;
+    const uint32_t d = (uint32_t)((((uint64_t)v1 << 32) | v0) >> sh) & mask;
+    if (d && (d & 63u) == lane) {
+#pragma unroll
+      for (int k = 0; k < (1 << FB_MAX_W) / 64; ++k)
+        if ((d >> 6) == (uint32_t)k) S[cur[k]++] = (uint16_t)j;
+    }
   }
   if (lane == 0) a.nsteps[i] = base;
 }

@@ -326,5 +326,58 @@ inline bool has_small_factor(const uint32_t* a, size_t n, const std::vector<uint
   return false;
 }
 
+// Trial division by a fixed prime list, several primes per pass: a mod M for
+// M = p_1 ... p_k < 2^63 (k <= 4) as sum_j a_j (2^(32 j) mod M), independent
+// 64 x 64 -> 128-bit products and one 128-bit reduction per M, then r mod p_i.
+// Same answer as has_small_factor (2 primes per pass, a dependent 64-bit
+// division per limb), ~10x fewer cycles: the correct-key primorial check of
+// 3 072 keys was most of prepare's 29 ms "ck" phase at configs[4].
+class SmallFactorSieve {
+ public:
+  SmallFactorSieve(const std::vector<uint32_t>& primes, size_t max_limbs) : L_(max_limbs) {
+    for (size_t i = 0; i < primes.size();) {
+      Group g;
+      while (i < primes.size() && g.np < 4 && (unsigned __int128)g.m * primes[i] < ((unsigned __int128)1 << 63)) {
+        g.m *= primes[i];
+        g.p[g.np++] = primes[i++];
+      }
+      groups_.push_back(g);
+    }
+    pw_.resize(groups_.size() * L_);
+    for (size_t gi = 0; gi < groups_.size(); ++gi) {
+      const uint64_t m = groups_[gi].m;
+      uint64_t v = 1 % m;
+      for (size_t k = 0; k < L_; ++k) {
+        pw_[gi * L_ + k] = v;
+        v = (uint64_t)(((unsigned __int128)v << 32) % m);
+      }
+    }
+  }
+  size_t max_limbs() const { return L_; }
+  // does a prime of the list divide a (n <= max_limbs limbs; a = 0: yes)?
+  bool divides(const uint32_t* a, size_t n) const {
+    for (size_t gi = 0; gi < groups_.size(); ++gi) {
+      const Group& g = groups_[gi];
+      const uint64_t* pw = pw_.data() + gi * L_;
+      unsigned __int128 acc = 0;
+      for (size_t k = 0; k < n; ++k) acc += (unsigned __int128)a[k] * pw[k];
+      const uint64_t r = (uint64_t)(acc % g.m);
+      for (uint32_t t = 0; t < g.np; ++t)
+        if (r % g.p[t] == 0) return true;
+    }
+    return false;
+  }
+
+ private:
+  struct Group {
+    uint64_t m = 1;
+    uint32_t p[4] = {0, 0, 0, 0};
+    uint32_t np = 0;
+  };
+  size_t L_;
+  std::vector<Group> groups_;
+  std::vector<uint64_t> pw_;
+};
+
 }  // namespace hbn
 }  // namespace fsdkr

@@ -74,6 +74,9 @@ def _struct_dtype(cls):
 
 
 _RECOVER_DT = _struct_dtype(RecoverJobC)
+_RECOVERED_DT = np.dtype({"names": ["pk_vec", "status"], "formats": [np.uint64, np.int32],
+                          "offsets": [RecoveredC.pk_vec.offset, RecoveredC.status.offset],
+                          "itemsize": ctypes.sizeof(RecoveredC)})
 RECOVER_OK, RECOVER_PANIC_LI, RECOVER_PANIC_DECRYPT = 0, 1, 2
 DRAW_BITS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                 ctypes.c_uint32)
@@ -529,25 +532,33 @@ class Context:
         return [int(x) for x in n_new]
 
     def collect_recover_finish(self, handle):
-        n_new = handle
-        outs = (RecoveredC * len(n_new))()
-        pks = []
-        for k, n in enumerate(n_new):
-            PK = np.zeros((max(1, n), 16), dtype=np.uint32)
-            pks.append(PK)
-            outs[k].pk_vec = _ptr(PK)
+        """Waits for the launched recovery; per job (status, share, y, pk_vec).
+        Every job's pk_vec rows land in one array (job k's at its offset) and the
+        results are converted in one pass each (no per-job allocations)."""
+        n_new = np.asarray(handle, dtype=np.int64)
+        J = len(n_new)
+        outs = (RecoveredC * J)()
+        PK = np.zeros((max(1, int(n_new.sum())), 16), dtype=np.uint32)
+        rows = np.frombuffer(outs, dtype=_RECOVERED_DT, count=J) if J else None
+        if J:
+            off = np.concatenate([[0], np.cumsum(n_new)[:-1]]).astype(np.uint64)
+            rows["pk_vec"] = np.uint64(PK.ctypes.data) + off * np.uint64(64)
         self.check(self._lib.fsdkr_collect_recover_finish(self._h, outs))
+        if not J:
+            return []
 
         def point(v):
-            x, y = v & ((1 << 256) - 1), v >> 256
-            return None if (x == 0 and y == 0) else (x, y)
-        res = []
-        for k, n in enumerate(n_new):
-            o = outs[k]
-            share = int.from_bytes(bytes(o.share), "little")
-            y = point(int.from_bytes(bytes(o.y), "little"))
-            pk = [point(v) for v in limbs_to_ints(pks[k][:n])] if n else []
-            res.append((int(o.status), share, y, pk))
+            return None if v == 0 else (v & ((1 << 256) - 1), v >> 256)
+        raw = np.frombuffer(outs, dtype=np.uint8).reshape(J, ctypes.sizeof(RecoveredC))
+        o_sh, o_y = RecoveredC.share.offset, RecoveredC.y.offset
+        shares = limbs_to_ints(raw[:, o_sh:o_sh + 32].copy().view(np.uint32))
+        ys = [point(v) for v in limbs_to_ints(raw[:, o_y:o_y + 64].copy().view(np.uint32))]
+        pks = [point(v) for v in limbs_to_ints(PK[:int(n_new.sum())])] if n_new.sum() else []
+        res, at = [], 0
+        for k in range(J):
+            n = int(n_new[k])
+            res.append((int(rows["status"][k]), shares[k], ys[k], pks[at:at + n]))
+            at += n
         return res
 
     def ec_msm(self, points, scalars):
