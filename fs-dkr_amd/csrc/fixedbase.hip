@@ -133,14 +133,11 @@ __global__ __launch_bounds__(64) void fb_table_wave_kernel(const FbTableArgs a) 
 // with LDS atomics; the 2^w bins are scanned across the wave; then one uniform
 // pass over the windows (scalar digit reads) appends window j to its digit's
 // group, the lane owning bin d holding that group's cursor in a register, so
-// every group lists its windows in ascending order.  That order matters to
-// fb_exp_kernel: the 16 instances of a wave then walk their base's table
-// roughly in step (L2 locality); an atomic-order scatter left the results
-// unchanged but made the n = 64 fixed-base launch ~8 ms slower
-// (profiles/r03za_ab_fbsched_n64.jsonl).  Round 2 ran one thread per instance
-// (uncoalesced digit reads, 2-byte scatters over 64 rows per wave, 32 KB of LDS
-// per 64 instances): 3.8 ms on the n = 64 critical chain and ~110 ms ahead of
-// the configs[4] fixed-base exponents.
+// every group lists its windows in ascending order (a deterministic schedule;
+// an LDS-atomic scatter gives the same residues in any order).  Round 2
+// ran one thread per instance (uncoalesced digit reads, 2-byte scatters over
+// 64 rows per wave, 32 KB of LDS per 64 instances): ~110 ms ahead of the
+// configs[4] fixed-base exponents.
 constexpr int FB_SCHED_IPB = 4;   // instances (waves) per block
 constexpr int FB_MAX_W = 8;
 __global__ __launch_bounds__(64 * FB_SCHED_IPB) void fb_sched_kernel(const FbSchedArgs a) {
@@ -148,8 +145,10 @@ __global__ __launch_bounds__(64 * FB_SCHED_IPB) void fb_sched_kernel(const FbSch
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t i = blockIdx.x * FB_SCHED_IPB + wv;   // wave-uniform
   if (i >= a.count) return;
-  // a short job at the head of the fixed-base chain: ahead of the long modexp waves
-  __builtin_amdgcn_s_setprio(3);
+  // no issue-priority raise: at s_setprio 3 this kernel ended in 0.9 ms, the
+  // n = 64 fixed-base exponents then started ~8 ms earlier beside the prestarted
+  // GA chains, and GA's last chain ended 14 ms later (whole call 53 -> 61 ms,
+  // profiles/r03zc_*); at the default priority it runs beside GA in ~7 ms
   const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[i]);
   const uint32_t elen = a.exp_len[i];
   const uint32_t h = a.h[i], w = a.w, nd = 1u << w, mask = nd - 1;
