@@ -24,6 +24,7 @@ void free_ga_pre(Ctx* c) {
   if (g && g->done) (void)hipEventDestroy(g->done);
   if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
+  if (g && g->ck_done) (void)hipEventDestroy(g->ck_done);
   delete g;
   c->ga_pre = nullptr;
 }

@@ -288,6 +288,10 @@ struct CollectPlan {
   // h1 / h2 fixed-base tables built by fsdkr_collect_prestart (fb_hit)
   bool fb_hit = false;
   FbPre fb_pre;
+  // correct-key sigma^n mod n computed by fsdkr_collect_prestart_multi (ck_hit):
+  // the correct-key equalities read them once ck_done has fired
+  bool ck_hit = false;
+  hipEvent_t ck_done = nullptr;
   FbJob fb;
   size_t d_FB = 0;
   uint32_t* fb_table = nullptr;
@@ -322,6 +326,13 @@ struct GaPre {
   uint32_t Mt = 0, fb_w = 0, bits_h1 = 0, bits_h2 = 0, bits_z = 0, fb_entries = 0;
   uint32_t* fb_table = nullptr;
   hipEvent_t fb_done = nullptr;     // every table built
+  // correct-key sigma_k^n mod n of every message (prepare's GC job), when stage 1
+  // packed ck_n and ck_sigma: rows at width ck_l, in prepare's message order
+  bool ck_valid = false;
+  uint32_t ck_l = 0, ck_bits = 0, ck_Mt = 0;
+  std::vector<uint32_t> ck_n, ck_sigma;   // the inputs (zero-extended to ck_l), for the match
+  uint32_t* ck_out = nullptr;             // [Mt * 11][ck_l]
+  hipEvent_t ck_done = nullptr;
 };
 
 // collect()'s fixed-base tables, base order [h1_i | T_m | h2_i] (FbJob::finalize

@@ -144,6 +144,7 @@ int collect_launch_impl(Ctx* c) {
     if ((rc = launch_group(1, ss, prio[2], 0, cons_nl)) || (rc = join_later(ss))) return rc;
     ss = c->side_stream(9);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
+    if (pl.ck_hit) (void)hipStreamWaitEvent(ss, pl.ck_done, 0);   // the prestarted sigma^n rows
     if ((rc = launch_group(4, ss, prio[2], 0, cons_ck))) return rc;
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqck), PI(pl.d_eqckm), cons_ck, PX(pl.x_pbits), DI(pl.o_one),
                   PX(pl.x_eqck), pl.n_eq_ck};

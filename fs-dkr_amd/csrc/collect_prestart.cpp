@@ -142,6 +142,94 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
 }
 
 
+// The correct-key job GC of a multi-session batch (zk-paillier NiCorrectKeyProof:
+// sigma_k^n mod n, k < 11, per message), when stage 1 packed ck_n and ck_sigma:
+// it needs nothing else, so it fills the chip beside GA's last chains while the
+// caller packs and prepares the rest.  Moduli that are not odd and > 1 get the
+// placeholder 3 and no exponent (prepare's verdict for them never reads GC);
+// smooth ones run with their own modulus (their verdict is false either way).
+static int prestart_ck(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, GaPre& g) {
+  if (g.sess.size() != count) return FSDKR_OK;
+  uint32_t ckl = 0, Mt = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (!b->ck_n || !b->ck_sigma || !b->ckl || !shape_digits(b->ckl) || b->ck_lens) return FSDKR_OK;
+    ckl = std::max(ckl, b->ckl);
+    Mt += b->n_refresh + b->n_join;
+  }
+  if (Mt == 0) return FSDKR_OK;
+  g.ck_n.assign((size_t)Mt * ckl, 0u);
+  g.ck_sigma.assign((size_t)Mt * CK_M2 * ckl, 0u);
+  for (uint32_t k = 0, mb = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const uint32_t mt = b->n_refresh + b->n_join;
+    for (uint32_t m = 0; m < mt; ++m) {
+      memcpy(g.ck_n.data() + (size_t)(mb + m) * ckl, b->ck_n + (size_t)m * b->ckl, (size_t)b->ckl * 4);
+      for (uint32_t j = 0; j < CK_M2; ++j)
+        memcpy(g.ck_sigma.data() + ((size_t)(mb + m) * CK_M2 + j) * ckl, b->ck_sigma + ((size_t)m * CK_M2 + j) * b->ckl,
+               (size_t)b->ckl * 4);
+    }
+    mb += mt;
+  }
+  auto al = Img::al;
+  const size_t o_mod = 0, o_sig = al((size_t)Mt * ckl * 4), o_desc = o_sig + al((size_t)Mt * CK_M2 * ckl * 4);
+  const size_t count_i = (size_t)Mt * CK_M2, o_out = o_desc + al(count_i * 32);
+  const size_t total = o_out + count_i * ckl * 4;
+  uint8_t* dev = (uint8_t*)c->buf("collect_ck_pre", total);
+  if (!dev) {
+    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
+    return FSDKR_E_OOM;
+  }
+  std::vector<uint8_t> img(o_out, 0);
+  uint32_t* mods = reinterpret_cast<uint32_t*>(img.data() + o_mod);
+  memcpy(img.data() + o_sig, g.ck_sigma.data(), g.ck_sigma.size() * 4);
+  std::vector<uint32_t> ebits(Mt, 0u);
+  uint32_t bits = 1;
+  for (uint32_t m = 0; m < Mt; ++m) {
+    const uint32_t* n = g.ck_n.data() + (size_t)m * ckl;
+    uint32_t* dst = mods + (size_t)m * ckl;
+    const uint32_t nb = hbn::bitlen(n, ckl);
+    if (nb > 1 && is_odd(n)) {
+      memcpy(dst, n, (size_t)ckl * 4);
+      ebits[m] = nb;
+      bits = std::max(bits, nb);
+    } else {
+      dst[0] = 3;
+    }
+  }
+  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
+  ModexpJob GC;
+  GC.k32 = ckl;
+  for (uint32_t m = 0; m < Mt; ++m)
+    for (uint32_t j = 0; j < CK_M2; ++j)   // prepare's GC order: base sigma, exponent n, modulus m
+      GC.add(DI(o_sig + ((size_t)m * CK_M2 + j) * ckl * 4), ckl, DI(o_mod + (size_t)m * ckl * 4), ckl, ebits[m], m);
+  GC.exp_bits = bits;
+  std::vector<uint8_t> desc;
+  GC.pack(desc);
+  memcpy(img.data() + o_desc, desc.data(), desc.size());
+  hipStream_t cs = c->side_stream(9);   // launch()'s correct-key stream
+  StreamScope scope(c, cs);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, cs), "prestart ck H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(cs), "prestart ck H2D sync")))   // img is pageable and local
+    return rc;
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, ckl, reinterpret_cast<const uint32_t*>(dev + o_mod), Mt, &cons, "collect_ckpre")))
+    return rc;
+  g.ck_out = reinterpret_cast<uint32_t*>(dev + o_out);
+  if ((rc = launch_modexp_desc(c, ckl, (uint32_t)count_i, bits, dev + o_desc, cons, g.ck_out, cs, "mxt_GCpre", 2, 0)))
+    return rc;
+  if (!g.ck_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.ck_done, hipEventDisableTiming), "event")))
+    return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.ck_done, cs), "event record"))) return rc;
+  g.ck_l = ckl;
+  g.ck_bits = bits;
+  g.ck_Mt = Mt;
+  g.ck_valid = true;
+  return FSDKR_OK;
+}
+
+
 // GA prestart of `count` sessions (one: fsdkr_collect_prestart; many:
 // fsdkr_collect_prestart_multi), in prepare's global order: session s's
 // receivers and pairs after session s-1's, every row at the widest nl.
@@ -150,6 +238,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
   g.valid = false;
   g.fb_valid = false;
+  g.ck_valid = false;
   *n_out = *P_out = 0;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
   if (running && running->launched) {
@@ -159,7 +248,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // a prepared plan that consumed the previous prestart reads its s^N rows and
   // fixed-base tables in place: this prestart overwrites (or reallocates) those
   // buffers, so the plan is dropped (a later launch reports "no prepared batch")
-  if (running && (running->ga_hit || running->fb_hit)) free_collect_plan(c);
+  if (running && (running->ga_hit || running->fb_hit || running->ck_hit)) free_collect_plan(c);
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prestart: no batch");
     return FSDKR_E_ARG;
@@ -292,7 +381,9 @@ int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count)
   uint32_t n = 0, P = 0;
   int rc = prestart_ga(c, bs, count, &n, &P);
   if (rc || P == 0) return rc;
-  return prestart_fb_tables(c, bs, count, *reinterpret_cast<GaPre*>(c->ga_pre), n, P);
+  GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
+  if ((rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
+  return prestart_ck(c, bs, count, g);
 }
 
 // does the prestarted GA belong to these sessions (same shapes, same inputs)?

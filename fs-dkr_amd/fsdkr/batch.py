@@ -482,8 +482,8 @@ class SessionSet:
 
     def _stage1(self, sessions, reg, M):
         """The fields fsdkr_collect_prestart_multi reads: the GA chains' (receivers'
-        N, PDL s2, range-proof s) and the fixed-base tables' bases (receivers' N~,
-        h1, h2; ring-Pedersen T and N).  The exponents stay in stage 2: the tables
+        N, PDL s2, range-proof s), the fixed-base tables' bases (receivers' N~,
+        h1, h2; ring-Pedersen T and N) and the correct-key job's (ek.n, sigma).  The exponents stay in stage 2: the tables
         are sized by honest bounds (s1 < 2^770, s3 | s2 < 2^770 N~, Z < phi(N)),
         which prepare checks against the packed exponents."""
         ses = [sessions[s] for s in reg]
@@ -499,15 +499,23 @@ class SessionSet:
         if len(sts) != int(n.sum()):
             return
         f_nt, f_h1, f_h2 = G.field(sts, "N"), G.field(sts, "g"), G.field(sts, "ni")
-        rps = [m.ring_pedersen_statement for ms, lk, js in ses for m in ms + js]
+        am = [m for ms, lk, js in ses for m in ms + js]
+        rps = [m.ring_pedersen_statement for m in am]
         f_T, f_N = G.field(rps, "T"), G.field(rps, "N")
+        # the correct-key job's inputs (ek.n, sigma_vec): the prestart runs it beside GA
+        f_ckn = G.field([m.ek.n for m in am])
+        f_sig = G.rows([m.dk_correctness_proof for m in am], "sigma_vec", M2)
         bits = max(1, f_rn[1], f_s2[1], f_s[1], f_nt[1], f_h1[1], f_h2[1], f_T[1], f_N[1])
         nl = 64 if bits <= 2048 else 96 if bits <= 3072 else None
         if nl is None:
             return
+        ckl = next((w for w in _CK_WIDTHS if max(1, f_ckn[1], f_sig[1]) <= 32 * w), None)
         a_rn, a_s2, a_s = G.slot(f_rn, nl), G.slot(f_s2, nl), G.slot(f_s, nl)
         a_nt, a_h1, a_h2 = G.slot(f_nt, nl), G.slot(f_h1, nl), G.slot(f_h2, nl)
         a_T, a_N = G.slot(f_T, nl), G.slot(f_N, nl)
+        if ckl is not None:
+            ckl = max(ckl, nl)
+            a_ckn, a_sig = G.slot(f_ckn, ckl), G.slot(f_sig, ckl)
         G.run()
 
         def starts(counts):
@@ -525,6 +533,10 @@ class SessionSet:
             st[name] = np.uint64(self._k(arr)) + starts(n) * np.uint64(nl * 4)   # R + J messages per session
         st["m_security"] = M
         st["s1l"], st["s3l"], st["zl"] = _limbs_for(770), nl + _limbs_for(770), nl
+        if ckl is not None:
+            st["ckl"] = ckl
+            st["ck_n"] = np.uint64(self._k(a_ckn)) + starts(n) * np.uint64(ckl * 4)
+            st["ck_sigma"] = np.uint64(self._k(a_sig)) + starts(n * M2) * np.uint64(ckl * 4)
         self._pre, self.n_prestart = st, len(reg)
 
     def prestart_array(self):

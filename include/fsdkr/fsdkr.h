@@ -250,7 +250,12 @@ int fsdkr_collect_finish_multi(fsdkr_ctx* ctx, fsdkr_verdicts* out, uint32_t cou
  * counts, nl) of each batch; a later fsdkr_collect_prepare_multi of batches
  * with the same values and shapes consumes the results (otherwise it computes
  * them itself).  Lets the caller pack the other fields of 1024 custody
- * sessions (BASELINE configs[4]) while the longest chains run. */
+ * sessions (BASELINE configs[4]) while the longest chains run.  When every
+ * batch also carries recv_ntilde, recv_h1, recv_h2, ped_T, ped_N (and the s1l,
+ * s3l, zl widths) the fixed-base table chains start too; when every batch
+ * carries ck_n, ck_sigma and ckl (no ck_lens), so does the correct-key job
+ * (sigma_k^n mod n, zk-paillier NiCorrectKeyProof::verify).  Each part is
+ * reused only if prepare's values match it exactly. */
 int fsdkr_collect_prestart_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count);
 
 /* FsDkrError variants, in error.rs declaration order (error.rs:6-60). */

@@ -230,3 +230,31 @@ def test_session_set_pool_reuse():
     assert ids & {id(a) for a in second._owned}
     for k, a in enumerate(second._owned):
         assert np.array_equal(a, snap[k])
+
+
+def test_session_set_stage1_correct_key_rows():
+    """Stage 1 of a staged SessionSet carries every message's ek.n and sigma_vec
+    rows (fsdkr_collect_prestart_multi's correct-key job) at the width stage 2
+    uses, row k of session s at the session's message offset."""
+    import ctypes
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from pack_many_cpu import fake_sessions
+    from fsdkr.batch import M2, SessionSet
+    sess = fake_sessions(5, seed=4)
+    ss = SessionSet(sess, 256, 3072, staged=True)
+    pre = ss._pre
+    ckl = int(pre["ckl"][0])
+    assert ckl == 96
+    for s, (msgs, lk, joins) in enumerate(sess):
+        for k, m in enumerate(msgs):
+            row = np.ctypeslib.as_array(ctypes.cast(int(pre["ck_n"][s]) + k * ckl * 4, ctypes.POINTER(ctypes.c_uint32)),
+                                        (ckl,))
+            assert np.array_equal(row, _expect([m.ek.n], ckl)[0])
+            for j in range(M2):
+                at = int(pre["ck_sigma"][s]) + (k * M2 + j) * ckl * 4
+                row = np.ctypeslib.as_array(ctypes.cast(at, ctypes.POINTER(ctypes.c_uint32)), (ckl,))
+                assert np.array_equal(row, _expect([m.dk_correctness_proof.sigma_vec[j]], ckl)[0])
+    ss.complete()
+    assert int(ss.structs["ckl"][0]) == ckl
