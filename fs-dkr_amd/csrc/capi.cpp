@@ -275,7 +275,7 @@ int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, u
     return FSDKR_E_UNSUPPORTED;
   }
   std::string name = std::string("consts_") + tag;
-  *d_consts = (uint32_t*)c->buf(name.c_str(), sizeof(uint32_t) * (3 * (size_t)KD + 4) * (n_mod ? n_mod : 1));
+  *d_consts = (uint32_t*)c->buf(name.c_str(), sizeof(uint32_t) * (size_t)cons_stride(KD) * (n_mod ? n_mod : 1));
   if (!*d_consts) {
     c->fail("device allocation failed (mod consts)");
     return FSDKR_E_OOM;

@@ -44,6 +44,7 @@ int collect_launch_impl(Ctx* c) {
   // J2 / J5 (256-bit challenge exponents): 8 lanes per instance; a small 4096-bit
   // J2 (a multi-GPU rank's slice) one instance per wave: its chain is on the
   // critical path of the rank (J2 -> inverses -> equalities)
+  // (4 lanes for J2 / J5 measured no better at n = 64: profiles/r04/r04a_ab_ck_j2j5_v*)
   const uint32_t j2_group = (nn == 128 && pl.jcount[2] <= 1024) ? kWaveGroup : 8, j5_group = 8;
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;

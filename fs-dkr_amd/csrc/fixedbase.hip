@@ -31,7 +31,7 @@ __global__ __launch_bounds__(BLOCK) void fb_table_kernel(const FbTableArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
-  constexpr int STRIDE = 3 * KD + 4;
+  constexpr int STRIDE = cons_stride(KD);
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
@@ -87,7 +87,7 @@ template <int KR, int L, int K32>
 __global__ __launch_bounds__(64) void fb_table_wave_kernel(const FbTableArgs a) {
   constexpr int KD = 64 * L;
   using MT = Mont29<KD, 64, KR>;
-  constexpr int STRIDE = 3 * KR + 4;
+  constexpr int STRIDE = cons_stride(KR);
   const int g = threadIdx.x;
   const uint32_t b = blockIdx.x;
   if (b >= a.count) return;
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(BLOCK) void fb_exp_kernel(const FbExpArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
-  constexpr int STRIDE = 3 * KD + 4;
+  constexpr int STRIDE = cons_stride(KD);
   __shared__ uint32_t lds[2 * IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;

@@ -7,6 +7,15 @@ namespace fsdkr {
 
 constexpr int BLOCK = 256;
 
+// ---- per-modulus constants (mod_setup_kernel) ----------------------------------
+// Row of modulus m: [N | R mod N | R^2 mod N | ninv, pad x3] for the class's KD
+// digits, then the same block for N' = N (-N^-1 mod 2^29) (quotient-scaled rows;
+// written when SCALED_OK), R = 2^(29 KD).
+constexpr int cons_stride(int kd) { return 6 * kd + 8; }
+constexpr int cons_scaled(int kd) { return 3 * kd + 4; }
+// N' < 2^(32 K32 + 29) must leave R > 4N': 32 K32 + 31 <= 29 KD
+constexpr bool scaled_ok(int kd, int k32) { return 32 * k32 + 31 <= 29 * kd; }
+
 // One batched-modexp launch.  Operands are addressed per instance so a launch
 // can mix proof fields, device-computed challenges and other kernels' outputs.
 struct ModexpArgs {

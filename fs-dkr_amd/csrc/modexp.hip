@@ -24,18 +24,24 @@ __device__ __forceinline__ void lds_put(uint32_t* stream, const uint32_t* d, int
   for (int j = 0; j < L; ++j) stream[g * L + j] = d[j];
 }
 
-// consts[m] = {N digits | R mod N | R^2 mod N | ninv}   (STRIDE = 3*KD + 4 words)
+// consts row m (cons_stride(KD) words, kernels.h) = {N digits | R mod N | R^2 mod N |
+// ninv}, then when scaled_ok(KD, K32) the same block for N' = N (-N^-1 mod 2^29)
+// (the quotient-scaled chains of modexp_kernel<..., QS>).  Instances m < n_mod
+// write the N block of modulus m, instances n_mod + m its N' block.
 template <int KD, int G, int K32>
 __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __restrict__ mods, uint32_t n_mod,
                                                           uint32_t* __restrict__ consts) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
+  constexpr bool SC = scaled_ok(KD, K32);
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
-  const uint32_t m = blockIdx.x * IPB + li;
-  if (m >= n_mod) return;
+  const uint32_t mi = blockIdx.x * IPB + li;
+  if (mi >= (SC ? 2 * n_mod : n_mod)) return;
+  const bool scaled = SC && mi >= n_mod;
+  const uint32_t m = scaled ? mi - n_mod : mi;
   // a few waves at the head of every job's chain: they win issue arbitration
   // against the exponentiation waves already on the SIMD
   __builtin_amdgcn_s_setprio(3);
@@ -50,6 +56,7 @@ __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __rest
 #pragma unroll
   for (int it = 0; it < 5; ++it) inv *= 2u - n0 * inv;
   M.ninv = (0u - inv) & M29;
+  if (scaled) M.scale_modulus();   // n <- N', ninv <- 1
   int hb = -1;
 #pragma unroll
   for (int j = 0; j < L; ++j)
@@ -60,7 +67,7 @@ __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __rest
   for (int j = 0; j < L; ++j) y[j] = ((g * L + j) == hb / 29) ? (1u << (hb % 29)) : 0u;  // 2^(bitlen-1) < N
   const int nd1 = 29 * KD - hb;                 // -> 2^(29 KD) = R mod N
   for (int k = 0; k < nd1; ++k) M.dbl(y);
-  uint32_t* out = consts + (size_t)m * (3 * KD + 4);
+  uint32_t* out = consts + (size_t)m * cons_stride(KD) + (scaled ? cons_scaled(KD) : 0);
 #pragma unroll
   for (int j = 0; j < L; ++j) out[KD + g * L + j] = y[j];
   // R^2 mod N: 2^c * R (Montgomery form of 2^c) squared s times, c * 2^s = 29 KD
@@ -100,13 +107,18 @@ __device__ __forceinline__ void ct_row(uint32_t* dst, const uint32_t* T, uint32_
 }
 
 // CT: the regular-access variant for secret exponents (a separate instantiation:
-// its table scans would cost the throughput shapes occupancy)
-template <int KD, int G, int K32, bool CT = false>
+// its table scans would cost the throughput shapes occupancy).
+// QS: the chain runs modulo N' = N (-N^-1 mod 2^29) with quotient-scaled rows
+// (Mont29::row: the quotient digit is the retiring column, no multiply), from
+// the N' block of the constants row; a^e mod N' = a^e mod N (mod N), and the
+// exit product, a plain row pass modulo N, both leaves Montgomery form and
+// reduces: (acc + m N) / R < N + 2N'/R <= N + 1.
+template <int KD, int G, int K32, bool CT = false, bool QS = false>
 __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
-  constexpr int STRIDE = 3 * KD + 4;
+  constexpr int STRIDE = cons_stride(KD);
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
@@ -118,7 +130,9 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
-  const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  static_assert(!QS || (scaled_ok(KD, K32) && !CT), "quotient-scaled chains: public exponents, N' within R/4");
+  const uint32_t* C0 = a.consts + (size_t)a.mod_idx[inst] * STRIDE;   // N: the exit product
+  const uint32_t* C = QS ? C0 + cons_scaled(KD) : C0;                  // the chain's modulus
   MT M;
   M.init_lane(g);
 #pragma unroll
@@ -157,7 +171,8 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   const uint32_t n_build = tsize - 1;
   const uint32_t n_steps = n_build + (nwin - 1) * (w + 1) + 1;
   uint32_t k = 1, sub = 0;
-  for (uint32_t st = 0; st < n_steps; ++st) {
+  // QS: the last step (the exit product) runs after the loop with N's rows
+  for (uint32_t st = 0; st < n_steps - (QS ? 1 : 0); ++st) {
     const uint32_t* src = nullptr;
     bool from_acc = false, one = false;
     if (st == n_build) {                                                    // start of the ladder
@@ -193,14 +208,29 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
       for (int j = 0; j < L; ++j) stream[g * L + j] = src[g * L + j];
     }
     __builtin_amdgcn_wave_barrier();
-    if (from_acc) M.sqr(acc, acc, stream);   // the ladder's squarings: tournament rows
-    else M.mul(acc, acc, stream);
+    if constexpr (QS) {
+      if (from_acc) M.sqr_s(acc, acc, stream);
+      else M.mul_s(acc, acc, stream);
+    } else {
+      if (from_acc) M.sqr(acc, acc, stream);   // the ladder's squarings: tournament rows
+      else M.mul(acc, acc, stream);
+    }
     if (st < n_build) {
 #pragma unroll
       for (int j = 0; j < L; ++j) T[(size_t)(st + 1) * KD + g * L + j] = acc[j];
     } else if (st < n_steps - 1) {
       if (++sub == w + 1) { sub = 0; ++k; }
     }
+  }
+  if constexpr (QS) {   // exit: acc * 1 / R modulo N itself (acc = x R mod N' is x R mod N)
+#pragma unroll
+    for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
+    M.ninv = C0[3 * KD];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
+    __builtin_amdgcn_wave_barrier();
+    M.mul(acc, acc, stream);
   }
   M.carry_exact(acc);
   M.sub_if_ge(acc);
@@ -225,7 +255,7 @@ template <int KR, int L, int K32>
 __global__ __launch_bounds__(64) void modexp_wave_kernel(const ModexpArgs a) {
   constexpr int KD = 64 * L;
   using MT = Mont29<KD, 64, KR>;
-  constexpr int STRIDE = 3 * KR + 4;
+  constexpr int STRIDE = cons_stride(KR);
   __shared__ uint32_t lds[KD];
   const int g = threadIdx.x;
   const uint32_t inst = blockIdx.x;
@@ -306,7 +336,8 @@ __global__ __launch_bounds__(64) void modexp_wave_kernel(const ModexpArgs a) {
 template <int KD, int G, int K32>
 static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
   constexpr int IPB = BLOCK / G;
-  const uint32_t blocks = (n_mod + IPB - 1) / IPB;
+  const uint32_t inst = scaled_ok(KD, K32) ? 2 * n_mod : n_mod;
+  const uint32_t blocks = (inst + IPB - 1) / IPB;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((mod_setup_kernel<KD, G, K32>), dim3(blocks), dim3(BLOCK), 0, st, mods, n_mod, consts);
   return hipGetLastError();
@@ -317,13 +348,13 @@ static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* c
 constexpr uint32_t kSmallLaunchLanes = 256u * 4u * 64u;
 static inline uint32_t block_threads(uint32_t lanes) { return lanes <= kSmallLaunchLanes ? 64u : (uint32_t)BLOCK; }
 
-template <int KD, int G, int K32, bool CT = false>
+template <int KD, int G, int K32, bool CT = false, bool QS = false>
 static hipError_t launch_modexp(const ModexpArgs& a, hipStream_t st) {
   const uint32_t bs = block_threads(a.count * G);
   const uint32_t ipb = bs / G;
   const uint32_t blocks = (a.count + ipb - 1) / ipb;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((modexp_kernel<KD, G, K32, CT>), dim3(blocks), dim3(bs), 0, st, a);
+  hipLaunchKernelGGL((modexp_kernel<KD, G, K32, CT, QS>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
@@ -406,31 +437,41 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
       default: return hipErrorInvalidValue;
     }
   }
+  // the short-lane group shapes (8-32 lanes) run quotient-scaled chains
+  // (modexp_kernel QS); FSDKR_QS=0 selects the plain rows (A/B)
+  static int qs_env = -1;
+  if (qs_env < 0) {
+    const char* e = getenv("FSDKR_QS");
+    qs_env = (e && e[0] == '0') ? 0 : 1;
+  }
+  const bool qs = qs_env == 1;
   switch (k32) {
     case 32:   // 1024-bit primes of key generation: L = 9 (4 lanes) or 18
       return pick_group(a.count, (int)a.group, {2, 4}, 4) == 2 ? launch_modexp<36, 2, 32>(a, st)
                                                               : launch_modexp<36, 4, 32>(a, st);
     case 64:
       switch (pick_group(a.count, (int)a.group, {2, 4, 8}, 4)) {
-        case 8: return launch_modexp<72, 8, 64>(a, st);
+        case 8: return qs ? launch_modexp<72, 8, 64, false, true>(a, st) : launch_modexp<72, 8, 64>(a, st);
         case 4: return launch_modexp<72, 4, 64>(a, st);
         default: return launch_modexp<72, 2, 64>(a, st);
       }
     case 96: return launch_modexp<108, 4, 96>(a, st);
     case 128:
       // 32 lanes only on explicit request: it needs KD = 160 constants (mod_setup_g)
-      if (a.group == kWideGroup) return launch_modexp<160, 32, 128>(a, st);
+      if (a.group == kWideGroup)
+        return qs ? launch_modexp<160, 32, 128, false, true>(a, st) : launch_modexp<160, 32, 128>(a, st);
       if (a.group == kWaveGroup) return launch_modexp_wave<144, 3, 128>(a, st);
       // a launch past the resident-lane capacity: 4 lanes (L = 36, squaring rows
       // with 19 + 36 MACs per row) beat 8 (L = 18) by 4% (profiles/r02h_modexp_sqr.jsonl)
       switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
-        case 16: return launch_modexp<144, 16, 128>(a, st);
-        case 8: return launch_modexp<144, 8, 128>(a, st);
+        case 16: return qs ? launch_modexp<144, 16, 128, false, true>(a, st) : launch_modexp<144, 16, 128>(a, st);
+        case 8: return qs ? launch_modexp<144, 8, 128, false, true>(a, st) : launch_modexp<144, 8, 128>(a, st);
         default: return launch_modexp<144, 4, 128>(a, st);
       }
     case 192:
-      return pick_group(a.count, (int)a.group, {4, 8}, 4) == 8 ? launch_modexp<216, 8, 192>(a, st)
-                                                            : launch_modexp<216, 4, 192>(a, st);
+      if (pick_group(a.count, (int)a.group, {4, 8}, 4) == 8)
+        return qs ? launch_modexp<216, 8, 192, false, true>(a, st) : launch_modexp<216, 8, 192>(a, st);
+      return launch_modexp<216, 4, 192>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <utility>
 
+#include "kernels.h"
+
 namespace fsdkr {
 
 constexpr uint32_t M29 = (1u << 29) - 1;
@@ -241,22 +243,33 @@ struct Mont29 {
   // 64-bit accumulator between normalisations (NSTEP <= 18, L <= 18 here).
   static constexpr bool sq_raw(int d) { return d == 0 || (L % 2 == 0 && d == L / 2); }
   static constexpr bool sq_dbl(int d) { return d > 0 && (L % 2 == 1 ? d <= L / 2 : d < L / 2); }
+  // Short-lane group shapes (8-32 lanes) keep the doubled digits 2 b_j of a
+  // squaring in registers for the whole product (L shifts per product instead
+  // of one per row); the long-lane shapes cannot spare the L VGPRs, and the
+  // wave shape doubles its SGPR row digit on the scalar unit.
+  static constexpr bool USE_B2 = G >= 8 && G < 64;
+  static constexpr int NB2 = USE_B2 ? L : 1;
 
-  // a_r * b_j into slot (j + R) % L (squaring rows: the tournament slots only)
+  // a_r * b_j into slot (j + R) % L (squaring rows: the tournament slots only;
+  // 2 a_r b_j as a_r * (2 b_j) when the doubled digits are held, USE_B2)
   template <int R, bool SQ, int J>
-  __device__ __forceinline__ void mac_ab(uint64_t* acc, const uint32_t* b, uint32_t ai, uint32_t a2) const {
+  __device__ __forceinline__ void mac_ab(uint64_t* acc, const uint32_t* b, const uint32_t* b2, uint32_t ai,
+                                         uint32_t a2) const {
     if constexpr (SQ) {
       constexpr int d = (J - R % L + L) % L;
       if constexpr (sq_raw(d)) mac(acc[(J + R) % L], ai, b[J]);
-      else if constexpr (sq_dbl(d)) mac(acc[(J + R) % L], a2, b[J]);
+      else if constexpr (sq_dbl(d)) {
+        if constexpr (USE_B2) mac(acc[(J + R) % L], ai, b2[J]);
+        else mac(acc[(J + R) % L], a2, b[J]);
+      }
     } else {
       mac(acc[(J + R) % L], ai, b[J]);
     }
   }
   template <int R, bool SQ, int... Js>
-  __device__ __forceinline__ void mac_ab_rest(uint64_t* acc, const uint32_t* b, uint32_t ai, uint32_t a2,
-                                              std::integer_sequence<int, Js...>) const {
-    (mac_ab<R, SQ, Js + 1>(acc, b, ai, a2), ...);
+  __device__ __forceinline__ void mac_ab_rest(uint64_t* acc, const uint32_t* b, const uint32_t* b2, uint32_t ai,
+                                              uint32_t a2, std::integer_sequence<int, Js...>) const {
+    (mac_ab<R, SQ, Js + 1>(acc, b, b2, ai, a2), ...);
   }
 
   // One CIOS row at rotation R (logical column j lives in slot (j+R)%L).  For
@@ -271,15 +284,21 @@ struct Mont29 {
   // consecutive rows (measured: the fixed order cost 4-8 % at 8 lanes,
   // profiles/r03d_row_order_ab.txt).
   static constexpr bool ORDERED = HAS_ROT<G> && L > FSDKR_ROW_FENCE_MIN_L;
-  template <int R, bool SQ>
-  __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, const uint32_t* n, uint32_t ai) const {
+  // QS (quotient-scaled rows): the modulus is N' = N (-N^-1 mod 2^29), so
+  // -N'^-1 = 1 mod 2^29 and the quotient digit is the retiring column itself:
+  // no v_mul_lo_u32 on the row's dependency chain, and its mask folds into the
+  // broadcast (mul_s / sqr_s; the group shapes only).
+  template <int R, bool SQ, bool QS = false>
+  __device__ __forceinline__ void row(uint64_t* acc, const uint32_t* b, const uint32_t* b2, const uint32_t* n,
+                                      uint32_t ai) const {
     constexpr int s0 = R % L, s1 = (R + 1) % L;
-    const uint32_t a2 = SQ ? ai << 1 : 0u;
+    const uint32_t a2 = (SQ && !USE_B2) ? ai << 1 : 0u;
     if constexpr (ORDERED) {
-      mac_ab<R, SQ, 0>(acc, b, ai, a2);
+      static_assert(!QS, "quotient-scaled rows: group shapes of 8-32 lanes");
+      mac_ab<R, SQ, 0>(acc, b, b2, ai, a2);
       uint32_t m = (uint32_t)acc[s0] * ninv;
       __builtin_amdgcn_sched_barrier(0);
-      mac_ab_rest<R, SQ>(acc, b, ai, a2, std::make_integer_sequence<int, L - 1>{});
+      mac_ab_rest<R, SQ>(acc, b, b2, ai, a2, std::make_integer_sequence<int, L - 1>{});
       __builtin_amdgcn_sched_barrier(0);
       m = bcast_lane0<G>(m) & m29;   // one v_and_b32 with the DPP broadcast folded in
       mac(acc[s0], m, n[0]);
@@ -295,11 +314,13 @@ struct Mont29 {
       __builtin_amdgcn_sched_barrier(0);
       acc[s0] = (uint64_t)(dpp_next_rot<G>(digit) & m29);   // lane 0's digit is 0: the top lane gets the 0 it needs
     } else {
-      mac_ab<R, SQ, 0>(acc, b, ai, a2);
-      mac_ab_rest<R, SQ>(acc, b, ai, a2, std::make_integer_sequence<int, L - 1>{});
+      static_assert(!QS || G < 64, "quotient-scaled rows: group shapes of 8-32 lanes");
+      mac_ab<R, SQ, 0>(acc, b, b2, ai, a2);
+      mac_ab_rest<R, SQ>(acc, b, b2, ai, a2, std::make_integer_sequence<int, L - 1>{});
       // G = 64: the instance is the wave, so m is computed on the scalar unit
       // from lane 0's column (ninv is an SGPR there)
       const uint32_t m = (G == 64) ? ((bcast_lane0<G>((uint32_t)acc[s0]) * ninv) & M29)
+                         : QS      ? (bcast_lane0<G>((uint32_t)acc[s0]) & m29)
                                    : (bcast_lane0<G>((uint32_t)acc[s0] * ninv) & m29);
 #pragma unroll
       for (int j = 0; j < L; ++j) mac(acc[(j + R) % L], m, n[j]);
@@ -319,41 +340,52 @@ struct Mont29 {
   // the read's latency hides behind this row's MACs instead of stalling the
   // next row (one wave per SIMD in latency-bound launches has no other wave
   // to cover it).  arow[L] past the last cycle reads a harmless in-range word.
-  template <int R, bool SQ>
-  __device__ __forceinline__ void row_pf(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* arow,
-                                         uint32_t& cur, uint32_t next_off) const {
+  template <int R, bool SQ, bool QS>
+  __device__ __forceinline__ void row_pf(uint64_t* acc, const uint32_t* b, const uint32_t* b2, const uint32_t* n,
+                                         const uint32_t* arow, uint32_t& cur, uint32_t next_off) const {
     const uint32_t ai = cur;
     cur = (R + 1 < L) ? arow[R + 1] : arow[next_off];
-    row<R, SQ>(acc, b, n, ai);
+    row<R, SQ, QS>(acc, b, b2, n, ai);
   }
 
-  template <bool SQ, int... Rs>
-  __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* arow,
-                                        uint32_t& cur, uint32_t next_off, std::integer_sequence<int, Rs...>) const {
-    (row_pf<Rs, SQ>(acc, b, n, arow, cur, next_off), ...);
+  template <bool SQ, bool QS, int... Rs>
+  __device__ __forceinline__ void cycle(uint64_t* acc, const uint32_t* b, const uint32_t* b2, const uint32_t* n,
+                                        const uint32_t* arow, uint32_t& cur, uint32_t next_off,
+                                        std::integer_sequence<int, Rs...>) const {
+    (row_pf<Rs, SQ, QS>(acc, b, b2, n, arow, cur, next_off), ...);
   }
 
   // out = a * b / R  (almost Montgomery, < 2N), b = this lane's L digits (regs),
   // a = full KD-digit operand in LDS.  out may alias b.  (Non-const: b and n
   // pass through opaque(), which leaves their values unchanged.)
-  __device__ __forceinline__ void mul(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<false>(out, b, a_lds); }
+  __device__ __forceinline__ void mul(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<false, false>(out, b, a_lds); }
   // out = a^2 / R where a_lds holds the same value as b (squaring rows above)
-  __device__ __forceinline__ void sqr(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<true>(out, b, a_lds); }
+  __device__ __forceinline__ void sqr(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<true, false>(out, b, a_lds); }
+  // the same products with quotient-scaled rows (n holds N' = N (-N^-1 mod 2^29), see row())
+  __device__ __forceinline__ void mul_s(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<false, true>(out, b, a_lds); }
+  __device__ __forceinline__ void sqr_s(uint32_t* out, uint32_t* b, const uint32_t* a_lds) { product<true, true>(out, b, a_lds); }
 
-  template <bool SQ>
+  template <bool SQ, bool QS>
   __device__ __forceinline__ void product(uint32_t* out, uint32_t* b, const uint32_t* a_lds) {
     static_assert(!SQ || NORM_IN_CYCLE || L <= 21, "squaring rows: column bound");
     static_assert(G != 64, "the wave shape streams from registers: product_w");
     uint64_t acc[L];
 #pragma unroll
     for (int j = 0; j < L; ++j) acc[j] = 0;
+    uint32_t b2[NB2];
+    if constexpr (SQ && USE_B2) {
+#pragma unroll
+      for (int j = 0; j < L; ++j) b2[j] = b[j] << 1;   // digits <= 2^29 + 127: fits
+    }
     uint32_t cur = a_lds[0];
 #pragma unroll 1
     for (int cyc = 0; cyc < G; ++cyc) {
       // values unchanged; only the optimiser's view of them is reset (see opaque)
       opaque<L>(b);
       opaque<L>(n);
-      cycle<SQ>(acc, b, n, a_lds + cyc * L, cur, cyc + 1 < G ? (uint32_t)L : 0u, std::make_integer_sequence<int, L>{});
+      if constexpr (SQ && USE_B2) opaque<L>(b2);
+      cycle<SQ, QS>(acc, b, b2, n, a_lds + cyc * L, cur, cyc + 1 < G ? (uint32_t)L : 0u,
+                    std::make_integer_sequence<int, L>{});
     }
     finish(out, acc);
   }
@@ -372,7 +404,7 @@ struct Mont29 {
     const uint32_t ai = cur;   // next row's digit first: the readlane latency hides behind this row
     cur = (R + 1 < L) ? (uint32_t)__builtin_amdgcn_readlane((int)a[R + 1], cyc)
                       : (uint32_t)__builtin_amdgcn_readlane((int)a[0], cyc + 1);   // lane KR/L past the end: unused
-    row<R, SQ>(acc, b, n, ai);
+    row<R, SQ>(acc, b, nullptr, n, ai);
   }
   template <bool SQ, int... Rs>
   __device__ __forceinline__ void cycle_w(uint64_t* acc, const uint32_t* b, const uint32_t* n, const uint32_t* a,
@@ -418,6 +450,31 @@ struct Mont29 {
       for (int j = 0; j < L; ++j) { uint32_t v = d[j] + in; d[j] = v & M29; in = v >> 29; }
       c = in;
     }
+  }
+
+  // n <- N' = N k with k = ninv = -N^-1 mod 2^29 (exact digits in, exact out), so
+  // N' = -1 mod 2^29: the modulus of the quotient-scaled rows.  The caller
+  // guarantees N' < 2^(29 KD) (SCALED_OK).
+  __device__ __forceinline__ void scale_modulus() {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const uint64_t t = (uint64_t)n[j] * ninv + c;   // < 2^58 + 2^30
+      n[j] = (uint32_t)t & M29;
+      c = (uint32_t)(t >> 29);
+    }
+#pragma unroll 1
+    for (int round = 0; round < G - 1; ++round) {   // each lane's carry into the next lane's digits
+      uint32_t in = dpp_prev<G>(c) & m_first;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const uint32_t v = n[j] + in;
+        n[j] = v & M29;
+        in = v >> 29;
+      }
+      c = in;
+    }
+    ninv = 1u;
   }
 
   // d (exact digits, value < 2N) -> d mod N

@@ -22,7 +22,7 @@ __global__ __launch_bounds__(BLOCK) void mr_tail_kernel(const MrTailArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
-  constexpr int STRIDE = 3 * KD + 4;
+  constexpr int STRIDE = cons_stride(KD);
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;

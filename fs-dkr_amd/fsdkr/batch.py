@@ -195,11 +195,14 @@ class CollectBatch:
     reads is packed (counts, party indices, lengths, ek.n)."""
 
     def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048, n_recv=None,
-                 header_only=False, staged=False):
+                 header_only=False, staged=False, ck_stage1=False):
         """n_recv: receivers (default R + J); a multi-GPU shard passes its slice of the
         messages together with the full receiver count.  staged: pack only the
         fields fsdkr_collect_prestart reads (recv_n, pdl s2, range-proof s; see
-        ga_ready) and leave the rest to complete()."""
+        ga_ready) and leave the rest to complete().  ck_stage1: stage 1 also packs
+        ek.n and sigma, so the prestart runs the correct-key job beside GA (at
+        n = 64 it competed with GA's chains: 56.2 -> 59.0 ms median,
+        profiles/r04/r04a_ab_ck_j2j5_v0/v1)."""
         msgs, joins = list(refresh_messages), list(join_messages)
         R, J = len(msgs), len(joins)
         n = n_recv if n_recv else R + J
@@ -288,6 +291,14 @@ class CollectBatch:
             names = ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s", "ped_T", "ped_N",
                      "pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
             ga = {name: Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c)) for name in names}
+            # the correct-key job (sigma^n mod n) reads only ek.n and sigma: stage 1
+            # packs them at the width complete() gives them, so the prestart runs
+            # it beside GA (csrc/collect_prestart.cpp prestart_ck)
+            ck_pre = ck_stage1 and not ck_short
+            if ck_pre:
+                c.ckl = max(ckl, nl_ga)
+                ga["ck_n"] = Gs.slot(f_ckn, c.ckl)
+                ga["ck_sigma"] = Gs.slot(f_sig, c.ckl)
             Gs.run()
             for name, arr in ga.items():
                 setattr(c, name, k(arr))
@@ -343,10 +354,14 @@ class CollectBatch:
         for name, f in F.items():
             if name not in keep:
                 setattr(c, name, k(G.slot(f, width.get(name, nl))))
-        c.ck_n = k(G.slot(st["f_ckn"], c.ckl))
+        ga_arrs = self._ga[1] if self._ga is not None else {}
+        if "ck_n" in ga_arrs and ga_arrs["ck_n"].shape[1] == c.ckl:   # stage 1 packed them at this width
+            pass
+        else:
+            c.ck_n = k(G.slot(st["f_ckn"], c.ckl))
+            c.ck_sigma = k(G.slot(st["f_sig"], c.ckl))
         if st["ck_short"]:
             c.ck_lens = k(np.array([len(x) for x in st["sig"]], dtype=np.uint32))
-        c.ck_sigma = k(G.slot(st["f_sig"], c.ckl))
         G.run()
         c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
         c.pdl_u1 = k(pack_points(pdl, "u1"))

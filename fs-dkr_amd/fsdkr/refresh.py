@@ -246,10 +246,10 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
         try:   # the share recovery's host pre-pass and GPU work overlap the pipeline
             if recovery == "speculative":
                 pend = _speculative_launch(ctx, [job])
-        finally:   # the batch never stays in flight
-            verdicts = ctx.collect_finish(batch)
-            if pend is not None:   # nor does the recovery
-                spec = _speculative_finish(ctx, pend)[0]
+        finally:   # neither the batch nor the recovery stays in flight
+            verdicts, specs = _finish_both(ctx, lambda: ctx.collect_finish(batch), pend)
+            if specs is not None:
+                spec = specs[0]
     err, applied = _mapped(ctx, batch, msgs, verdicts)
     if recovery == "after" or batch.header_only:
         spec = _recover_after(ctx, [job], [err])[0]
@@ -285,11 +285,10 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="sp
         try:   # the share recovery's host pre-pass and GPU work overlap the pipeline
             if recovery == "speculative":
                 pend = _speculative_launch(ctx, [jobs[i] for i in live])
-        finally:   # the batch never stays in flight
-            verdicts = ctx.collect_finish_set(sset)
-            if pend is not None:   # nor does the recovery
-                for i, r in zip(live, _speculative_finish(ctx, pend)):
-                    specs[i] = r
+        finally:   # neither the batch nor the recovery stays in flight
+            verdicts, rs = _finish_both(ctx, lambda: ctx.collect_finish_set(sset), pend)
+            for i, r in zip(live, rs or ()):
+                specs[i] = r
     errs = []
     for i, (msgs, lk, dk, joins) in enumerate(sess):
         if i in sset.row:
@@ -344,10 +343,10 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
             try:   # the share recovery's host pre-pass and GPU work overlap the pipeline
                 if recovery == "speculative":
                     pend = _speculative_launch(ctx, jobs)
-            finally:   # the batch never stays in flight
-                verdicts = ctx.collect_finish(batch)
-                if pend is not None:   # nor does the recovery
-                    specs = _speculative_finish(ctx, pend)
+            finally:   # neither the batch nor the recovery stays in flight
+                verdicts, rs = _finish_both(ctx, lambda: ctx.collect_finish(batch), pend)
+                if rs is not None:
+                    specs = rs
         err, applied = _mapped(ctx, batch, msgs, verdicts)
         if recovery == "after" or batch.header_only:
             specs = _recover_after(ctx, jobs, [err] * len(jobs))
@@ -387,15 +386,30 @@ def _speculative_launch(ctx, jobs):
             nl = _dk_limbs(lk.paillier_dk)
             if nl is None:
                 raise FsDkrPanic("share recovery: decryption key wider than 6144 bits")
-            if max(c.bit_length() for c in plan["cts"]) > 64 * nl:
-                raise FsDkrPanic("share recovery: a ciphertext wider than N^2")
+            # Paillier::mul / add / decrypt reduce their operands mod N^2 (powm and
+            # mulm mod NN), so a ciphertext c + k N^2 recovers like c: reduce here,
+            # the C ABI takes ciphertexts below 2^(64 nl) (fsdkr.h)
+            nn_ = (lk.paillier_dk.p * lk.paillier_dk.q) ** 2
+            cts = [c % nn_ if c >= nn_ else c for c in plan["cts"]]
         except (FsDkrPanic, IndexError, AttributeError, TypeError) as e:
             out[k] = e if isinstance(e, FsDkrPanic) else FsDkrPanic(f"share recovery: {e!r}")
             continue
         todo.append(k)
-        cj.append(dict(nl=nl, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=plan["cts"],
+        cj.append(dict(nl=nl, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=cts,
                        p=lk.paillier_dk.p, q=lk.paillier_dk.q, points=plan["pts"]))
     return out, todo, (ctx.collect_recover_launch(cj) if cj else None)
+
+
+def _finish_both(ctx, finish, pend):
+    """finish() the launched verification batch, then the launched share recovery
+    (pend, or None) even when finish() raises: a recovery left in flight would
+    refuse every later fsdkr_collect_recover_launch on the context.  Returns
+    (finish()'s verdicts, the recovery results or None)."""
+    try:
+        verdicts = finish()
+    finally:
+        specs = _speculative_finish(ctx, pend) if pend is not None else None
+    return verdicts, specs
 
 
 def _speculative_finish(ctx, pending):
