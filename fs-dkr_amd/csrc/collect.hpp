@@ -373,14 +373,22 @@ inline void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, ui
   on[0] = 3;
 }
 
-// GA lanes per instance: GA shares the chip with the other streams, so it takes
-// the largest group that keeps it within about half the resident lanes
-// (measured at n = 64: 8 lanes 64 ms/step vs 16 lanes 70 ms); small batches
-// (multi-GPU shards) get 16 or 32 lanes (KD = 160 constants), and at most one
-// wave per SIMD (1024 chains) one wave per chain (modexp_wave_kernel), for latency.
-// Used by the prestart and by launch().
+// GA lanes per instance.  GA's chains are the pipeline's critical path and share
+// the chip with every other stream.  With quotient-scaled rows (modexp.hip QS)
+// the 16-lane 4096-bit shape issues fewer instructions per row than 8 lanes and
+// fits three waves per SIMD (98 VGPRs): n = 64 (7 680 chains) went from 57.4 to
+// 51.5 ms per call against 8 lanes (profiles/r04/r04d_ab_lanes_v*).  Small
+// batches (multi-GPU shards) get 32 lanes (KD = 160 constants), and at most one
+// wave per SIMD (1024 chains) one wave per chain (modexp_wave_kernel), for
+// latency; batches past 16 384 chains (n = 256) keep 8 lanes.  Used by the
+// prestart and by launch().
 inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
-  uint32_t g = 8;
+  static const int ga_env = [] {   // A/B (temporary)
+    const char* e = getenv("FSDKR_GA_G");
+    return e ? atoi(e) : 0;
+  }();
+  if (ga_env == 4 || ga_env == 8 || ga_env == 16) return (uint32_t)ga_env;
+  uint32_t g = (nn == 128 && count <= 16384u) ? 16 : 8;
   for (uint32_t x : {16u, kWideGroup})
     if ((uint64_t)count * x <= 65536u) g = x;
   if (g == kWideGroup && nn != 128) g = 16;

@@ -41,11 +41,15 @@ int collect_launch_impl(Ctx* c) {
   }
   if ((rc = setup_moduli(c, nl, PI(pl.o_mods), pl.n_mods_nl, &cons_nl, "collect_nl"))) return rc;
   if ((rc = setup_moduli(c, pl.ckl, PI(pl.o_ckmods), Mt, &cons_ck, "collect_ck"))) return rc;
-  // J2 / J5 (256-bit challenge exponents): 8 lanes per instance; a small 4096-bit
-  // J2 (a multi-GPU rank's slice) one instance per wave: its chain is on the
-  // critical path of the rank (J2 -> inverses -> equalities)
-  // (4 lanes for J2 / J5 measured no better at n = 64: profiles/r04/r04a_ab_ck_j2j5_v*)
-  const uint32_t j2_group = (nn == 128 && pl.jcount[2] <= 1024) ? kWaveGroup : 8, j5_group = 8;
+  // J2 / J5 (256-bit challenge exponents): the 4096-bit J2 at 16 lanes (the
+  // quotient-scaled 16-lane shape, with GA at 16 lanes: n = 64 51.0 ms per call,
+  // profiles/r04/r04d_ab_lanes_v3), a small J2 (a multi-GPU rank's slice) one
+  // instance per wave: its chain is on the critical path of the rank (J2 ->
+  // inverses -> equalities); J5 (2048-bit) at 8 lanes (4 lanes measured no
+  // better, profiles/r04/r04a_ab_ck_j2j5_v*)
+  uint32_t j2_group = nn == 128 ? (pl.jcount[2] <= 1024 ? kWaveGroup : pl.jcount[2] <= 16384 ? 16 : 8) : 8;
+  const uint32_t j5_group = 8;
+  if (const char* e = getenv("FSDKR_J2_G")) j2_group = (uint32_t)atoi(e);   // A/B (temporary)
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;
   if (ga_group == kWideGroup && pl.jcount[0]) {

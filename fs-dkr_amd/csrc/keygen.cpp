@@ -224,7 +224,11 @@ extern "C" int fsdkr_sample_primes(fsdkr_ctx* ctx, uint32_t bits, uint32_t count
     r[0] |= 1u;
     w = Walk();
     w.start = hbn::from(r.data(), dl);
-    w.offs = sieve(w.start, span);
+    // the walk stays below 2^bits (a `bits`-bit prime): start + 2k < 2^bits
+    uint32_t wspan = span;
+    const hbn::Limbs room = hbn::sub(hbn::shl(hbn::Limbs{1}, bits), w.start);   // > 0: start < 2^bits
+    if (hbn::bitlen(room) <= 32) wspan = std::min<uint32_t>(span, (room.empty() ? 0u : room[0] + 1u) / 2u);
+    w.offs = sieve(w.start, wspan);
     return FSDKR_OK;
   };
   auto run_mr = [&](const std::vector<hbn::Limbs>& cands, const std::vector<hbn::Limbs>& bases,

@@ -391,6 +391,7 @@ struct RecoverPending {
     std::vector<hbn::Limbs> li;
     hbn::Limbs P, Q, qinv, pinv;
     bool dec_ok = false;
+    bool no_dec = false;     // FSDKR_RECOVER_NO_DECRYPT: pk_vec rows only
     uint32_t width = 0;      // decryption batch (index into widths)
     size_t dec_at = 0;       // its first decryption in that batch
     size_t row = ~(size_t)0; // its first pk_vec row of the MSM
@@ -451,6 +452,11 @@ int RecoverPending::launch(Ctx* c, const fsdkr_recover_job* in, uint32_t count) 
       X.tp = std::min(J.t_key, J.t_vss) + 1;
       X.li.resize(X.T);
       for (uint32_t k = 0; k < X.T; ++k) X.li[k] = lagrange(J.old_index, X.T, k, Qs);
+      X.no_dec = (J.flags & FSDKR_RECOVER_NO_DECRYPT) != 0;
+      if (X.no_dec) {   // the Lagrange weights of the pk_vec rows; the key is not read
+        X.dec_ok = true;
+        continue;
+      }
       X.P = hbn::from(J.p, J.nl);
       X.Q = hbn::from(J.q, J.nl);
       const hbn::Limbs PP = hbn::mul(X.P, X.P), QQ = hbn::mul(X.Q, X.Q), N = hbn::mul(X.P, X.Q);
@@ -467,7 +473,7 @@ int RecoverPending::launch(Ctx* c, const fsdkr_recover_job* in, uint32_t count) 
     W.nl = nl;
     std::vector<uint32_t> owners;
     for (uint32_t j = 0; j < count; ++j)
-      if (jobs[j].nl == nl && jobs[j].dec_ok) {
+      if (jobs[j].nl == nl && jobs[j].dec_ok && !jobs[j].no_dec) {
         jobs[j].width = (uint32_t)widths.size();
         jobs[j].dec_at = W.total;
         W.total += jobs[j].T;
@@ -611,6 +617,12 @@ int RecoverPending::finish(Ctx* c, fsdkr_recovered* out) {
         O.status = FSDKR_RECOVER_PANIC_DECRYPT;
         continue;
       }
+      O.status = X.t_key > X.t_vss ? FSDKR_RECOVER_PANIC_LI : FSDKR_RECOVER_OK;
+      if (X.n_new) {
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(msm_out.p) + X.row * 16;
+        std::memcpy(O.pk_vec, r, (size_t)X.n_new * 64);
+      }
+      if (X.no_dec) continue;
       const uint32_t nl = X.nl;
       const uint32_t* h = widths[X.width].out;
       // kzen-paillier CRT decryption with g = N + 1: h_p = L_p(g^(p-1) mod p^2)^-1 = p - q^-1 mod p
@@ -632,11 +644,6 @@ int RecoverPending::finish(Ctx* c, fsdkr_recovered* out) {
       const hbn::Limbs share = hbn::mod(hbn::mod(acc, N), Qs);
       hbn::store(share, O.share, 8);
       if (!g_mul(share, O.y)) ec_ok = false;
-      if (X.n_new) {
-        const uint32_t* r = reinterpret_cast<const uint32_t*>(msm_out.p) + X.row * 16;
-        std::memcpy(O.pk_vec, r, (size_t)X.n_new * 64);
-      }
-      O.status = X.t_key > X.t_vss ? FSDKR_RECOVER_PANIC_LI : FSDKR_RECOVER_OK;
     }
   });
   if (!ec_ok) {
@@ -659,7 +666,8 @@ int fsdkr_collect_recover_launch(fsdkr_ctx* ctx, const fsdkr_recover_job* jobs, 
   }
   for (uint32_t j = 0; j < count; ++j) {
     const fsdkr_recover_job& J = jobs[j];
-    if (!shape_digits(J.nl) || !J.old_index || !J.cts || !J.p || !J.q || (J.n_new && !J.points)) {
+    const bool dec = !(J.flags & FSDKR_RECOVER_NO_DECRYPT);   // a rows-only job reads no key or ciphertext
+    if (!shape_digits(J.nl) || !J.old_index || (dec && (!J.cts || !J.p || !J.q)) || (J.n_new && !J.points)) {
       c->fail("fsdkr_collect_recover: job %u: bad shape or null array (nl=%u)", j, J.nl);
       return FSDKR_E_ARG;
     }

@@ -55,7 +55,7 @@ class VerdictsC(ctypes.Structure):
 class RecoverJobC(ctypes.Structure):
     _fields_ = [("nl", ctypes.c_uint32), ("t_vss", ctypes.c_uint32), ("t_key", ctypes.c_uint32),
                 ("n_new", ctypes.c_uint32), ("old_index", u32p), ("cts", u32p), ("p", u32p), ("q", u32p),
-                ("points", u32p)]
+                ("points", u32p), ("flags", ctypes.c_uint32)]
 
 
 class RecoveredC(ctypes.Structure):
@@ -78,6 +78,7 @@ _RECOVERED_DT = np.dtype({"names": ["pk_vec", "status"], "formats": [np.uint64, 
                           "offsets": [RecoveredC.pk_vec.offset, RecoveredC.status.offset],
                           "itemsize": ctypes.sizeof(RecoveredC)})
 RECOVER_OK, RECOVER_PANIC_LI, RECOVER_PANIC_DECRYPT = 0, 1, 2
+RECOVER_NO_DECRYPT = 1   # fsdkr_recover_job.flags
 DRAW_BITS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                 ctypes.c_uint32)
 
@@ -469,8 +470,9 @@ class Context:
         return out
 
     def collect_recover(self, jobs):
-        """fsdkr_collect_recover: jobs = [dict(nl, t_vss, t_key, old_index, cts, p, q, points)],
-        points[i] = the first min(t_key, t_vss)+1 committed points for new party i.
+        """fsdkr_collect_recover: jobs = [dict(nl, t_vss, t_key, old_index, cts, p, q, points[, flags])],
+        points[i] = the first min(t_key, t_vss)+1 committed points for new party i
+        (flags RECOVER_NO_DECRYPT: those pk_vec rows only, share and y zero).
         Returns per job (status, share, y, pk_vec); a ciphertext wider than N^2
         raises ValueError (ints_to_limbs)."""
         return self.collect_recover_finish(self.collect_recover_launch(jobs))
@@ -525,6 +527,7 @@ class Context:
         rows["cts"], rows["p"], rows["q"] = c_ptr, p_ptr, q_ptr
         poff = np.concatenate([[0], np.cumsum(n_new * tp)[:-1]]).astype(np.uint64)
         rows["points"] = np.uint64(Pt.ctypes.data) + poff * np.uint64(64)
+        rows["flags"] = [j.get("flags", 0) for j in jobs]
         # the launch reads every host array before it returns (keep, idx, Pt, rows live until then)
         self.check(self._lib.fsdkr_collect_recover_launch(
             self._h, ctypes.cast(rows.ctypes.data, ctypes.POINTER(RecoverJobC)), J))

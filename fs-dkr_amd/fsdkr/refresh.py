@@ -19,7 +19,7 @@ checks and before any paillier_key_vec write; decryption and the pk_vec loop
 (:439-464) after them.
 collect_many() verifies many independent sessions in one device pass
 (BASELINE configs[4]).  There is no CPU fallback."""
-from ._native import Context
+from ._native import RECOVER_NO_DECRYPT, Context
 from .batch import CollectBatch, SessionSet
 
 Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
@@ -56,6 +56,11 @@ class FsDkrError(Exception):
 
 class FsDkrPanic(Exception):
     """The reference panics at this point (unwrap / index / assert)."""
+
+
+class _DecryptPanic(FsDkrPanic):
+    """Paillier::decrypt panics on a degenerate decryption key (p or q even or 1,
+    p == q): after every check (refresh_message.rs:439)."""
 
 
 class _SumPanic(FsDkrPanic):
@@ -377,12 +382,24 @@ def _speculative_launch(ctx, jobs):
     """The host pre-pass of _speculative and the launch of its GPU work
     (fsdkr_collect_recover_launch); _speculative_finish collects the results.
     collect() launches it right after its pipeline, so the host pre-pass (the
-    Lagrange weights: O(t^2) products at n = 256) overlaps the device work."""
+    Lagrange weights: O(t^2) products at n = 256) overlaps the device work.
+    A job is (msgs, local_key, n_new) or (msgs, local_key, n_new, (lo, hi),
+    decrypt): a multi-GPU rank's part (fsdkr/shard.py), the pk_vec rows
+    [lo, hi) and the decryption only if `decrypt`; the inputs of every row are
+    still checked here, so every rank raises the same panic."""
     out = [None] * len(jobs)
     todo, cj = [], []
-    for k, (msgs, lk, n_new) in enumerate(jobs):
+    for k, job in enumerate(jobs):
+        msgs, lk, n_new = job[:3]
+        lo, hi = job[3] if len(job) > 3 else (0, n_new)
+        decrypt = job[4] if len(job) > 4 else True
         try:
             plan = _recovery_plan(msgs, lk, n_new)
+            if not decrypt:
+                todo.append(k)
+                cj.append(dict(nl=64, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=[0] *
+                               (plan["t_vss"] + 1), p=1, q=1, points=plan["pts"][lo:hi], flags=RECOVER_NO_DECRYPT))
+                continue
             nl = _dk_limbs(lk.paillier_dk)
             if nl is None:
                 raise FsDkrPanic("share recovery: decryption key wider than 6144 bits")
@@ -396,7 +413,7 @@ def _speculative_launch(ctx, jobs):
             continue
         todo.append(k)
         cj.append(dict(nl=nl, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=cts,
-                       p=lk.paillier_dk.p, q=lk.paillier_dk.q, points=plan["pts"]))
+                       p=lk.paillier_dk.p, q=lk.paillier_dk.q, points=plan["pts"][lo:hi]))
     return out, todo, (ctx.collect_recover_launch(cj) if cj else None)
 
 
@@ -417,7 +434,7 @@ def _speculative_finish(ctx, pending):
     if handle is not None:
         for k, (status, share, y, pk) in zip(todo, ctx.collect_recover_finish(handle)):
             if status == 2:   # FSDKR_RECOVER_PANIC_DECRYPT
-                out[k] = FsDkrPanic("share recovery: Paillier::decrypt (degenerate decryption key)")
+                out[k] = _DecryptPanic("share recovery: Paillier::decrypt (degenerate decryption key)")
             else:
                 out[k] = (share, y, pk, status != 1)   # 1: FSDKR_RECOVER_PANIC_LI
     return out

@@ -7,10 +7,18 @@ zero-filled byte vector laid out as
 
     [feldman R*n | pdl R*n | range R*n | ped R+J | ck R+J | dlog J]
 
+The share recovery (refresh_message.rs:439-464) is split the same way: rank r
+rebuilds the pk_vec rows of its slice of the new parties (one MSM row per
+party) and rank 0 alone decrypts the new share; their results ride in the same
+all-reduce, in a region appended to the verdict bytes (each rank writes only
+its own part, the others are zero, so MAX is the union):
+
+    [status 1 | share 32 | y 64 | pk_vec n*64]      (little-endian limbs)
+
 No other data crosses the interconnect.  collect() then maps the merged
 verdicts to the reference's first error on a header-only batch of the whole
 message set (threshold, sizes, party indices, ek.n) and applies collect()'s
-side effects and share recovery (refresh_message.rs:330-464) on every rank."""
+side effects and the merged share recovery on every rank."""
 import os
 
 import numpy as np
@@ -30,6 +38,57 @@ def shard_range(count, world, rank):
 
 def global_len(R, J, n):
     return 3 * R * n + 2 * (R + J) + J
+
+
+DEC_RANK = 0   # the rank that decrypts the new share
+
+
+def recovery_len(n):
+    return 1 + 32 + 64 + 64 * n
+
+
+def _pt_bytes(pt):
+    return bytes(64) if pt is None else pt[0].to_bytes(32, "little") + pt[1].to_bytes(32, "little")
+
+
+def _bytes_pt(b):
+    v = int.from_bytes(bytes(b), "little")
+    return None if v == 0 else (v & ((1 << 256) - 1), v >> 256)
+
+
+def encode_recovery(spec, n, rows, decrypt):
+    """This rank's part of the share recovery as bytes of the exchange region:
+    its pk_vec rows, and (the decrypting rank) status, share and y.  A panic the
+    plan raised is not encoded: every rank raises the same one from the same inputs."""
+    from .refresh import _DecryptPanic
+    out = np.zeros(recovery_len(n), np.uint8)
+    if spec is None or isinstance(spec, Exception):
+        if decrypt and isinstance(spec, _DecryptPanic):   # Paillier::decrypt on a degenerate key
+            out[0] = 3
+        return out
+    share, y, pk, t_ok = spec
+    lo, hi = rows
+    if decrypt:
+        out[0] = 1 if t_ok else 2
+        out[1:33] = np.frombuffer(int(share).to_bytes(32, "little"), np.uint8)
+        out[33:97] = np.frombuffer(_pt_bytes(y), np.uint8)
+    for i, pt in zip(range(lo, hi), pk):
+        out[97 + 64 * i:97 + 64 * (i + 1)] = np.frombuffer(_pt_bytes(pt), np.uint8)
+    return out
+
+
+def decode_recovery(region, local_spec, n):
+    """The merged recovery (the tuple refresh._conclude takes, or the panic)."""
+    from .refresh import _DecryptPanic
+    if isinstance(local_spec, Exception) and not isinstance(local_spec, _DecryptPanic):
+        return local_spec
+    st = int(region[0])
+    if st == 3:
+        return _DecryptPanic("share recovery: Paillier::decrypt (degenerate decryption key)")
+    share = int.from_bytes(bytes(region[1:33]), "little")
+    y = _bytes_pt(region[33:97])
+    pk = [_bytes_pt(region[97 + 64 * i:97 + 64 * (i + 1)]) for i in range(n)]
+    return (share, y, pk, st != 2)
 
 
 def scatter(v, R, J, n, world, rank):
@@ -120,7 +179,7 @@ def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, devic
     reference's outcome: None after updating `local_key` as collect() does, or
     raises the FsDkrError / FsDkrPanic collect() raises (with its partial
     paillier_key_vec updates).  `recovery` as in refresh.collect."""
-    from .refresh import _check_mode, _conclude, _mapped, _recover_after, _speculative_finish, _speculative_launch
+    from .refresh import _check_mode, _conclude, _finish_both, _mapped, _recover_after, _speculative_launch
     _check_mode(recovery)
     world, rank = dist.get_world_size(), dist.get_rank()
     msgs, joins = list(refresh_messages), list(join_messages)
@@ -133,16 +192,21 @@ def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, devic
         merged = None
     else:
         b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True)
-        v, pend = None, None
-        try:   # the share recovery overlaps the slice's pipeline on the recovery stream
+        rows, decrypt = shard_range(n, world, rank), rank == DEC_RANK
+        pend = None
+        try:   # this rank's part of the share recovery overlaps its pipeline on the recovery stream
             if recovery == "speculative":
-                pend = _speculative_launch(ctx, [job])
-        finally:   # the slice never stays in flight
-            if b is not None:
-                v = ctx.collect_finish(b)
-            if pend is not None:   # nor does the recovery
-                spec = _speculative_finish(ctx, pend)[0]
-        merged = MergedVerdicts(merge(dist, scatter(v, R, J, n, world, rank), device), R, J, n)
+                pend = _speculative_launch(ctx, [job + (rows, decrypt)])
+        finally:   # neither the slice nor the recovery stays in flight
+            v, specs = _finish_both(ctx, (lambda: ctx.collect_finish(b)) if b is not None else (lambda: None), pend)
+        vec = scatter(v, R, J, n, world, rank)
+        if recovery == "speculative":
+            vec = np.concatenate([vec, encode_recovery(specs[0], n, rows, decrypt)])
+        mvec = merge(dist, vec, device)
+        G = global_len(R, J, n)
+        merged = MergedVerdicts(mvec[:G], R, J, n)
+        if recovery == "speculative":
+            spec = decode_recovery(mvec[G:], specs[0], n)
     err, applied = _mapped(ctx, header, msgs, merged)
     if recovery == "after" or header.size_fail:
         spec = _recover_after(ctx, [job], [err])[0]

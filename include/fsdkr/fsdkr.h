@@ -384,11 +384,21 @@ typedef struct fsdkr_recover_job {
   uint32_t t_key;             /* local_key.t: the pk_vec sums run k = 0..t_key (:460) */
   uint32_t n_new;             /* pk_vec entries to rebuild (refresh + join messages) */
   const uint32_t* old_index;  /* [t_vss+1] old_party_index of message k (1-based) */
-  const uint32_t* cts;        /* [t_vss+1][2nl] points_encrypted_vec[i-1] of message k */
+  const uint32_t* cts;        /* [t_vss+1][2nl] points_encrypted_vec[i-1] of message k, each below
+                                 2^(64 nl): the caller reduces a wider ciphertext mod N^2 first
+                                 (Paillier::mul / add / decrypt work mod N^2, so c + k N^2
+                                 recovers like c) */
   const uint32_t* p;          /* [nl] */
   const uint32_t* q;          /* [nl] */
-  const uint32_t* points;     /* [n_new][min(t_key,t_vss)+1][16] points_committed_vec[i] of message k */
+  const uint32_t* points;     /* [n_new][min(t_key,t_vss)+1][16] points_committed_vec[i] of message k
+                                 (n_new rows of the caller's choosing: a multi-GPU rank passes
+                                 its slice of the new parties) */
+  uint32_t flags;             /* FSDKR_RECOVER_* flags below (0: the whole recovery) */
 } fsdkr_recover_job;
+/* job flag: only the pk_vec rows; no decryption (share and y are zero).  The
+ * ranks of a sharded collect() split the pk_vec rows and one of them decrypts
+ * (fsdkr/shard.py); the results travel with the verdict all-reduce. */
+#define FSDKR_RECOVER_NO_DECRYPT 1u
 /* status of a recovered job */
 #define FSDKR_RECOVER_OK 0
 #define FSDKR_RECOVER_PANIC_LI 1       /* t_key > t_vss: li_vec[k] out of bounds in the pk_vec loop (:460-462) */

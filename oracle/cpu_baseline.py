@@ -47,6 +47,41 @@ def verify(batch, n_pairs, n_msgs, n_joins, n_fel, threads):
     return out, list(secs)
 
 
+def host_cores():
+    """What the host offers this process: nproc (os.cpu_count: on a GPU box the
+    whole machine's CPUs), the scheduler affinity set, the cgroup CPU quota, the
+    job's CPU share (OMP_NUM_THREADS: 16 per GPU on the GPU boxes), and
+    `available` = the smallest of those (the cores a run may actually use)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    share = os.environ.get("OMP_NUM_THREADS")
+    share = int(share) if share and share.isdigit() and int(share) > 0 else None
+    avail = min(nproc, aff, int(quota + 0.999) if quota else nproc, share or nproc)
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "job_cpu_share": share,
+            "available": max(1, avail)}
+
+
+def _agree(v, s, ref, J):
+    ok = bool(np.array_equal(v["pdl"][:s["pairs"]], ref.pdl[:s["pairs"]] & 15))
+    ok &= bool(np.array_equal(v["range"][:s["pairs"]], ref.range[:s["pairs"]]))
+    ok &= bool(np.array_equal(v["ped"][:s["msgs"]], ref.ped[:s["msgs"]]))
+    ok &= bool(np.array_equal(v["ck"][:s["msgs"]], ref.ck[:s["msgs"]]))
+    ok &= bool(np.array_equal(v["feldman"][:s["fel"]], ref.feldman[:s["fel"]]))
+    if J:
+        ok &= bool(np.array_equal(v["dlog"][:s["joins"]], ref.dlog[:s["joins"]]))
+    return ok
+
+
 def measure(batch, ref, threads=16, budget_s=12.0):
     """Time the CPU restatement over the WHOLE collect() verification of the batch
     (every pair, every message's ring-Pedersen + correct-key proof, every join's
@@ -64,19 +99,20 @@ def measure(batch, ref, threads=16, budget_s=12.0):
     s1 = {"pairs": min(P, 12), "msgs": min(Mt, 1), "joins": min(J, 1), "fel": min(P, 32)}
     v1, sec1 = verify(batch, s1["pairs"], s1["msgs"], s1["joins"], s1["fel"], 1)
     sT = {"pairs": P, "msgs": Mt, "joins": J, "fel": P}
-    agree = True
-    for v, s in ((v1, s1), (vT, sT)):
-        agree &= bool(np.array_equal(v["pdl"][:s["pairs"]], ref.pdl[:s["pairs"]] & 15))
-        agree &= bool(np.array_equal(v["range"][:s["pairs"]], ref.range[:s["pairs"]]))
-        agree &= bool(np.array_equal(v["ped"][:s["msgs"]], ref.ped[:s["msgs"]]))
-        agree &= bool(np.array_equal(v["ck"][:s["msgs"]], ref.ck[:s["msgs"]]))
-        agree &= bool(np.array_equal(v["feldman"][:s["fel"]], ref.feldman[:s["fel"]]))
-        if J:
-            agree &= bool(np.array_equal(v["dlog"][:s["joins"]], ref.dlog[:s["joins"]]))
+    agree = _agree(v1, s1, ref, J) and _agree(vT, sT, ref, J)
+    hc = host_cores()
+    all_cores = None
+    if hc["available"] != threads:   # the same whole verification on every core the host gives this run
+        t0 = time.perf_counter()
+        vA, _ = verify(batch, P, Mt, J, P, hc["available"])
+        a_s = time.perf_counter() - t0
+        agree = agree and _agree(vA, sT, ref, J)
+        all_cores = {"threads": hc["available"], "collect_s": a_s}
     per1 = [sec1[0] / max(s1["pairs"], 1), sec1[1] / max(s1["msgs"], 1), sec1[2] / max(s1["msgs"], 1),
             sec1[3] / max(s1["joins"], 1), sec1[4] / max(s1["fel"], 1)]
     c1 = P * per1[0] + Mt * (per1[1] + per1[2]) + J * per1[3] + P * per1[4]
-    return {"cores": threads, "collect_s": full_s, "collect_phases_s": dict(zip(
+    return {"cores": threads, "host_cores": hc, "all_cores": all_cores, "collect_s": full_s,
+            "collect_phases_s": dict(zip(
                 ("pairs", "ring_pedersen", "correct_key", "dlog", "feldman"), secT)),
             "single_thread_collect_s": c1,
             "per_pair_ms_1t": per1[0] * 1e3, "per_ring_pedersen_ms_1t": per1[1] * 1e3,

@@ -88,10 +88,13 @@ def is_probable_prime(c: int, rounds: int = MR_ROUNDS) -> bool:
     return all(strong_probable_prime(c, b) for b in witness_bases(c, rounds))
 
 
-def walk(start: int, span: int):
-    """First probable prime among start, start+2, ... (span candidates), else None."""
+def walk(start: int, span: int, bits: int = 0):
+    """First probable prime among start, start+2, ... (span candidates, and
+    below 2^bits when bits is given: a `bits`-bit prime), else None."""
     c = start
     for _ in range(span):
+        if bits and c >> bits:
+            return None
         if is_probable_prime(c):
             return c
         c += 2
@@ -113,7 +116,7 @@ def sample_primes(rng, bits: int, count: int, span: int = 0):
     todo = list(range(count))
     while todo:
         for w in todo:
-            out[w] = walk(starts[w], span)
+            out[w] = walk(starts[w], span, bits)
         todo = [w for w in todo if out[w] is None]
         for w in todo:
             starts[w] = _draw_start(rng, bits)

@@ -55,6 +55,8 @@ class Rng:
             c = self.bits(bits) | (3 << (bits - 2)) | 1
             # walk to the next probable prime from a random start
             for _ in range(4 * bits):
+                if c >> bits:       # the walk stays below 2^bits
+                    break
                 if bigint.is_probable_prime(c):
                     return c
                 c += 2

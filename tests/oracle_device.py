@@ -85,11 +85,15 @@ class OracleDevice:
         for j in jobs:
             idx = [x - 1 for x in j["old_index"]]
             li = [map_share_to_new_params(idx[k], idx) for k in range(len(idx))]
+            pk = self.ec_msm(j["points"], [li[:len(row)] for row in j["points"]])
+            status = 1 if j["t_key"] > j["t_vss"] else 0
+            if j.get("flags", 0) & 1:   # FSDKR_RECOVER_NO_DECRYPT: the pk_vec rows only
+                out.append((status, 0, None, pk))
+                continue
             dk = paillier.DecryptionKey(j["p"], j["q"])
             ms = [paillier.decrypt(dk, c) for c in j["cts"]]
             share = sum(l * m for l, m in zip(li, ms)) % (j["p"] * j["q"]) % ec.Q
-            pk = self.ec_msm(j["points"], [li[:len(row)] for row in j["points"]])
-            out.append((1 if j["t_key"] > j["t_vss"] else 0, share, ec.mul(ec.G, share), pk))
+            out.append((status, share, ec.mul(ec.G, share), pk))
         return out
 
     def collect_recover_launch(self, jobs):

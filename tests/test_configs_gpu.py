@@ -8,8 +8,8 @@
               joins' DLog proofs cross-checked with the oracle, 8 injected
               tampers -> verdict vector == the injected set, first error ==
               the oracle's;
-  configs[3]  n=256, t=128, 2048-bit (16 distinct messages tiled to 256, every
-              pair verified independently): the same injected-tamper check;
+  configs[3]  n=256, t=128, 2048-bit, 256 distinct messages: the clean batch,
+              64 sampled pairs against the oracle, the injected-tamper check;
   configs[4]  many independent t=1 n=3 sessions with 3072-bit keys in ONE
               device pass (fsdkr_verify_collect_multi / refresh.collect_many):
               per-session outcome == the oracle's, with tampers in a few
@@ -127,13 +127,22 @@ def test_config2_n64_injected_tampers(gpu_ctx, config2):
 
 
 # ------------------------------------------------------------------ configs[3]
-def test_config3_n256_injected_tampers(gpu_ctx):
+def test_config3_n256_distinct_messages(gpu_ctx):
+    """configs[3] on 256 DISTINCT refresh messages (65 536 distinct PDL + Alice
+    pairs; VERDICT r3 "what's missing" 3): the clean batch verifies, 64 randomly
+    sampled pairs verify in the oracle, and the injected tampers give exactly
+    the injected verdict set and the oracle's first error."""
     from fsdkr import synth
-    msgs, joins, lk = synth.synth_collect_tiled(gpu_ctx, 256, 128, 77, 16, key_bits=2048)
+    msgs, joins, lk = synth.synth_collect(gpu_ctx, 256, 0, 128, 77, key_bits=2048)
+    assert len({m.points_encrypted_vec[0] for m in msgs}) == 256
+    assert len({m.ring_pedersen_statement.N for m in msgs}) == 256
+    b, v = _verdicts(gpu_ctx, msgs, lk, joins)
+    tamper.check_verdicts(v, 256, 0, 256, {}, {}, {})
+    assert _first(b, v) is None
+    _sample_pairs_with_oracle(msgs, lk, 256, 64, seed=3)
     spec = [("pdl_s3", 17, 200), ("range_e", 100, 255), ("pdl_u2", 250, 3), ("rp_Z", 128, 77), ("ck", 255, 0)]
     first = _tamper_check(gpu_ctx, msgs, joins, lk, spec)
     assert first[0] == "PDLwSlackProof"
-    _sample_pairs_with_oracle(msgs, lk, 256, 8, seed=3)
 
 
 # ------------------------------------------------------------------ configs[4]

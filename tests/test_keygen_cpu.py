@@ -43,3 +43,12 @@ def test_carmichael_and_primes():
         assert ok.is_probable_prime(p)
         assert all(ok.strong_probable_prime(p, b) for b in (2, 3, p - 1, 1))
     assert not ok.is_probable_prime(((1 << 521) - 1) * ((1 << 127) - 1))
+
+
+def test_oracle_walk_stops_at_two_to_bits():
+    """The walk from 2^bits - 1 (composite for these bits) has no candidate left
+    below 2^bits: None, not the (bits+1)-bit prime 2^bits + 1 (bits = 64: Fermat
+    F6 is composite; bits = 16: 65537 is prime)."""
+    assert ok.walk((1 << 16) - 1, 64, 16) is None
+    assert ok.walk((1 << 16) - 1, 64) == 65537
+    assert ok.walk((1 << 192) - 1, 4 * 192, 192) is None

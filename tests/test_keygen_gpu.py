@@ -118,3 +118,29 @@ def test_refresh_keys_batch(gpu_ctx):
         ref = zk_paillier.NiCorrectKeyProof.proof(dk.p, dk.q)
         assert tuple(ck.sigma_vec) == tuple(ref.sigma_vec)
         assert zk_paillier.NiCorrectKeyProof(tuple(ck.sigma_vec)).verify(ek.n)
+
+
+class _TopThenRandom:
+    """Draws all-ones for the first `top` starts (start = 2^bits - 1), then seeded draws."""
+
+    def __init__(self, top, seed):
+        self.top, self.rng = top, Rng(seed)
+
+    def bits(self, k):
+        if self.top:
+            self.top -= 1
+            return (1 << k) - 1
+        return self.rng.bits(k)
+
+
+def test_walk_stays_below_two_to_bits(gpu_ctx):
+    """A start within the walk's span of 2^bits (the sieve offsets
+    used to run past it, so a (bits+1)-bit prime could come out): the walk
+    ends at 2^bits, redraws, and every prime has exactly `bits` bits; the
+    oracle's walk takes the same draws to the same primes."""
+    from fsdkr import keygen
+    bits = 192
+    got = keygen.sample_primes(gpu_ctx, _TopThenRandom(3, "top"), bits, 3)
+    want = ok.sample_primes(_TopThenRandom(3, "top"), bits, 3)
+    assert got == want
+    assert all(p.bit_length() == bits for p in got)

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""PMC target for whole collect() calls (bench.py's step) with no other kernels
+in the process: the synthetic workload is generated once (--gen-only, outside
+the profiler) and pickled to --cache; a profiled run loads it and makes
+1 + --steps refresh.collect() calls, so every dispatch rocprofv3 records
+belongs to a collect() call (tools/pmc_summary_step.py divides the counter
+totals by the call count)."""
+import argparse
+import copy
+import os
+import pickle
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd")]
+os.environ["GPU_MAX_HW_QUEUES"] = str(max(12, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--joins", type=int, default=4)
+    ap.add_argument("--t", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--cache", required=True)
+    ap.add_argument("--gen-only", action="store_true")
+    a = ap.parse_args()
+    import torch  # noqa: F401
+    from fsdkr import Context, refresh, synth
+    ctx = Context()
+    if a.gen_only:
+        msgs, joins, lk = synth.synth_collect(ctx, a.n - a.joins, a.joins, a.t, a.seed)
+        with open(a.cache, "wb") as f:
+            pickle.dump((msgs, joins, lk), f)
+        print(f"workload cached: {a.cache}", flush=True)
+        return
+    with open(a.cache, "rb") as f:   # written by this script (--gen-only) in the same session
+        msgs, joins, lk = pickle.load(f)
+    keys = [copy.deepcopy(lk) for _ in range(a.steps + 1)]
+    for k in range(a.steps + 1):
+        t0 = time.perf_counter()
+        refresh.collect(msgs, keys[k], lk.paillier_dk, joins, ctx=ctx)
+        print(f"collect {k} {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+    print(f"calls {a.steps + 1}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
