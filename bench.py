@@ -278,6 +278,8 @@ def phases(ctx, msgs, lk, joins, key_bits):
     b = CollectBatch(msgs, lk, joins, 256, key_bits, staged=True)
     ts = time.perf_counter()
     ctx.collect_prestart(b)
+    if b.stage1b():
+        ctx.collect_prestart(b)
     tp = time.perf_counter()
     b.complete()
     t1 = time.perf_counter()

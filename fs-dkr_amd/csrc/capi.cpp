@@ -183,26 +183,50 @@ uint32_t choose_window(uint32_t ebits) {
 }
 
 // Launch one modexp job whose descriptors are already in device memory.
+// Sliding-window width for an exponent of `ebits` bits: 2^(w-1) odd powers plus
+// about ebits / (w + 1) window products, fewest total (2048 bits: w = 6)
+uint32_t choose_slide_window(uint32_t ebits) {
+  uint32_t best_w = 1;
+  double best = 1e30;
+  for (uint32_t w = 1; w <= 7; ++w) {
+    const double cost = (double)(1u << (w - 1)) + (double)ebits / (double)(w + 1);
+    if (cost < best) {
+      best = cost;
+      best_w = w;
+    }
+  }
+  return best_w;
+}
+
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st, const char* table_tag,
-                       uint32_t prio, uint32_t group) {
+                       uint32_t prio, uint32_t group, uint32_t desc_flags) {
   if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
+  // sliding windows: the 4096-bit group shapes, public exponents, wave-uniform (caller)
   // a forced context setting wins (tuning, tests), except that the 32-lane shape
   // runs only where the caller asked for it (it prepared KD = 160 constants)
   uint32_t grp = c->modexp_group ? c->modexp_group : group;
   if (grp == kWideGroup && (group != kWideGroup || k32 != 128)) grp = 16;
   if (grp == kWaveGroup && k32 != 128) grp = 16;
   if (c->ct) grp = 0;   // the regular-access kernels have one shape per width
+  // sliding windows: the 4096-bit 4/8/16-lane shapes, public exponents, waves of
+  // `group` lanes uniform (caller), so only at the caller's lane count
+  // FSDKR_SLIDE=0: fixed windows (A/B; n = 64 and n = 256 whole calls within
+  // noise of each other, profiles/r04/r04h_*: fewer products, more control flow)
+  static const bool slide_off = getenv("FSDKR_SLIDE") && atoi(getenv("FSDKR_SLIDE")) == 0;
+  const bool slide = !slide_off && (desc_flags & kDescSlide) && (desc_flags & kDescOutIdx) && k32 == 128 && !c->ct &&
+                     grp == group && (grp == 4 || grp == 8 || grp == 16);
   const int KD = table_digits(k32, grp);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
     return FSDKR_E_UNSUPPORTED;
   }
   const uint32_t ebits = exp_bits ? exp_bits : 1;
-  const uint32_t w = choose_window(ebits);
+  const uint32_t w = slide ? choose_slide_window(ebits) : choose_window(ebits);
   const uint32_t nwin = (ebits + w - 1) / w;
-  uint32_t* d_table = (uint32_t*)c->buf(table_tag, sizeof(uint32_t) * (size_t)count * ((size_t)1 << w) * KD);
+  const size_t entries = slide ? ((size_t)1 << (w - 1)) + 1 : (size_t)1 << w;
+  uint32_t* d_table = (uint32_t*)c->buf(table_tag, sizeof(uint32_t) * (size_t)count * entries * KD);
   if (!d_table) {
     c->fail("device allocation failed (%u instances, window %u)", count, w);
     return FSDKR_E_OOM;
@@ -224,6 +248,8 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.prio = prio;
   a.group = grp;
   a.ct = c->ct ? 1u : 0u;
+  a.slide = slide ? 1u : 0u;
+  a.out_idx = (desc_flags & kDescOutIdx) ? reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 4 * n4) : nullptr;
   const size_t tm = c->tbeg("modexp", st);
   int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
   c->tend(tm, st);
@@ -242,6 +268,7 @@ void ModexpJob::pack(std::vector<uint8_t>& dst) const {
   const uint32_t w = choose_window(exp_bits ? exp_bits : 1);
   uint32_t* nw = reinterpret_cast<uint32_t*>(dst.data() + o + 2 * n8 + 3 * n4);
   for (size_t k = 0; k < size(); ++k) nw[k] = ebits[k] ? (ebits[k] + w - 1) / w : 1u;
+  if (!out_idx.empty()) memcpy(dst.data() + o + 2 * n8 + 4 * n4, out_idx.data(), n4);
 }
 
 // Upload a modexp descriptor set and launch it against prepared constants.

@@ -25,6 +25,7 @@ void free_ga_pre(Ctx* c) {
   if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
   if (g && g->ck_done) (void)hipEventDestroy(g->ck_done);
+  if (g && g->tz_done) (void)hipEventDestroy(g->tz_done);
   delete g;
   c->ga_pre = nullptr;
 }
@@ -203,6 +204,12 @@ int fsdkr_collect_prestart_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batc
   fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
   if (!c) return FSDKR_E_ARG;
   return fsdkr::collect_prestart_impl(c, batches, count);
+}
+
+int fsdkr_collect_prestart_rp(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count) {
+  fsdkr::Ctx* c = reinterpret_cast<fsdkr::Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  return fsdkr::collect_prestart_rp_impl(c, batches, count);
 }
 
 int fsdkr_collect_launch(fsdkr_ctx* ctx) {

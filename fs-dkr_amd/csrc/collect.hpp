@@ -260,7 +260,7 @@ struct CollectPlan {
   // modexp jobs: 0 GA (nn long), 1 GD (nl: DLog), 2 J2 (nn short), 3 J5 (nl short), 4 GC (ckl: correct key)
   static constexpr int NJOB = 5;
   size_t d_J[NJOB], x_J[NJOB];
-  uint32_t jk32[NJOB], jcount[NJOB], jbits[NJOB];
+  uint32_t jk32[NJOB], jcount[NJOB], jbits[NJOB], jflags[NJOB] = {};   // jflags: launch_modexp_desc desc_flags
   // descriptor offsets
   size_t d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_eqck, d_eqckm, d_p3nn, d_p3nl,
       d_p3m, d_ahn, d_ahc, d_alpre;
@@ -292,6 +292,10 @@ struct CollectPlan {
   // the correct-key equalities read them once ck_done has fired
   bool ck_hit = false;
   hipEvent_t ck_done = nullptr;
+  // ring-Pedersen T^Z computed by fsdkr_collect_prestart_rp (tz_hit): the RP
+  // equalities read them once tz_done has fired
+  bool tz_hit = false;
+  hipEvent_t tz_done = nullptr;
   FbJob fb;
   size_t d_FB = 0;
   uint32_t* fb_table = nullptr;
@@ -333,7 +337,24 @@ struct GaPre {
   std::vector<uint32_t> ck_n, ck_sigma;   // the inputs (zero-extended to ck_l), for the match
   uint32_t* ck_out = nullptr;             // [Mt * 11][ck_l]
   hipEvent_t ck_done = nullptr;
+  // the constants of the table chains' moduli [Ntilde_i | RP modulus_m] (rows n + m: T_m's)
+  const uint32_t* fb_cons = nullptr;
+  // ring-Pedersen T_m^Z_{m,k} of every message (fsdkr_collect_prestart_rp): the
+  // fixed-base exponents behind the prestarted T tables, rows m*M + k at width nl;
+  // prepare drops them from its fixed-base job when tz_digest and the T rows match
+  bool tz_valid = false;
+  uint32_t tz_Mt = 0, tz_M = 0;
+  uint64_t tz_digest = 0;
+  uint32_t* tz_out = nullptr;
+  const uint32_t* tz_z = nullptr;        // the device copy of the Z rows [Mt*M][tz_zl]
+  uint32_t tz_zl = 0;
+  hipEvent_t tz_done = nullptr;
 };
+
+// width-independent 64-bit digest of `rows` rows of `w` words (trailing zero
+// words ignored), order-dependent, computed in parallel (prestart and prepare
+// compare the ring-Pedersen Z rows with it)
+uint64_t rows_digest(const uint32_t* p, size_t rows, uint32_t w, uint64_t row0);
 
 // collect()'s fixed-base tables, base order [h1_i | T_m | h2_i] (FbJob::finalize
 // sizes: one entry per w exponent bits, at least one)
@@ -380,15 +401,13 @@ inline void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, ui
 // 51.5 ms per call against 8 lanes (profiles/r04/r04d_ab_lanes_v*).  Small
 // batches (multi-GPU shards) get 32 lanes (KD = 160 constants), and at most one
 // wave per SIMD (1024 chains) one wave per chain (modexp_wave_kernel), for
-// latency; batches past 16 384 chains (n = 256) keep 8 lanes.  Used by the
-// prestart and by launch().
+// latency.  Past 16 384 chains the launch fills the chip several times over and
+// the most MAC-efficient 4-lane shape wins: n = 256 (131 072 chains) 592 ms per
+// call at 8 lanes, 571 ms at 4, 628 ms at 16 (profiles/r04/r04e_ab_n256_lanes_v*).
+// 32 lanes at n = 64: 51 -> 64 ms (profiles/r04/r04g_*).
+// Used by the prestart and by launch().
 inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
-  static const int ga_env = [] {   // A/B (temporary)
-    const char* e = getenv("FSDKR_GA_G");
-    return e ? atoi(e) : 0;
-  }();
-  if (ga_env == 4 || ga_env == 8 || ga_env == 16) return (uint32_t)ga_env;
-  uint32_t g = (nn == 128 && count <= 16384u) ? 16 : 8;
+  uint32_t g = nn != 128 ? 8 : count <= 16384u ? 16 : 4;
   for (uint32_t x : {16u, kWideGroup})
     if ((uint64_t)count * x <= 65536u) g = x;
   if (g == kWideGroup && nn != 128) g = 16;
@@ -396,9 +415,56 @@ inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
   return g;
 }
 
+// J1 (s2^N_i | s^N_i mod N_i^2) regrouped so the instances of every wave share
+// their exponent N_i: stable order by exponent address (receiver), out_idx = the
+// original row.  With a scratch output row (pad_row != kNoPad) every run of one
+// exponent is padded to whole waves of `per_wave` instances with copies of its
+// last chain writing pad_row (at most per_wave - 1 per receiver); returns whether
+// every wave is then uniform (the launch may use sliding windows: kDescSlide).
+constexpr uint32_t kNoPad = 0xffffffffu;
+inline bool group_by_exponent(ModexpJob& J, uint32_t per_wave, uint32_t pad_row) {
+  const size_t cnt = J.size();
+  std::vector<uint32_t> ord(cnt);
+  for (size_t k = 0; k < cnt; ++k) ord[k] = (uint32_t)k;
+  std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return J.exp_ptr[x] < J.exp_ptr[y]; });
+  auto same = [&](uint32_t x, uint32_t y) {
+    return J.exp_ptr[x] == J.exp_ptr[y] && J.exp_len[x] == J.exp_len[y] && J.ebits[x] == J.ebits[y];
+  };
+  bool aligned = per_wave > 0;
+  for (size_t s = 0; s < cnt && aligned && pad_row == kNoPad;) {   // unpadded: every run whole waves
+    size_t e = s;
+    while (e < cnt && same(ord[e], ord[s])) ++e;
+    aligned = (e - s) % per_wave == 0;
+    s = e;
+  }
+  ModexpJob G;
+  G.k32 = J.k32;
+  auto put = [&](uint32_t k, uint32_t row) {
+    G.add(J.base_ptr[k], J.base_len[k], J.exp_ptr[k], J.exp_len[k], J.ebits[k], J.mod_idx[k]);
+    G.out_idx.push_back(row);
+  };
+  for (size_t s = 0; s < cnt;) {
+    size_t e = s;
+    while (e < cnt && same(ord[e], ord[s])) ++e;
+    for (size_t q = s; q < e; ++q) put(ord[q], J.out_idx.empty() ? ord[q] : J.out_idx[ord[q]]);
+    if (aligned && pad_row != kNoPad)
+      for (size_t q = e - s; q % per_wave; ++q) put(ord[e - 1], pad_row);
+    s = e;
+  }
+  G.exp_bits = J.exp_bits;
+  J = std::move(G);
+  return aligned;
+}
+// the descriptor flags of a regrouped GA job launched with `group` lanes
+inline uint32_t ga_desc_flags(bool aligned_for, uint32_t group) {
+  const bool slide_shape = group == 4 || group == 8 || group == 16;
+  return kDescOutIdx | ((aligned_for && slide_shape) ? kDescSlide : 0u);
+}
+
 // collect_prestart.cpp
 int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t* n_out, uint32_t* P_out);
 int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
+int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_prepare.cpp
 int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);

@@ -47,9 +47,8 @@ int collect_launch_impl(Ctx* c) {
   // instance per wave: its chain is on the critical path of the rank (J2 ->
   // inverses -> equalities); J5 (2048-bit) at 8 lanes (4 lanes measured no
   // better, profiles/r04/r04a_ab_ck_j2j5_v*)
-  uint32_t j2_group = nn == 128 ? (pl.jcount[2] <= 1024 ? kWaveGroup : pl.jcount[2] <= 16384 ? 16 : 8) : 8;
+  const uint32_t j2_group = nn == 128 ? (pl.jcount[2] <= 1024 ? kWaveGroup : pl.jcount[2] <= 16384 ? 16 : 8) : 8;
   const uint32_t j5_group = 8;
-  if (const char* e = getenv("FSDKR_J2_G")) j2_group = (uint32_t)atoi(e);   // A/B (temporary)
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;
   if (ga_group == kWideGroup && pl.jcount[0]) {
@@ -93,7 +92,7 @@ int collect_launch_impl(Ctx* c) {
   auto launch_group = [&](int k, hipStream_t ss, uint32_t pr, uint32_t group, const uint32_t* cons) -> int {
     if (!pl.jcount[k]) return FSDKR_OK;
     return launch_modexp_desc(c, pl.jk32[k], pl.jcount[k], pl.jbits[k], dev + pl.d_J[k], cons, PX(pl.x_J[k]), ss,
-                              tags[k], pr, group);
+                              tags[k], pr, group, pl.jflags[k]);
   };
   // (1) chains that need only the inputs and the moduli constants start at once
   hipEvent_t consts_ready;
@@ -209,6 +208,7 @@ int collect_launch_impl(Ctx* c) {
     (void)hipEventDestroy(ev);
   }
   if (pl.ga_hit) (void)hipStreamWaitEvent(st, pl.ga_done, 0);   // the prestarted s^N rows
+  if (pl.tz_hit) (void)hipStreamWaitEvent(st, pl.tz_done, 0);   // the prestarted ring-Pedersen T^Z rows
   // equality checks and exact products
   {
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqnn), PI(pl.d_eqnnm), cons_nn, PX(pl.x_pbits), DI(pl.o_one),

@@ -372,6 +372,36 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       voff += nc;
     }
   }
+  // a prestarted ring-Pedersen T^Z job of these messages (fsdkr_collect_prestart_rp):
+  // the same moduli, T rows and Z rows (digest), Z at the same width
+  GaPre* gtz = reinterpret_cast<GaPre*>(c->ga_pre);
+  bool tz_hit = gtz && gtz->tz_valid && gtz->nl == nl && gtz->tz_Mt == Mt && gtz->tz_M == M && gtz->tz_zl == zl &&
+                gtz->pedmod.size() == (size_t)Mt * nl && gtz->T.size() == (size_t)Mt * nl &&
+                memcmp(gtz->pedmod.data(), PEDN.data(), (size_t)Mt * nl * 4) == 0;
+  for (uint32_t s = 0; s < count && tz_hit; ++s) {
+    const Sess& x = pl.ss[s];
+    for (uint32_t lm = 0; lm < x.Mt && tz_hit; ++lm) {
+      const uint32_t* a = gtz->T.data() + (size_t)(x.mbase + lm) * nl;
+      tz_hit = memcmp(a, x.b->ped_T + (size_t)lm * x.b->nl, (size_t)x.b->nl * 4) == 0;
+      for (uint32_t k = x.b->nl; k < nl && tz_hit; ++k) tz_hit = a[k] == 0;
+    }
+  }
+  if (tz_hit) {
+    uint64_t d = 0;
+    for (uint32_t s = 0; s < count; ++s) {
+      const Sess& x = pl.ss[s];
+      d += rows_digest(x.b->ped_Z, (size_t)x.Mt * M, x.b->zl, (size_t)x.mbase * M);
+    }
+    tz_hit = d == gtz->tz_digest;
+  }
+  if (tz_hit) {
+    pl.tz_hit = true;
+    pl.tz_done = gtz->tz_done;
+    gtz->tz_valid = false;   // consumed (the buffers live until the next prestart)
+  }
+  // device address of Z row z: the prestart's copy on a hit (not uploaded again)
+  const uint32_t* const tz_z = tz_hit ? gtz->tz_z : nullptr;
+  const uint32_t* const tz_out = tz_hit ? gtz->tz_out : nullptr;
   clk.lap("dlog+maxes");
 
   // ---------------- device layout: inputs (planned; bytes written after the device allocation)
@@ -414,12 +444,12 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   const size_t o_vss = I.reserve((size_t)V * 64);
   for (const Sess& x : pl.ss) I.rows_at(o_vss + (size_t)x.vbase * 64, x.b->vss, x.V, 16, 16);
   const size_t o_pSraw = I.reserve((size_t)Mt * nl * 4), o_pT = I.reserve((size_t)Mt * nl * 4);
-  const size_t o_pA = I.reserve((size_t)Mt * M * nl * 4), o_pZ = I.reserve((size_t)Mt * M * zl * 4);
+  const size_t o_pA = I.reserve((size_t)Mt * M * nl * 4), o_pZ = tz_z ? 0 : I.reserve((size_t)Mt * M * zl * 4);
   for (const Sess& x : pl.ss) {
     I.rows_at(o_pSraw + (size_t)x.mbase * nl * 4, x.b->ped_S, x.Mt, x.b->nl, nl);
     I.rows_at(o_pT + (size_t)x.mbase * nl * 4, x.b->ped_T, x.Mt, x.b->nl, nl);
     I.rows_at(o_pA + (size_t)x.mbase * M * nl * 4, x.b->ped_A, (size_t)x.Mt * M, x.b->nl, nl);
-    I.rows_at(o_pZ + (size_t)x.mbase * M * zl * 4, x.b->ped_Z, (size_t)x.Mt * M, x.b->zl, zl);
+    if (!tz_z) I.rows_at(o_pZ + (size_t)x.mbase * M * zl * 4, x.b->ped_Z, (size_t)x.Mt * M, x.b->zl, zl);
   }
   const size_t o_pS = I.own(PEDS);
   const size_t o_cks = I.reserve((size_t)Mt * CK_M2 * ckl * 4);
@@ -512,7 +542,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   const size_t in_bytes_pre = Img::al(I.size);
   const size_t n_eqall = (size_t)P + n_eqnl + (size_t)Mt * CK_M2;
   const size_t desc_bound =
-      ((size_t)7 * P + 4 * (size_t)J + (size_t)Mt * CK_M2) * 32 +                        // modexp jobs
+      ((size_t)7 * P + 4 * (size_t)J + (size_t)Mt * CK_M2) * 32 + (size_t)3 * P * 4 +    // modexp jobs (+ GA out_idx)
+      (size_t)n * 63 * 36 +                                                                // GA pads
       (2 * (size_t)n + Mt) * 24 + (4 * (size_t)P + (size_t)Mt * M) * 32 + 24 * 512 +      // fixed-base job
       4 * (size_t)P * 8 + 4 * (size_t)P * 16 +                                            // binom, inverses
       n_eqall * (sizeof(EqOperand) + 4) + 2 * (size_t)P * sizeof(Prod3Operand) + 4 * (size_t)P +
@@ -584,7 +615,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       J9.add(DI(o_NP1 + (size_t)r * nn * 4), nn, DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, r);
     }
   clk.lap("desc pairs");
-  {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
+  if (!tz_hit) {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
     const size_t o = FB.grow((size_t)Mt * M);
     for (uint32_t m = 0; m < Mt; ++m) FB.b_bits[fb_T[m]] = std::max(FB.b_bits[fb_T[m]], std::max(z_max, 1u));
     parallel_for(Mt, 16, [&](size_t m0, size_t m1) {
@@ -592,7 +623,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
         const uint32_t b = fb_T[m], md = FB.b_mod[b];
         for (uint32_t k = 0; k < M; ++k) {
           const size_t i = o + m * M + k, z = m * M + k;
-          FB.e_ptr[i] = DI(o_pZ + z * zl * 4);
+          FB.e_ptr[i] = DI(o_pZ + z * zl * 4);   // (uploaded: no prestarted job)
           FB.e_len[i] = zl;
           FB.e_base[i] = b;
           FB.e_mod[i] = md;
@@ -634,8 +665,16 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     if (bytes) memcpy(desc.data() + at, src, bytes);
     return o;
   };
+  // GA: J1 receiver-major (every wave's chains share N_i: sliding windows when the
+  // groups fill whole waves and no J9 instance joins the launch), then J9
+  const uint32_t ga_group = ga_lanes((uint32_t)(J1.size() + J9.size()), nn);
+  // (pads write the first J9 row, unused when J9 is empty)
+  const uint32_t ga_pw = ga_group <= 64 ? 64 / ga_group : 0;
+  const bool ga_aligned = J1.size() && group_by_exponent(J1, ga_pw, J9.size() ? kNoPad : (uint32_t)(2 * P)) &&
+                          J9.size() == 0;
   ModexpJob GA = J1, GD = J7;
   GA.append(J9);
+  pl.jflags[0] = GA.out_idx.empty() ? 0u : ga_desc_flags(ga_aligned, ga_group);
   GD.append(J8);
   const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD),
                d_GC = pack_job(GC);
@@ -753,7 +792,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N; the odd part here)
       EqOperand e;
-      e.a = DX(x_RP + ((size_t)m * M + k) * nl * 4);
+      e.a = tz_out ? (uint64_t)(uintptr_t)(tz_out + ((size_t)m * M + k) * nl) : DX(x_RP + ((size_t)m * M + k) * nl * 4);
       e.b = DI(o_one);
       e.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
       e.d = DI(o_pS + (size_t)m * nl * 4);
@@ -827,7 +866,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       o = Pow2Op{};
       o.a = DI(o_pT + (size_t)m * nl * 4);
       o.a_len = nl;
-      o.ea = DI(o_pZ + ((size_t)m * M + k) * zl * 4);
+      o.ea = tz_z ? (uint64_t)(uintptr_t)(tz_z + ((size_t)m * M + k) * zl) : DI(o_pZ + ((size_t)m * M + k) * zl * 4);
       o.ea_len = zl;
       o.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
       o.c_len = nl;

@@ -120,6 +120,7 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
   if (!g.fb_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done, hipEventDisableTiming), "event")))
     return rc;
   g.fb_table = reinterpret_cast<uint32_t*>(dev + o_tab);
+  g.fb_cons = cons;
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
   FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
@@ -239,6 +240,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   g.valid = false;
   g.fb_valid = false;
   g.ck_valid = false;
+  g.tz_valid = false;
   *n_out = *P_out = 0;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
   if (running && running->launched) {
@@ -248,7 +250,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // a prepared plan that consumed the previous prestart reads its s^N rows and
   // fixed-base tables in place: this prestart overwrites (or reallocates) those
   // buffers, so the plan is dropped (a later launch reports "no prepared batch")
-  if (running && (running->ga_hit || running->fb_hit || running->ck_hit)) free_collect_plan(c);
+  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit)) free_collect_plan(c);
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prestart: no batch");
     return FSDKR_E_ARG;
@@ -286,8 +288,13 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   auto al = Img::al;
   const size_t o_NN = 0, o_rn = al((size_t)n * nn * 4), o_s2 = o_rn + al((size_t)n * nl * 4),
                o_s = o_s2 + al((size_t)P * nl * 4), o_desc = o_s + al((size_t)P * nl * 4);
-  const size_t desc_bytes = (size_t)2 * P * 32, o_out = o_desc + al(desc_bytes);
-  const size_t total = o_out + (size_t)2 * P * nn * 4;
+  // the lanes launch() would give GA: 32 lanes (KD = 160 constants) for the small
+  // batches of a multi-GPU shard, where GA's chain latency is the critical path
+  const uint32_t group = ga_lanes(2 * P, nn), per_wave = group <= 64 ? 64 / group : 0;
+  // descriptors with out_idx, for 2P chains + at most per_wave - 1 pads per receiver
+  const size_t desc_bytes = ((size_t)2 * P + (size_t)n * (per_wave ? per_wave - 1 : 0)) * 36,
+               o_out = o_desc + al(desc_bytes);
+  const size_t total = o_out + ((size_t)2 * P + 1) * nn * 4;   // + the pads' scratch row
   uint8_t* dev = (uint8_t*)c->buf("collect_ga", total);
   if (!dev) {
     c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
@@ -337,8 +344,14 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
         J1.add(DI((which == 0 ? o_s2 : o_s) + p * nl * 4), nl, DI(o_rn + r * nl * 4), nl, recvn_max, (uint32_t)r);
       }
     }
+  // receiver-major, padded to whole waves: the chains of a wave share N_i -> sliding windows
+  const uint32_t flags = ga_desc_flags(group_by_exponent(J1, per_wave, (uint32_t)(2 * P)), group);
   std::vector<uint8_t> desc;
   J1.pack(desc);
+  if (desc.size() > desc_bytes) {
+    c->fail("fsdkr_collect_prestart: GA descriptors %zu > %zu bytes", desc.size(), desc_bytes);
+    return FSDKR_E_ARG;
+  }
   memcpy(img.data() + o_desc, desc.data(), desc.size());
   hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
   StreamScope scope(c, gs);
@@ -346,9 +359,6 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, gs), "prestart H2D")) ||
       (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // img is pageable and local
     return rc;
-  // the lanes launch() would give GA: 32 lanes (KD = 160 constants) for the small
-  // batches of a multi-GPU shard, where GA's chain latency is the critical path
-  const uint32_t group = ga_lanes(2 * P, nn);
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
                          group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
@@ -361,9 +371,11 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   (void)hipEventRecord(g.ga_setup, gs);   // GA's constants are ready
   // issue priority 2: GA ends ~13 ms before the pipeline's last jobs, which need
   // the issue slots more (n = 64 median of 7 interleaved calls 56.4 -> 55.3 ms vs
-  // priority 3, profiles/r03s_ga_prio_ab.jsonl; round 2, with the PDL hash on the
-  // GPU's critical path, measured 3 faster)
-  if ((rc = launch_modexp_desc(c, nn, 2 * P, recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", 2, group)))
+  // priority 3, profiles/r03s_ga_prio_ab.jsonl; again 0.5 ms in round 4 with
+  // 16-lane GA, profiles/r04/r04g_*)
+  constexpr uint32_t ga_prio = 2;
+  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, group,
+                               flags)))
     return rc;
   if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
@@ -379,11 +391,164 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
 
 int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
   uint32_t n = 0, P = 0;
-  int rc = prestart_ga(c, bs, count, &n, &P);
-  if (rc || P == 0) return rc;
-  GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
-  if ((rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
-  return prestart_ck(c, bs, count, g);
+  int rc;
+  GaPre* gp = reinterpret_cast<GaPre*>(c->ga_pre);
+  const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
+  if (gp && gp->valid && !(running && running->launched) && ga_pre_matches(c, bs, count)) {
+    // a second call for the same batches (a caller that packed GA's fields first and
+    // started it at once, then the rest of stage 1): GA keeps running, the missing
+    // parts start now
+    n = gp->n;
+    for (const GaPre::Sess& x : gp->sess) P += x.R * x.n;
+  } else {
+    if ((rc = prestart_ga(c, bs, count, &n, &P)) || P == 0) return rc;
+    gp = reinterpret_cast<GaPre*>(c->ga_pre);
+  }
+  GaPre& g = *gp;
+  if (!g.fb_valid && (rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
+  return g.ck_valid ? FSDKR_OK : prestart_ck(c, bs, count, g);
+}
+
+uint64_t rows_digest(const uint32_t* p, size_t rows, uint32_t w, uint64_t row0) {
+  const size_t chunks = std::max<size_t>(1, std::min<size_t>(host_threads(), rows / 4096 + 1));
+  std::vector<uint64_t> part(chunks, 0);
+  parallel_for(chunks, 1, [&](size_t c0, size_t c1) {
+    for (size_t ch = c0; ch < c1; ++ch) {
+      uint64_t acc = 0;
+      for (size_t r = rows * ch / chunks; r < rows * (ch + 1) / chunks; ++r) {
+        const uint32_t* x = p + r * w;
+        int top = (int)w - 1;
+        while (top >= 0 && x[top] == 0) --top;
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ (row0 + r);
+        for (int k = 0; k <= top; ++k) h = (h ^ x[k]) * 0x100000001B3ull + (h >> 29);
+        acc += h * (2 * (row0 + r) + 1);
+      }
+      part[ch] = acc;
+    }
+  });
+  uint64_t d = 0;
+  for (uint64_t v : part) d += v;
+  return d;
+}
+
+// fsdkr_collect_prestart_rp: every message's ring-Pedersen T^Z_k (ring_pedersen_proof.rs:144)
+// as fixed-base exponents behind the prestarted T tables, once stage 1b packed Z.
+// For many small sessions (BASELINE configs[4]) the prestarted GA fills the chip
+// for one dispatch round and leaves it mostly idle until the pipeline launches;
+// these waves take that window.  (In one n = 64 collect the same early exponents
+// slowed the GA chains of the critical path, profiles/r03zc_fb_sched_variants/.)
+int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
+  GaPre* gp = reinterpret_cast<GaPre*>(c->ga_pre);
+  if (!bs || count == 0) {
+    c->fail("fsdkr_collect_prestart_rp: no batch");
+    return FSDKR_E_ARG;
+  }
+  if (!gp || !gp->fb_valid || gp->sess.size() != count || !gp->fb_cons) return FSDKR_OK;   // nothing to start behind
+  GaPre& g = *gp;
+  g.tz_valid = false;
+  const uint32_t M = bs[0].m_security, nl = g.nl, n = g.n, Mt = g.Mt;
+  uint32_t zl = 0, mt_sum = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (!b->ped_Z || !b->zl || b->m_security != M || b->ped_lens) return FSDKR_OK;
+    zl = std::max(zl, b->zl);
+    mt_sum += b->n_refresh + b->n_join;
+  }
+  if (mt_sum != Mt || !M) return FSDKR_OK;
+  // the Z rows, zero-extended to zl, in the prestart's message order; their bound
+  // must fit the T tables (sized for g.bits_z exponent bits)
+  const size_t rows = (size_t)Mt * M;
+  auto al = Img::al;
+  const size_t o_z = 0, o_out = al(rows * zl * 4), o_sched0 = o_out + al(rows * nl * 4);
+  FbJob TZ;
+  TZ.k32 = nl;
+  for (uint32_t r = 0; r < n; ++r) TZ.add_base(0, nl, r);
+  for (uint32_t m = 0; m < Mt; ++m) TZ.add_base(0, nl, n + m);
+  for (uint32_t r = 0; r < n; ++r) TZ.add_base(0, nl, r);
+  for (uint32_t r = 0; r < n; ++r) {
+    TZ.b_bits[r] = g.bits_h1;
+    TZ.b_bits[n + Mt + r] = g.bits_h2;
+  }
+  for (uint32_t m = 0; m < Mt; ++m) TZ.b_bits[n + m] = g.bits_z;
+  const size_t o0 = TZ.grow(rows);
+  // device buffer first (the descriptors hold device addresses)
+  TZ.finalize();   // b_h / b_toff / w / stride only depend on the bases
+  if (TZ.w != g.fb_w || TZ.entries != g.fb_entries) return FSDKR_OK;
+  const size_t sched_b = rows * (size_t)TZ.stride * 2;
+  const size_t o_nsteps = o_sched0 + al(sched_b), o_desc = o_nsteps + al(rows * 4);
+  const size_t desc_est = rows * 40 + (size_t)(2 * n + Mt) * 32 + 16 * 256;
+  const size_t total = o_desc + al(desc_est);
+  uint8_t* dev = (uint8_t*)c->buf("collect_tz_pre", total);
+  if (!dev) {
+    c->fail("fsdkr_collect_prestart_rp: device allocation of %zu bytes failed", total);
+    return FSDKR_E_OOM;
+  }
+  std::atomic<bool> fits{true};
+  parallel_for(Mt, 64, [&](size_t m0, size_t m1) {
+    for (size_t m = m0; m < m1; ++m)
+      for (uint32_t k = 0; k < M; ++k) {
+        const size_t i = o0 + m * M + k;
+        TZ.e_ptr[i] = (uint64_t)(uintptr_t)(dev + o_z + (m * M + k) * zl * 4);
+        TZ.e_len[i] = zl;
+        TZ.e_base[i] = n + (uint32_t)m;
+        TZ.e_mod[i] = n + (uint32_t)m;
+        TZ.o_ptr[i] = (uint64_t)(uintptr_t)(dev + o_out + (m * M + k) * nl * 4);
+      }
+  });
+  TZ.finalize();
+  std::vector<uint8_t> desc;
+  TZ.pack(desc);
+  if (desc.size() > total - o_desc) {
+    c->fail("fsdkr_collect_prestart_rp: descriptor image larger than planned");
+    return FSDKR_E_ARG;
+  }
+  hipStream_t zs = c->side_stream(10);
+  StreamScope scope(c, zs);
+  int rc;
+  // Z rows: H2D per session (contiguous when the sessions' rows are), then the digest
+  uint64_t digest = 0;
+  size_t row = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const size_t r = (size_t)(b->n_refresh + b->n_join) * M;
+    for (size_t q = 0; q < r; ++q) {
+      const uint32_t* z = b->ped_Z + q * b->zl;
+      if (hbn::bitlen(z, b->zl) > g.bits_z) fits = false;
+    }
+    if (b->zl == zl) {
+      if ((rc = c->hip_check(hipMemcpyAsync(dev + o_z + row * zl * 4, b->ped_Z, r * zl * 4, hipMemcpyHostToDevice, zs),
+                             "prestart rp Z H2D")))
+        return rc;
+    } else {   // zero-extend row by row
+      std::vector<uint32_t> tmp(r * zl, 0u);
+      for (size_t q = 0; q < r; ++q) memcpy(tmp.data() + q * zl, b->ped_Z + q * b->zl, (size_t)b->zl * 4);
+      if ((rc = c->hip_check(hipMemcpyAsync(dev + o_z + row * zl * 4, tmp.data(), tmp.size() * 4,
+                                            hipMemcpyHostToDevice, zs), "prestart rp Z H2D")) ||
+          (rc = c->hip_check(hipStreamSynchronize(zs), "prestart rp Z sync")))
+        return rc;
+    }
+    digest += rows_digest(b->ped_Z, r, b->zl, row);
+    row += r;
+  }
+  if (!fits) return c->hip_check(hipStreamSynchronize(zs), "prestart rp sync");   // prepare sizes its own tables
+  if ((rc = c->hip_check(hipMemcpyAsync(dev + o_desc, desc.data(), desc.size(), hipMemcpyHostToDevice, zs),
+                         "prestart rp desc H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(zs), "prestart rp H2D sync")))   // pageable sources
+    return rc;
+  FbDev fd{dev + o_desc, nullptr, reinterpret_cast<uint16_t*>(dev + o_sched0), reinterpret_cast<uint32_t*>(dev + o_nsteps)};
+  FbPre pre{g.fb_table, g.fb_entries, g.fb_done};
+  if ((rc = fb_launch(c, TZ, fd, g.fb_cons, zs, "fb rp prestart", nullptr, &pre))) return rc;
+  if (!g.tz_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.tz_done, hipEventDisableTiming), "event")))
+    return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.tz_done, zs), "event record"))) return rc;
+  g.tz_out = reinterpret_cast<uint32_t*>(dev + o_out);
+  g.tz_z = reinterpret_cast<const uint32_t*>(dev + o_z);
+  g.tz_zl = zl;
+  g.tz_Mt = Mt;
+  g.tz_M = M;
+  g.tz_digest = digest;
+  g.tz_valid = true;
+  return FSDKR_OK;
 }
 
 // does the prestarted GA belong to these sessions (same shapes, same inputs)?

@@ -117,6 +117,10 @@ struct ModexpJob {
   std::vector<uint32_t> base_len, exp_len;   // limbs
   std::vector<uint32_t> mod_idx;
   std::vector<uint32_t> ebits;               // per-instance exponent bit bound
+  // output row of each instance (empty: row = instance); a job laid out so the
+  // instances of every wave share their exponent (GA receiver-major) carries it
+  // and launches with sliding windows (launch_modexp_desc slide)
+  std::vector<uint32_t> out_idx;
   void add(uint64_t b, uint32_t blen, uint64_t e, uint32_t elen, uint32_t eb, uint32_t m) {
     base_ptr.push_back(b);
     base_len.push_back(blen);
@@ -128,6 +132,11 @@ struct ModexpJob {
   }
   // append another job's instances (same modulus width): one merged launch
   void append(const ModexpJob& o) {
+    const size_t base = size();
+    if (!out_idx.empty() || !o.out_idx.empty()) {   // rows of the appended part follow this job's rows
+      for (size_t k = out_idx.size(); k < base; ++k) out_idx.push_back((uint32_t)k);
+      for (size_t k = 0; k < o.size(); ++k) out_idx.push_back((uint32_t)(base + (o.out_idx.empty() ? k : o.out_idx[k])));
+    }
     base_ptr.insert(base_ptr.end(), o.base_ptr.begin(), o.base_ptr.end());
     exp_ptr.insert(exp_ptr.end(), o.exp_ptr.begin(), o.exp_ptr.end());
     base_len.insert(base_len.end(), o.base_len.begin(), o.base_len.end());
@@ -137,12 +146,16 @@ struct ModexpJob {
     if (o.exp_bits > exp_bits) exp_bits = o.exp_bits;
   }
   size_t size() const { return base_ptr.size(); }
-  size_t desc_bytes() const { return size() * (8 + 8 + 4 + 4 + 4 + 4); }
+  size_t desc_bytes() const { return size() * (8 + 8 + 4 + 4 + 4 + 4 + (out_idx.empty() ? 0 : 4)); }
   // append base_ptr | exp_ptr | base_len | exp_len | mod_idx | nwin (window of choose_window(exp_bits))
+  // [| out_idx]
   void pack(std::vector<uint8_t>& dst) const;
 };
 
 uint32_t choose_window(uint32_t ebits);
+// launch_modexp_desc desc_flags: the descriptors end with out_idx (ModexpJob.out_idx);
+// the instances of every wave share their exponent (sliding windows)
+constexpr uint32_t kDescOutIdx = 1, kDescSlide = 2;
 
 // RingPedersenProof::verify outcome from the per-index equalities and the
 // challenge-length word of ped_hash (ring_pedersen_proof.rs:136-153): checks run
@@ -161,7 +174,8 @@ int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, ui
                       uint32_t group = 0);
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st = nullptr,
-                       const char* table_tag = "mxtable", uint32_t prio = 0, uint32_t group = 0);
+                       const char* table_tag = "mxtable", uint32_t prio = 0, uint32_t group = 0,
+                       uint32_t desc_flags = 0);
 // group: kWideGroup prepares the KD = 160 constants of the 32-lane 4096-bit shape
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
                  uint32_t group = 0);

@@ -16,6 +16,7 @@ static int fb_group(Ctx* c, size_t count) {
   if (c->modexp_group == 2 || c->modexp_group == 4 || c->modexp_group == 8) return (int)c->modexp_group;
   constexpr size_t kLaneCapacity = 256ull * 4 * 2 * 64;   // CUs x SIMDs x resident waves x lanes
   // 4 lanes (L = 18, no in-cycle normalisation) is the most efficient per MAC
+  // (8 lanes at n = 64: no faster, profiles/r04/r04g_*)
   return count * 8 <= kLaneCapacity ? 8 : 4;
 }
 

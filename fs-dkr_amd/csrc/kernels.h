@@ -35,6 +35,10 @@ struct ModexpArgs {
   uint32_t group;            // lanes per instance (0 = choose by batch size)
   uint32_t ct;               // 1: regular access for secret exponents (every window-table read
                              // scans the whole table; every instance runs `nwin` windows)
+  uint32_t slide;            // 1: sliding windows of up to `window` bits (odd-power table of
+                             // 2^(window-1) + 1 entries); the caller guarantees that the
+                             // instances of every wave share their exponent (modexp_slide_kernel)
+  const uint32_t* out_idx;   // [count] output row of each instance (nullptr: row = instance)
 };
 
 int shape_digits(uint32_t k32);   // KD for a K32-limb modulus class (0 if unsupported)

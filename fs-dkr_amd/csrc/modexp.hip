@@ -237,7 +237,156 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
   __builtin_amdgcn_wave_barrier();
   lds_put<KD, G>(stream, acc, g);
   __builtin_amdgcn_wave_barrier();
-  uint32_t* O = a.out + (size_t)inst * K32;
+  uint32_t* O = a.out + (size_t)(a.out_idx ? a.out_idx[inst] : inst) * K32;
+  constexpr int LO = K32 / G;
+#pragma unroll
+  for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
+}
+
+// Sliding-window exponentiation for launches whose instances share their
+// exponent within every wave (ModexpArgs.slide): the 2R chains s^N_i of
+// receiver i in GA (the host orders them receiver-major), or a shared-exponent
+// batch.  The schedule -- the odd powers x, x^3, .., x^(2^w - 1) (one squaring
+// and 2^(w-1) - 1 products), then per 1 bit of the exponent a window of up to w
+// bits ending in a 1 bit (its squarings and ONE product), a squaring per 0 bit
+// between windows -- depends only on the exponent bits, so every lane of the
+// wave takes the same path.  For a 2048-bit exponent at w = 6: 2048 squarings
+// and ~325 other products instead of 2045 + 441 (fixed 5-bit windows).  Results
+// are bit-identical to base^exp mod N.
+template <int KD, int G, int K32, bool QS>
+__global__ __launch_bounds__(BLOCK) void modexp_slide_kernel(const ModexpArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = cons_stride(KD);
+  static_assert(!QS || scaled_ok(KD, K32), "quotient-scaled chains: N' within R/4");
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * (blockDim.x / G) + li;
+  if (inst >= a.count) return;
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  uint32_t* stream = lds + li * KD;
+  const uint32_t* C0 = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  const uint32_t* C = QS ? C0 + cons_scaled(KD) : C0;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
+  M.ninv = C[3 * KD];
+  const uint32_t w = a.window, tw = 1u << (w - 1);   // odd powers T[0..tw), x^2 at T[tw]
+  uint32_t* T = a.table + (size_t)inst * (tw + 1) * KD;
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[inst]);
+  const int exp_limbs = (int)a.exp_len[inst];
+  auto bit = [&](int i) -> uint32_t { return (E[i >> 5] >> (i & 31)) & 1u; };
+  int top = 32 * exp_limbs - 1;
+  while (top >= 0 && E[top >> 5] == 0) top = (top & ~31) - 1;   // skip zero limbs
+  while (top >= 0 && !bit(top)) --top;
+  // the window that ends the run of bits at i (bit i set): lowest set bit jl >= i - w + 1
+  auto window = [&](int i, int* jl) -> uint32_t {
+    int j = max(i - (int)w + 1, 0);
+    while (!bit(j)) ++j;
+    uint32_t d = 0;
+    for (int k = i; k >= j; --k) d = (d << 1) | bit(k);
+    *jl = j;
+    return d;   // odd
+  };
+  uint32_t acc[L];
+  const uint32_t* B = reinterpret_cast<const uint32_t*>(a.base_ptr[inst]);
+  const int blen = (int)min(a.base_len[inst], (uint32_t)K32);
+#pragma unroll
+  for (int j = 0; j < L; ++j) acc[j] = digit_of(B, blen, g * L + j);
+  auto load = [&](const uint32_t* row) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[j] = row[g * L + j];
+  };
+  auto store = [&](uint32_t* row) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) row[g * L + j] = acc[j];
+  };
+  // phase 0: x = base * R^2;  1: x^2;  2: T[jt] = T[jt-1] * x^2;  3: the windows
+  int phase = top < 0 ? 4 : 0, i = top, pend_mul = -1;
+  uint32_t jt = 1, pend_sq = 0;
+  if (top < 0) load(C + KD);   // exponent 0: the Montgomery one
+  while (phase < 4) {
+    const uint32_t* src = nullptr;
+    bool sq = false;
+    if (phase == 0) {
+      src = C + 2 * KD;
+    } else if (phase == 1) {
+      sq = true;
+    } else if (phase == 2) {
+      src = T + (size_t)tw * KD;
+    } else if (pend_sq) {
+      sq = true;
+      --pend_sq;
+    } else if (pend_mul >= 0) {
+      src = T + (size_t)pend_mul * KD;
+      pend_mul = -1;
+    } else if (i < 0) {
+      break;
+    } else if (!bit(i)) {
+      sq = true;
+      --i;
+    } else {
+      int jl;
+      const uint32_t d = window(i, &jl);
+      pend_sq = (uint32_t)(i - jl + 1);
+      pend_mul = (int)(d >> 1);
+      i = jl - 1;
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (sq) lds_put<KD, G>(stream, acc, g);
+    else {
+#pragma unroll
+      for (int j = 0; j < L; ++j) stream[g * L + j] = src[g * L + j];
+    }
+    __builtin_amdgcn_wave_barrier();
+    if constexpr (QS) {
+      if (sq) M.sqr_s(acc, acc, stream);
+      else M.mul_s(acc, acc, stream);
+    } else {
+      if (sq) M.sqr(acc, acc, stream);
+      else M.mul(acc, acc, stream);
+    }
+    if (phase == 0) {
+      store(T);
+      phase = 1;
+    } else if (phase == 1) {
+      store(T + (size_t)tw * KD);
+      load(T);
+      phase = tw > 1 ? 2 : 3;
+    } else if (phase == 2) {
+      store(T + (size_t)jt * KD);
+      if (++jt == tw) phase = 3;
+    }
+    if (phase == 3 && i == top) {   // the first window: its odd power, no squarings of 1
+      int jl;
+      const uint32_t d = window(i, &jl);
+      load(T + (size_t)(d >> 1) * KD);
+      i = jl - 1;
+    }
+  }
+  // exit: acc * 1 / R, modulo N itself for quotient-scaled chains
+  if constexpr (QS) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
+    M.ninv = C0[3 * KD];
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
+  __builtin_amdgcn_wave_barrier();
+  M.mul(acc, acc, stream);
+  M.carry_exact(acc);
+  M.sub_if_ge(acc);
+  __builtin_amdgcn_wave_barrier();
+  lds_put<KD, G>(stream, acc, g);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* O = a.out + (size_t)(a.out_idx ? a.out_idx[inst] : inst) * K32;
   constexpr int LO = K32 / G;
 #pragma unroll
   for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
@@ -328,7 +477,7 @@ __global__ __launch_bounds__(64) void modexp_wave_kernel(const ModexpArgs a) {
   M.sub_if_ge(acc);
   lds_put<KD, 64>(lds, acc, g);
   __builtin_amdgcn_wave_barrier();
-  uint32_t* O = a.out + (size_t)inst * K32;
+  uint32_t* O = a.out + (size_t)(a.out_idx ? a.out_idx[inst] : inst) * K32;
   for (int q = g; q < K32; q += 64) O[q] = limb_of(lds, KR, q);
 }
 
@@ -355,6 +504,16 @@ static hipError_t launch_modexp(const ModexpArgs& a, hipStream_t st) {
   const uint32_t blocks = (a.count + ipb - 1) / ipb;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((modexp_kernel<KD, G, K32, CT, QS>), dim3(blocks), dim3(bs), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int KD, int G, int K32, bool QS>
+static hipError_t launch_modexp_slide(const ModexpArgs& a, hipStream_t st) {
+  const uint32_t bs = block_threads(a.count * G);
+  const uint32_t ipb = bs / G;
+  const uint32_t blocks = (a.count + ipb - 1) / ipb;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((modexp_slide_kernel<KD, G, K32, QS>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
@@ -445,6 +604,14 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
     qs_env = (e && e[0] == '0') ? 0 : 1;
   }
   const bool qs = qs_env == 1;
+  if (a.slide) {   // shared exponent per wave: the 4096-bit shapes of GA
+    if (k32 != 128 || a.ct || a.group == kWideGroup || a.group == kWaveGroup) return hipErrorInvalidValue;
+    switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
+      case 16: return qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st);
+      case 8: return qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st);
+      default: return launch_modexp_slide<144, 4, 128, false>(a, st);
+    }
+  }
   switch (k32) {
     case 32:   // 1024-bit primes of key generation: L = 9 (4 lanes) or 18
       return pick_group(a.count, (int)a.group, {2, 4}, 4) == 2 ? launch_modexp<36, 2, 32>(a, st)

@@ -625,23 +625,32 @@ int RecoverPending::finish(Ctx* c, fsdkr_recovered* out) {
       if (X.no_dec) continue;
       const uint32_t nl = X.nl;
       const uint32_t* h = widths[X.width].out;
-      // kzen-paillier CRT decryption with g = N + 1: h_p = L_p(g^(p-1) mod p^2)^-1 = p - q^-1 mod p
+      // kzen-paillier CRT decryption with g = N + 1: h_p = L_p(g^(p-1) mod p^2)^-1 = p - q^-1 mod p.
+      // The reference decrypts C = Enc(0) prod_k c_k^l_k once; per CRT half that is
+      // sum_k l_k L_p(c_k^(p-1)) h_p mod p (L_p is a homomorphism on units), and 0
+      // when p divides some c_k (then p | C, C^(p-1) = 0 mod p^2 and L_p(0) =
+      // (0 - 1) / p truncates to 0).  Units give (sum_k l_k m_k) mod N exactly.
       const hbn::Limbs hp = hbn::sub(X.P, X.qinv), hq = hbn::sub(X.Q, X.pinv);
-      const hbn::Limbs N = hbn::mul(X.P, X.Q);
-      hbn::Limbs acc;
+      hbn::Limbs acc_p, acc_q;
+      bool zero_p = false, zero_q = false;
       for (uint32_t k = 0; k < X.T; ++k) {
         const size_t i = X.dec_at + k;
         const hbn::Limbs up = hbn::from(h + (2 * i) * nl, nl), uq = hbn::from(h + (2 * i + 1) * nl, nl);
+        zero_p = zero_p || up.empty();
+        zero_q = zero_q || uq.empty();
         const hbn::Limbs mp = hbn::mulmod(hbn::div_exact(hbn::sub(up.empty() ? one : up, one), X.P), hp, X.P);
         const hbn::Limbs mq = hbn::mulmod(hbn::div_exact(hbn::sub(uq.empty() ? one : uq, one), X.Q), hq, X.Q);
-        // m = mq + q * ((mp - mq) q^-1 mod p)
-        const hbn::Limbs mqp = hbn::mod(mq, X.P);
-        const hbn::Limbs d = hbn::cmp(mp, mqp) >= 0 ? hbn::sub(mp, mqp) : hbn::sub(hbn::add(mp, X.P), mqp);
-        const hbn::Limbs m = hbn::add(mq, hbn::mul(X.Q, hbn::mulmod(d, X.qinv, X.P)));
-        acc = hbn::add(acc, hbn::mul(X.li[k], m));
+        acc_p = hbn::add(acc_p, hbn::mul(X.li[k], mp));
+        acc_q = hbn::add(acc_q, hbn::mul(X.li[k], mq));
       }
-      // new share = (sum_k l_k m_k mod N) mod q (one decryption of the summed ciphertext)
-      const hbn::Limbs share = hbn::mod(hbn::mod(acc, N), Qs);
+      const hbn::Limbs mp = zero_p ? hbn::Limbs{} : hbn::mod(acc_p, X.P);
+      const hbn::Limbs mq = zero_q ? hbn::Limbs{} : hbn::mod(acc_q, X.Q);
+      // m = mq + q * ((mp - mq) q^-1 mod p)
+      const hbn::Limbs mqp = hbn::mod(mq, X.P);
+      const hbn::Limbs d = hbn::cmp(mp, mqp) >= 0 ? hbn::sub(mp, mqp) : hbn::sub(hbn::add(mp, X.P), mqp);
+      const hbn::Limbs m = hbn::add(mq, hbn::mul(X.Q, hbn::mulmod(d, X.qinv, X.P)));
+      // new share = the decrypted sum (in [0, N)) mod q
+      const hbn::Limbs share = hbn::mod(m, Qs);
       hbn::store(share, O.share, 8);
       if (!g_mul(share, O.y)) ec_ok = false;
     }

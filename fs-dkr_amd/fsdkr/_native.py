@@ -147,6 +147,8 @@ def lib():
     L.fsdkr_collect_prepare_multi.restype = ctypes.c_int
     L.fsdkr_collect_prestart_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
     L.fsdkr_collect_prestart_multi.restype = ctypes.c_int
+    L.fsdkr_collect_prestart_rp.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
+    L.fsdkr_collect_prestart_rp.restype = ctypes.c_int
     L.fsdkr_collect_finish_multi.argtypes = [vp, ctypes.POINTER(VerdictsC), ctypes.c_uint32]
     L.fsdkr_collect_finish_multi.restype = ctypes.c_int
     L.fsdkr_verify_collect_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32,
@@ -389,6 +391,13 @@ class Context:
         if arr is not None:
             self._prestart_keep = sset
             self.check(self._lib.fsdkr_collect_prestart_multi(self._h, arr, sset.n_prestart))
+
+    def collect_prestart_rp_set(self, sset):
+        """Start the ring-Pedersen T^Z exponents of a SessionSet whose stage 1b
+        (SessionSet.stage_z) packed Z, behind the prestarted T tables."""
+        arr = sset.prestart_array()
+        if arr is not None:
+            self.check(self._lib.fsdkr_collect_prestart_rp(self._h, arr, sset.n_prestart))
 
     def collect_prepare_set(self, sset):
         """Prepare every live session of a fsdkr.batch.SessionSet as ONE device image."""

@@ -195,14 +195,16 @@ class CollectBatch:
     reads is packed (counts, party indices, lengths, ek.n)."""
 
     def __init__(self, refresh_messages, local_key, join_messages, m_security=256, key_bits=2048, n_recv=None,
-                 header_only=False, staged=False, ck_stage1=False):
+                 header_only=False, staged=False, ck_stage1=False, split_stage1=True):
         """n_recv: receivers (default R + J); a multi-GPU shard passes its slice of the
         messages together with the full receiver count.  staged: pack only the
         fields fsdkr_collect_prestart reads (recv_n, pdl s2, range-proof s; see
         ga_ready) and leave the rest to complete().  ck_stage1: stage 1 also packs
         ek.n and sigma, so the prestart runs the correct-key job beside GA (at
         n = 64 it competed with GA's chains: 56.2 -> 59.0 ms median,
-        profiles/r04/r04a_ab_ck_j2j5_v0/v1)."""
+        profiles/r04/r04a_ab_ck_j2j5_v0/v1).  split_stage1: stage 1 packs only
+        GA's fields; stage1b() the table bases and exponents (complete() packs
+        them if stage1b() never ran)."""
         msgs, joins = list(refresh_messages), list(join_messages)
         R, J = len(msgs), len(joins)
         n = n_recv if n_recv else R + J
@@ -286,15 +288,19 @@ class CollectBatch:
                                               "ped_T", "ped_N")))
         nl_ga = 64 if ga_bits <= 2048 else 96 if ga_bits <= 3072 else None
         self._ga = None
+        self._stage1b = None
         if staged and nl_ga is not None:
             Gs = _Gather()
-            names = ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s", "ped_T", "ped_N",
-                     "pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
+            # GA's own fields first when split: GA starts after converting 2Rn + n
+            # values instead of every stage-1 field (stage1b() packs the rest; n = 64
+            # whole call 0.5-1.2 ms shorter, profiles/r04/r04g_*, r04h_*)
+            names = ("recv_n", "pdl_s2", "rp_s") + (() if split_stage1 else _STAGE1B)
+            self._stage1b = _STAGE1B if split_stage1 else None
             ga = {name: Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c)) for name in names}
             # the correct-key job (sigma^n mod n) reads only ek.n and sigma: stage 1
             # packs them at the width complete() gives them, so the prestart runs
             # it beside GA (csrc/collect_prestart.cpp prestart_ck)
-            ck_pre = ck_stage1 and not ck_short
+            ck_pre = ck_stage1 and not ck_short and not split
             if ck_pre:
                 c.ckl = max(ckl, nl_ga)
                 ga["ck_n"] = Gs.slot(f_ckn, c.ckl)
@@ -373,6 +379,24 @@ class CollectBatch:
         self.nl = nl
         return self
 
+    def stage1b(self):
+        """The rest of stage 1 (the fixed-base tables' bases and the exponents
+        that size them) when GA's fields went first; True when it packed them
+        (fsdkr_collect_prestart may then run again: GA keeps running and the
+        tables start)."""
+        if not self._stage1b or self._pending is None or self._ga is None:
+            return False
+        F, c = self._pending["F"], self.c
+        nl_ga, ga = self._ga
+        Gs = _Gather()
+        for name in self._stage1b:
+            ga[name] = Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c))
+        Gs.run()
+        for name in self._stage1b:
+            setattr(c, name, self._k(ga[name]))
+        self._stage1b = None
+        return True
+
     @property
     def ga_ready(self):
         """Stage 1 packed the prestart fields (fsdkr_collect_prestart may run)."""
@@ -392,6 +416,10 @@ class CollectBatch:
             raise RuntimeError(f"fsdkr_collect_first_error failed ({rc})")
         return err
 
+
+# stage-1 fields after GA's own (recv_n, pdl_s2, rp_s): the fixed-base tables'
+# bases and the exponents that size them
+_STAGE1B = ("recv_ntilde", "recv_h1", "recv_h2", "ped_T", "ped_N", "pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
 
 # stage-1 fields whose slot width does not depend on nl
 _STAGE1_WIDTH = {"pdl_s1": lambda c: c.s1l, "rp_s1": lambda c: c.s1l, "pdl_s3": lambda c: c.s3l,
@@ -471,6 +499,7 @@ class SessionSet:
         self.structs = np.zeros(len(self.live), dtype=_BATCH_DT)
         self.row = {s: r for r, s in enumerate(self.live)}
         self._pre, self.n_prestart = None, 0
+        self._z = None   # stage 1b: (Z rows array, max bits), reused by stage 2
         self._pending = (sessions, reg, M, key_bits)
         # the prestart covers the set only when every prepared session is regular
         # (prepare_multi's session list must equal the prestart's)
@@ -554,6 +583,27 @@ class SessionSet:
             st["ck_sigma"] = np.uint64(self._k(a_sig)) + starts(n * M2) * np.uint64(ckl * 4)
         self._pre, self.n_prestart = st, len(reg)
 
+    def stage_z(self):
+        """Stage 1b of a staged set: the ring-Pedersen Z rows of every regular
+        session (the largest field: 0.3 GB at configs[4]), packed at the width
+        stage 2 gives them and reused there, for fsdkr_collect_prestart_rp.
+        Returns whether the prestart rows now carry them."""
+        if self._pre is None or self._pending is None:
+            return False
+        sessions, reg, M, key_bits = self._pending
+        ses = [sessions[s] for s in reg]
+        G = _Gather(self._owned)
+        f_z = G.rows([m.ring_pedersen_proof for ms, lk, js in ses for m in ms + js], "Z", M)
+        zl = _limbs_for(max(1, f_z[1]))
+        a_z = G.slot(f_z, zl)
+        G.run()
+        n = self._pre["n_refresh"].astype(np.int64) + self._pre["n_join"].astype(np.int64)
+        starts = np.concatenate([[0], np.cumsum(n * M)[:-1]]).astype(np.uint64)
+        self._pre["ped_Z"] = np.uint64(self._k(a_z)) + starts * np.uint64(zl * 4)
+        self._pre["zl"] = zl
+        self._z = (a_z, f_z[1])
+        return True
+
     def prestart_array(self):
         """fsdkr_collect_batch rows for fsdkr_collect_prestart_multi (None: nothing to start)."""
         if self._pre is None:
@@ -595,7 +645,8 @@ class SessionSet:
         # regular sessions hold full-length vectors (_regular): flattened in C
         rpp = [m.ring_pedersen_proof for m in am]
         F["ped_A"] = G.rows(rpp, "A", M)
-        F["ped_Z"] = G.rows(rpp, "Z", M)
+        if self._z is None:   # (stage 1b packed Z already: reused below)
+            F["ped_Z"] = G.rows(rpp, "Z", M)
         f_ckn = G.field([m.ek.n for m in am])
         f_sig = G.rows([m.dk_correctness_proof for m in am], "sigma_vec", M2)
         if joins:
@@ -617,12 +668,15 @@ class SessionSet:
         nl = 64 if nl_bits <= 2048 else 96 if nl_bits <= 3072 else None
         if nl is None:
             raise UnsupportedInput(f"{nl_bits}-bit value in a 3072-bit slot")
+        z_bits = self._z[1] if self._z is not None else bits("ped_Z")
         W = {"nl": nl, "ckl": max(ckl, nl), "s1l": _limbs_for(bits("pdl_s1", "rp_s1")),
              "s3l": _limbs_for(bits("pdl_s3", "rp_s2")), "el": _limbs_for(bits("rp_e")),
-             "zl": _limbs_for(bits("ped_Z")), "yl": _limbs_for(bits("dlog_y1", "dlog_y2"))}
+             "zl": _limbs_for(max(1, z_bits)), "yl": _limbs_for(bits("dlog_y1", "dlog_y2"))}
         width = {"enc": 2 * nl, "pdl_u2": 2 * nl, "pdl_s1": W["s1l"], "rp_s1": W["s1l"], "pdl_s3": W["s3l"],
                  "rp_s2": W["s3l"], "rp_e": W["el"], "ped_Z": W["zl"], "dlog_y1": W["yl"], "dlog_y2": W["yl"]}
         arrs = {name: G.slot(f, width.get(name, nl)) for name, f in F.items()}
+        if self._z is not None:
+            arrs["ped_Z"] = self._z[0]
         arrs["ck_n"] = G.slot(f_ckn, W["ckl"])
         arrs["ck_sigma"] = G.slot(f_sig, W["ckl"])
         G.run()

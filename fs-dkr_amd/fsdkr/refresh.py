@@ -243,6 +243,8 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     batch = CollectBatch(msgs, local_key, joins, m_security, key_bits, staged=True)
     if batch.ga_ready:
         ctx.collect_prestart(batch)
+        if batch.stage1b():   # the tables' fields after GA's: GA keeps running, the tables start
+            ctx.collect_prestart(batch)
     spec, verdicts, pend = None, None, None
     batch.complete()
     if not batch.header_only:
@@ -280,6 +282,8 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="sp
     sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits, staged=True)
     if sset.n_prestart:   # every session's s2^N, s^N mod N^2 chains start while the rest is packed
         ctx.collect_prestart_set(sset)
+        if sset.stage_z():   # then the ring-Pedersen T^Z exponents behind the T tables
+            ctx.collect_prestart_rp_set(sset)
     sset.complete()
     live = sset.live
     specs = [None] * len(sess)
@@ -338,6 +342,8 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
         batch = CollectBatch(msgs, lk0, joins, m_security, key_bits, staged=True)
         if batch.ga_ready:
             ctx.collect_prestart(batch)
+            if batch.stage1b():
+                ctx.collect_prestart(batch)
         jobs = [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members]
         specs = [None] * len(members)
         verdicts, pend = None, None

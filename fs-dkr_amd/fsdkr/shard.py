@@ -162,6 +162,8 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
         return None, None
     if b.ga_ready and hasattr(ctx, "collect_prestart"):   # the long chains start while stage 2 packs
         ctx.collect_prestart(b)
+        if b.stage1b():
+            ctx.collect_prestart(b)
     b.complete()
     ctx.collect_prepare(b)
     ctx.collect_launch()

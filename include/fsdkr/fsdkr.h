@@ -230,7 +230,11 @@ int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
  * fsdkr_collect_prepare of a single batch with equal values of those fields
  * reuses the results (anything else recomputes them).  Fails with FSDKR_E_ARG
  * while a launched batch is not finished.  Does not validate: a batch it cannot
- * start is left to prepare. */
+ * start is left to prepare.  The fixed-base tables (recv_ntilde, recv_h1,
+ * recv_h2, ped_T, ped_N and the exponent widths) and the correct-key job (ck_n,
+ * ck_sigma) start too when present.  Called again with the same GA fields while
+ * those chains run (a caller that packed them first), it leaves GA running and
+ * starts only the parts that are new. */
 int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
 
 /* ---- Many independent collect() calls in ONE device pass -------------------
@@ -257,6 +261,15 @@ int fsdkr_collect_finish_multi(fsdkr_ctx* ctx, fsdkr_verdicts* out, uint32_t cou
  * (sigma_k^n mod n, zk-paillier NiCorrectKeyProof::verify).  Each part is
  * reused only if prepare's values match it exactly. */
 int fsdkr_collect_prestart_multi(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count);
+/* After fsdkr_collect_prestart[_multi] started the fixed-base tables: every
+ * message's ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144) as fixed-base
+ * exponents behind the T tables, from ped_Z / zl / m_security of the same
+ * batches (no ped_lens).  The Z rows are copied to the device before the call
+ * returns.  A later prepare of batches with the same T, N and Z rows (compared
+ * by a 64-bit digest of the Z rows) reads these results instead of computing
+ * them, and takes the Z rows from the prestart's copy.  Does nothing when the
+ * tables were not prestarted or an exponent exceeds their bound. */
+int fsdkr_collect_prestart_rp(fsdkr_ctx* ctx, const fsdkr_collect_batch* batches, uint32_t count);
 
 /* FsDkrError variants, in error.rs declaration order (error.rs:6-60). */
 #define FSDKR_ERR_NONE 0

@@ -53,13 +53,27 @@ def add(ek: EncryptionKey, c1: int, c2: int) -> int:
     return c1 * c2 % ek.nn
 
 
+def _l_trunc(u: int, n: int) -> int:
+    """L(u) = (u - 1) / n with BigInt division (truncating toward zero): L(0) = 0."""
+    v = u - 1
+    return v // n if v >= 0 else -((-v) // n)
+
+
 def decrypt(dk: DecryptionKey, c: int) -> int:
-    """m = L(c^lambda mod n^2) * mu mod n (kzen-paillier computes the same value
-    through CRT; both are the unique m of c = (1+n)^m r^n)."""
-    n = dk.p * dk.q
-    nn = n * n
-    lam = (dk.p - 1) * (dk.q - 1)
-    u = bigint.mod_pow(c, lam, nn)
-    L = (u - 1) // n
-    mu = pow(lam, -1, n)
-    return L * mu % n
+    """kzen-paillier's CRT decryption [dep, published algorithm]: per prime,
+    m_p = L_p(c^(p-1) mod p^2) h_p mod p with h_p = L_p(g^(p-1) mod p^2)^-1,
+    g = n + 1, then m = m_q + q ((m_p - m_q) q^-1 mod p).  For a unit c this is
+    the unique m of c = (1+n)^m r^n (= L(c^lambda) mu mod n); for p | c the p
+    half is L_p(0) h_p = 0 (truncating division), which fixes the reference's
+    decryption of a non-unit ciphertext sum (JoinMessage::collect has no PDL
+    check that would have rejected such a ciphertext first)."""
+    p, q = dk.p, dk.q
+    n = p * q
+    out = []
+    for a in (p, q):
+        aa = a * a
+        h = pow(_l_trunc(bigint.mod_pow((n + 1) % aa, a - 1, aa), a), -1, a)
+        d = bigint.mod_pow(c % aa, a - 1, aa)
+        out.append(_l_trunc(d, a) * h % a)
+    mp, mq = out
+    return mq + q * ((mp - mq) * pow(q, -1, p) % p)

@@ -210,3 +210,42 @@ def test_config4_prestart_hit_and_miss(gpu_ctx):
     assert base == [0] * 6
     assert run(bad) == base      # stale prestart: recomputed
     assert run(work) == base     # matching prestart: consumed
+
+
+def test_config4_prestarted_ring_pedersen_hit_and_miss(gpu_ctx):
+    """fsdkr_collect_prestart_rp (the T^Z exponents behind the prestarted T
+    tables, from stage 1b's Z rows): a prestart over Z rows that differ in one
+    message must not leak into the prepare of the real set (whose one tampered
+    Z must still be caught in the right session), and a matching prestart gives
+    the same verdicts as no prestart."""
+    import dataclasses
+    from fsdkr import synth
+    from fsdkr.batch import SessionSet
+    sessions = synth.synth_sessions(gpu_ctx, 6, n=3, t=1, seed=321, key_bits=3072)
+    work = [(m, lk, j) for m, j, lk, dk in sessions]
+    other = copy.deepcopy(work)
+    rp = other[2][0][0].ring_pedersen_proof
+    other[2][0][0].ring_pedersen_proof = dataclasses.replace(rp, Z=(rp.Z[0] + 1,) + tuple(rp.Z[1:]))
+    bad = copy.deepcopy(work)            # the set whose session 5 carries a bad Z
+    rp = bad[5][0][1].ring_pedersen_proof
+    bad[5][0][1].ring_pedersen_proof = dataclasses.replace(rp, Z=tuple(rp.Z[:9]) + (rp.Z[9] + 1,) + tuple(rp.Z[10:]))
+
+    def run(target, prestart_of):
+        if prestart_of is not None:
+            pre = SessionSet(prestart_of, 256, 3072, staged=True)
+            gpu_ctx.collect_prestart_set(pre)
+            assert pre.stage_z()
+            gpu_ctx.collect_prestart_rp_set(pre)
+        sset = SessionSet(target, 256, 3072)
+        gpu_ctx.collect_prepare_set(sset)
+        gpu_ctx.collect_launch()
+        v = gpu_ctx.collect_finish_set(sset)
+        return [sset.first_error(s, v).variant for s in range(6)]
+    base = run(work, None)
+    assert base == [0] * 6
+    assert run(work, other) == base        # stale T^Z prestart: recomputed
+    assert run(work, work) == base         # matching: consumed
+    want = run(bad, None)
+    assert want[5] != 0 and want[:5] == [0] * 5
+    assert run(bad, bad) == want           # consumed, the tamper still caught
+    assert run(bad, work) == want          # a prestart of the clean Z: must not hide it

@@ -389,3 +389,63 @@ def test_recovery_orders_agree(gpu_ctx, dkr5):
     assert a[5] == b[5] == [None, None]
     with pytest.raises(ValueError):
         refresh.collect(msgs, keys[0].clone(), dks[0], [], ctx=gpu_ctx, recovery="later")
+
+
+def test_join_collect_non_unit_ciphertext(gpu_ctx):
+    """JoinMessage::collect decrypts without a PDL check (add_party_message.rs:183-213),
+    so a refresh message may carry, for the joiner, a ciphertext divisible by the
+    joiner's p.  The reference decrypts Enc(0) * prod_k c_k^l_k once
+    with kzen-paillier's CRT decryption: p divides the product, so the p half is
+    L_p(0) h_p = 0 (truncating division); the product's per-half recovery
+    (csrc/recover.cpp) and the oracle (oracle/paillier.decrypt) both follow it.
+    The decomposition sum_k l_k Dec(c_k) would have kept the other messages'
+    p halves.  (kzen-paillier's own source is not in the image: parity with it
+    is pinned only by this restatement.)"""
+    from fsdkr import join
+    rng = Rng("edge-nonunit")
+    t, n = 1, 4
+    all_keys = protocol.simulate_keygen(t, n, rng, KB)
+    keys = [k.clone() for k in all_keys[:3]]
+    jm, kk = protocol.join_distribute(rng, KB)
+    jm.set_party_index(4)
+    msgs = [protocol.replace([jm], key, {1: 1, 2: 2, 3: 3}, 4, rng, KB)[0] for key in keys]
+    honest = join.collect(jm, copy.deepcopy(msgs), kk, [], t, n, ctx=gpu_ctx, key_bits=KB, rng=Rng("jc"))
+    m2 = copy.deepcopy(msgs)
+    N2 = kk.ek.n * kk.ek.n
+    m2[0].points_encrypted_vec[3] = m2[0].points_encrypted_vec[3] * kk.dk.p % N2
+    lo = protocol.join_collect(jm, copy.deepcopy(m2), kk, [], t, n, Rng("jc"), KB)
+    lg = join.collect(jm, copy.deepcopy(m2), kk, [], t, n, ctx=gpu_ctx, key_bits=KB, rng=Rng("jc"))
+    assert (lo.x_i, lo.y, lo.pk_vec) == (lg.x_i, lg.y, lg.pk_vec)
+    assert lg.x_i != honest.x_i
+
+
+def test_ciphertext_wider_than_n_squared(gpu_ctx, dkr5):
+    """A ciphertext c + k N^2 wider than 2^(64 nl).  In
+    RefreshMessage::collect the PDL transcript hashes c itself, so the pair's
+    proof fails (same error in the oracle and on the GPU, whose batch runs at the
+    3072-bit width).  JoinMessage::collect has no PDL check: there Paillier::mul /
+    add / decrypt reduce mod N^2, so the joiner recovers the same share as with c;
+    the share recovery reduces the ciphertext mod N^2 before the C ABI (which
+    takes values < 2^(64 nl))."""
+    from fsdkr import join
+    keys, msgs, dks, _ = dkr5
+    i = 2
+    N2 = keys[i].paillier_key_vec[i].n ** 2
+    m2 = copy.deepcopy(msgs)
+    m2[0].points_encrypted_vec[i] += N2 << 2100
+    assert m2[0].points_encrypted_vec[i].bit_length() > 64 * 64
+    ro = _check(gpu_ctx, m2, keys[i], dks[i])
+    assert ro is not None and ro[0] == "PDLwSlackProof", ro
+    # the join path
+    rng = Rng("edge-wide-join")
+    t, n = 1, 4
+    all_keys = protocol.simulate_keygen(t, n, rng, KB)
+    jm, kk = protocol.join_distribute(rng, KB)
+    jm.set_party_index(4)
+    jmsgs = [protocol.replace([jm], k.clone(), {1: 1, 2: 2, 3: 3}, 4, rng, KB)[0] for k in all_keys[:3]]
+    honest = join.collect(jm, copy.deepcopy(jmsgs), kk, [], t, n, ctx=gpu_ctx, key_bits=KB, rng=Rng("jc"))
+    j2 = copy.deepcopy(jmsgs)
+    j2[0].points_encrypted_vec[3] += (kk.ek.n ** 2) << 2100
+    lo = protocol.join_collect(jm, copy.deepcopy(j2), kk, [], t, n, Rng("jc"), KB)
+    lg = join.collect(jm, copy.deepcopy(j2), kk, [], t, n, ctx=gpu_ctx, key_bits=KB, rng=Rng("jc"))
+    assert (lo.x_i, lo.y, lo.pk_vec) == (lg.x_i, lg.y, lg.pk_vec) == (honest.x_i, honest.y, honest.pk_vec)

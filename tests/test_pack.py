@@ -137,16 +137,19 @@ def _dump(b, M):
 
 
 @pytest.mark.parametrize("big_ped", [False, True])
-def test_staged_batch_equals_one_shot(big_ped):
+@pytest.mark.parametrize("split", [False, True])
+def test_staged_batch_equals_one_shot(big_ped, split):
     """CollectBatch(staged=True) + complete() packs exactly what the one-shot
     constructor packs, also when stage 1's width is superseded (a 3000-bit PDL z,
-    a stage-2 field, moves the batch to 3072-bit slots)."""
+    a stage-2 field, moves the batch to 3072-bit slots), and when stage 1 is
+    split (GA's fields, then stage1b())."""
     from fsdkr.batch import CollectBatch
     M = 8
     msgs, joins, lk = _fake_collect(M=M, big_ped=big_ped)
     one = CollectBatch(msgs, lk, joins, M, 2048)
-    st = CollectBatch(msgs, lk, joins, M, 2048, staged=True)
+    st = CollectBatch(msgs, lk, joins, M, 2048, staged=True, split_stage1=split)
     assert st.ga_ready and st.c.nl == 64
+    assert st.stage1b() == split and not st.stage1b()
     st.complete()
     one._msgs = st._msgs = msgs
     a, b = _dump(one, M), _dump(st, M)
@@ -258,3 +261,33 @@ def test_session_set_stage1_correct_key_rows():
                 assert np.array_equal(row, _expect([m.dk_correctness_proof.sigma_vec[j]], ckl)[0])
     ss.complete()
     assert int(ss.structs["ckl"][0]) == ckl
+
+
+def test_session_set_stage_z_rows_reused_by_stage2():
+    """Stage 1b (SessionSet.stage_z, fsdkr_collect_prestart_rp's input) packs every
+    message's ring-Pedersen Z rows at the width stage 2 gives them; stage 2 then
+    points ped_Z at the same rows, byte-identical to a one-shot set."""
+    import ctypes
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from pack_many_cpu import fake_sessions
+    from fsdkr.batch import SessionSet
+    sess = fake_sessions(6, seed=7)
+    M = 256
+    one = SessionSet(sess, M, 3072)
+    ss = SessionSet(sess, M, 3072, staged=True)
+    assert ss.stage_z()
+    zl = int(ss._pre["zl"][0])
+    ss.complete()
+    assert int(ss.structs["zl"][0]) == zl == int(one.structs["zl"][0])
+    for s, (msgs, lk, joins) in enumerate(sess):
+        assert int(ss._pre["ped_Z"][s]) == int(ss.structs["ped_Z"][ss.row[s]])
+        rows = len(msgs + joins) * M
+        a = np.ctypeslib.as_array(ctypes.cast(int(ss.structs["ped_Z"][ss.row[s]]), ctypes.POINTER(ctypes.c_uint32)),
+                                  (rows * zl,))
+        b = np.ctypeslib.as_array(ctypes.cast(int(one.structs["ped_Z"][one.row[s]]), ctypes.POINTER(ctypes.c_uint32)),
+                                  (rows * zl,))
+        assert np.array_equal(a, b)
+        want = _expect([z for m in msgs + joins for z in m.ring_pedersen_proof.Z[:M]], zl).reshape(-1)
+        assert np.array_equal(a, want)

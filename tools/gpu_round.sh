@@ -1,25 +1,81 @@
 #!/bin/bash
-# One GPU-box session: GPU tests, the bench, a kernel-trace profile of the bench.
-# Usage (from the repo root, via gpurun): bash tools/gpu_round.sh TAG [tests|bench|prof ...]
+# One GPU-box session (run via gpurun from the repo root):
+#   bash tools/gpu_round.sh TAG STEP [STEP ...]
+# Outputs go to gpurun_out/TAG/.  Steps (each under its own time limit; the
+# script stops at the first failing step):
+#   tests            the whole -m gpu suite                      -> tests.log
+#   tests:F1,F2      those test files only (tests/F1, tests/F2)  -> tests.log
+#   smoke            __graft_entry__ build-free smoke             -> smoke.log
+#   bench            bench.py (default: n = 64 headline, metric 2, configs[3] n = 256,
+#                    configs[4], key generation, CPU baseline)    -> bench.json
+#   benchq           bench.py without the CPU baseline            -> bench.json
+#   prof             rocprofv3 --kernel-trace --stats of a short bench.py run -> prof/
+#   trace            kernel trace of whole n = 64 collect() calls + timeline of one -> trace_summary.txt
+#   trace4           the same for whole configs[4] collect_many() calls (1024 sessions) -> trace4_summary.txt
+#   pmc64 | pmc256   one --pmc pass over whole n = 64 / n = 256 calls (tools/pmc_step.py)
+#                    -> pmc_step_n64.json / pmc_step_n256.json (per-call counter totals)
+#   pmcmx            PMC passes over the metric-2 modexp launch (tools/pmc.sh)
+#   shard256         bench.py --emulate-shard 2 / 4 / 8 at n = 256 -> shard_n256.jsonl
+#   shard64          the same at n = 64                            -> shard_n64.jsonl
+#   anything else    run as a shell command                       -> extra.log
+# Interleaved A/B runs: tools/ab_env.sh (environment variants of one build) and
+# tools/ab_lib.sh (two builds of libfsdkr.so).
 set -o pipefail
 TAG=${1:-run}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-# collect() runs 8 concurrent streams; rocprofv3's preload initialises HIP before
-# bench.py can set this, so export it here (bench.py/conftest set it otherwise)
+# collect() runs about twelve concurrent streams; rocprofv3's preload initialises
+# HIP before bench.py can set this, so export it here (bench.py/conftest set it otherwise)
 export GPU_MAX_HW_QUEUES=12
+fail() { echo "$1 failed rc=$2"; tail -30 "$3"; exit 1; }
+pmc_step() {   # $1 = label, $2.. = pmc_step.py shape args
+  local label=$1; shift
+  timeout -k 10 300 python $R/tools/pmc_step.py --gen-only --cache /tmp/$label.pkl "$@" > $OUT/pmc_$label.gen.log 2>&1 \
+    || fail "pmc $label workload" $? $OUT/pmc_$label.gen.log
+  (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_WAVES SQ_ACTIVE_INST_VALU \
+     SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
+     -d $OUT/pmc_$label -o run -- python3 $R/tools/pmc_step.py --cache /tmp/$label.pkl --steps 2 "$@" \
+     > $OUT/pmc_$label.log 2>&1) || fail "pmc $label" $? $OUT/pmc_$label.log
+  local f
+  f=$(find $OUT/pmc_$label -name "*counter_collection.csv" | head -1)
+  python3 $R/tools/pmc_summary_step.py "$f" 3 --label $label > $OUT/pmc_step_$label.json || exit 1
+}
 for step in "$@"; do
   case $step in
-    tests) timeout -k 10 600 python -m pytest $R/tests -m gpu -x -q > $OUT/tests.log 2>&1 || { echo "tests failed rc=$?"; tail -30 $OUT/tests.log; exit 1; } ;;
-    bench) timeout -k 10 420 python $R/bench.py > $OUT/bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 $OUT/bench.log; exit 1; } ;;
-    benchq) timeout -k 10 300 python $R/bench.py --no-cpu-baseline > $OUT/bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 $OUT/bench.log; exit 1; } ;;
-    prof) (cd /tmp && timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1) || { echo "prof failed rc=$?"; tail -30 $OUT/prof.log; exit 1; } ;;
-    trace) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr -- python3 $R/tools/prof_collect.py --full --steps 4 > $OUT/trace.log 2>&1) || { echo "trace failed rc=$?"; tail -30 $OUT/trace.log; exit 1; }
-      f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
-      python $R/tools/prof_summary.py "$f" --gap 10 --step 2 > $OUT/trace_summary.txt || exit 1 ;;
-    *) timeout -k 10 420 bash -c "$step" > $OUT/extra.log 2>&1 || { echo "step failed rc=$?"; tail -30 $OUT/extra.log; exit 1; } ;;
+    tests) timeout -k 10 900 python -u -m pytest $R/tests -m gpu -x -q --timeout 400 --timeout-method thread \
+             > $OUT/tests.log 2>&1 || fail tests $? $OUT/tests.log ;;
+    tests:*) files=$(echo ${step#tests:} | tr ',' '\n' | sed "s|^|$R/tests/|" | tr '\n' ' ')
+             timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 400 --timeout-method thread \
+               > $OUT/tests.log 2>&1 || fail tests $? $OUT/tests.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+             || fail smoke $? $OUT/smoke.log ;;
+    bench) timeout -k 10 600 python $R/bench.py > $OUT/bench.json 2> $OUT/bench.err || fail bench $? $OUT/bench.err ;;
+    benchq) timeout -k 10 500 python $R/bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err \
+              || fail bench $? $OUT/bench.err ;;
+    prof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
+             -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1) \
+             || fail prof $? $OUT/prof.log ;;
+    trace) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tr \
+              -- python3 $R/tools/prof_collect.py --full --steps 4 > $OUT/trace.log 2>&1) || fail trace $? $OUT/trace.log
+           f=$(find $OUT/trace -name "*kernel_trace.csv" | head -1)
+           python $R/tools/prof_summary.py "$f" --gap 10 --step -2 > $OUT/trace_summary.txt || exit 1 ;;
+    trace4) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace4 -o tr \
+              -- python3 $R/tools/prof_collect.py --full --sessions 1024 --steps 2 > $OUT/trace4.log 2>&1) \
+              || fail trace4 $? $OUT/trace4.log
+            f=$(find $OUT/trace4 -name "*kernel_trace.csv" | head -1)
+            python $R/tools/prof_summary.py "$f" --gap 19 --step -1 > $OUT/trace4_summary.txt || exit 1 ;;
+    pmc64) pmc_step n64 --n 64 --joins 4 --t 32 ;;
+    pmc256) pmc_step n256 --n 256 --joins 0 --t 128 ;;
+    pmcmx) bash $R/tools/pmc.sh $TAG/pmcmx || exit 1 ;;
+    shard256|shard64)
+      n=${step#shard}; t=$((n / 2)); j=$([ $n = 64 ] && echo 4 || echo 0)
+      for W in 2 4 8; do
+        timeout -k 10 300 python $R/bench.py --n $n --t $t --joins $j --steps 5 --warmup 1 --emulate-shard $W \
+          >> $OUT/shard_n$n.jsonl 2>> $OUT/shard_n$n.err || fail "shard $W" $? $OUT/shard_n$n.err
+      done ;;
+    *) timeout -k 10 600 bash -c "$step" > $OUT/extra.log 2>&1 || fail "$step" $? $OUT/extra.log ;;
   esac
   echo "step $step ok"
 done

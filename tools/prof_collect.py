@@ -33,6 +33,16 @@ def main():
     ctx = Context()
     if a.sessions:
         sess = synth.synth_sessions(ctx, a.sessions, n=3, t=1, seed=5, key_bits=3072)
+        if a.full:   # whole refresh.collect_many() calls (bench.py's configs[4] step)
+            import copy
+            from fsdkr import refresh
+            for k in range(a.steps + 1):
+                work = [(m, copy.deepcopy(lk), dk, j) for (m, j, lk, dk) in sess]
+                time.sleep(0.02)
+                t0 = time.perf_counter()
+                refresh.collect_many(work, ctx=ctx, key_bits=3072)
+                print(f"collect_many {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+            return
         batches = [CollectBatch(m, lk, j, 256, 3072) for (m, j, lk, dk) in sess]
         ctx.collect_prepare_many(batches)
         for _ in range(a.steps):
