@@ -474,10 +474,20 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
   // device buffer first (the descriptors hold device addresses)
   TZ.finalize();   // b_h / b_toff / w / stride only depend on the bases
   if (TZ.w != g.fb_w || TZ.entries != g.fb_entries) return FSDKR_OK;
-  const size_t sched_b = rows * (size_t)TZ.stride * 2;
+  // M = 256 exponents per T: a Lim-Lee comb over the same T chains (entries every
+  // w squarings: P_m = entry m pstep) takes ~30 % fewer products than BGMW
+  // (3072-bit: ~400 instead of ~575 per exponent, comb.hip)
+  CombParams cp;
+  if (comb_mode() != 0)
+    cp = comb_choose(g.bits_z, g.fb_w, TZ.b_h[n], comb_mode() == 2 ? 1e9 : (double)M, Mt,
+                     (size_t)shape_digits(nl) * 4, comb_mem_cap(c));
+  CombJob CJ;
+  if (cp.h) CJ.init(cp, nl, Mt, (uint32_t)rows);
+  const size_t sched_b = cp.h ? CJ.sched_bytes() : rows * (size_t)TZ.stride * 2;
   const size_t o_nsteps = o_sched0 + al(sched_b), o_desc = o_nsteps + al(rows * 4);
-  const size_t desc_est = rows * 40 + (size_t)(2 * n + Mt) * 32 + 16 * 256;
-  const size_t total = o_desc + al(desc_est);
+  const size_t desc_est = rows * 40 + (size_t)(2 * n + Mt) * 32 + 16 * 256 + CJ.ulist.size() * 2;
+  const size_t o_comb = o_desc + al(desc_est);
+  const size_t total = o_comb + (cp.h ? al(CJ.table_bytes()) : 0);
   uint8_t* dev = (uint8_t*)c->buf("collect_tz_pre", total);
   if (!dev) {
     c->fail("fsdkr_collect_prestart_rp: device allocation of %zu bytes failed", total);
@@ -497,8 +507,32 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
   });
   TZ.finalize();
   std::vector<uint8_t> desc;
-  TZ.pack(desc);
-  if (desc.size() > total - o_desc) {
+  size_t c_ptoff = 0, c_bmod = 0, c_ibase = 0, c_ul = 0;
+  if (cp.h) {   // the comb job's descriptors: TZ's instance arrays, T bases only
+    auto put = [&](const void* src, size_t bytes) {
+      const size_t o = (desc.size() + 255) & ~(size_t)255;
+      desc.resize(o + ((bytes + 255) & ~(size_t)255) + 256, 0);
+      if (bytes) memcpy(desc.data() + o, src, bytes);
+      return o;
+    };
+    std::vector<uint32_t> ptoff(Mt), bmod(Mt), ibase(rows);
+    for (uint32_t m = 0; m < Mt; ++m) {
+      ptoff[m] = TZ.b_toff[n + m];
+      bmod[m] = n + m;
+    }
+    for (size_t i = 0; i < rows; ++i) ibase[i] = TZ.e_base[o0 + i] - n;
+    c_ptoff = put(ptoff.data(), (size_t)Mt * 4);
+    c_bmod = put(bmod.data(), (size_t)Mt * 4);
+    c_ibase = put(ibase.data(), rows * 4);
+    c_ul = put(CJ.ulist.data(), CJ.ulist.size() * 2);
+    TZ.off.e_ptr = put(TZ.e_ptr.data() + o0, rows * 8);
+    TZ.off.e_len = put(TZ.e_len.data() + o0, rows * 4);
+    TZ.off.e_mod = put(TZ.e_mod.data() + o0, rows * 4);
+    TZ.off.o_ptr = put(TZ.o_ptr.data() + o0, rows * 8);
+  } else {
+    TZ.pack(desc);
+  }
+  if (desc.size() > o_comb - o_desc) {
     c->fail("fsdkr_collect_prestart_rp: descriptor image larger than planned");
     return FSDKR_E_ARG;
   }
@@ -535,9 +569,20 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
                          "prestart rp desc H2D")) ||
       (rc = c->hip_check(hipStreamSynchronize(zs), "prestart rp H2D sync")))   // pageable sources
     return rc;
-  FbDev fd{dev + o_desc, nullptr, reinterpret_cast<uint16_t*>(dev + o_sched0), reinterpret_cast<uint32_t*>(dev + o_nsteps)};
-  FbPre pre{g.fb_table, g.fb_entries, g.fb_done};
-  if ((rc = fb_launch(c, TZ, fd, g.fb_cons, zs, "fb rp prestart", nullptr, &pre))) return rc;
+  if (cp.h) {
+    const uint8_t* D = dev + o_desc;
+    auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(D + o); };
+    auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(D + o); };
+    CombDev cd{U32(c_ptoff), U32(c_bmod), U64(TZ.off.e_ptr), U32(TZ.off.e_len), U32(c_ibase), U32(TZ.off.e_mod),
+               U64(TZ.off.o_ptr), reinterpret_cast<const uint16_t*>(D + c_ul),
+               reinterpret_cast<uint32_t*>(dev + o_comb), reinterpret_cast<uint16_t*>(dev + o_sched0)};
+    if ((rc = comb_launch(c, CJ, cd, g.fb_table, g.fb_cons, zs, g.fb_done, "comb rp prestart"))) return rc;
+  } else {
+    FbDev fd{dev + o_desc, nullptr, reinterpret_cast<uint16_t*>(dev + o_sched0),
+             reinterpret_cast<uint32_t*>(dev + o_nsteps)};
+    FbPre pre{g.fb_table, g.fb_entries, g.fb_done};
+    if ((rc = fb_launch(c, TZ, fd, g.fb_cons, zs, "fb rp prestart", nullptr, &pre))) return rc;
+  }
   if (!g.tz_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.tz_done, hipEventDisableTiming), "event")))
     return rc;
   if ((rc = c->hip_check(hipEventRecord(g.tz_done, zs), "event record"))) return rc;

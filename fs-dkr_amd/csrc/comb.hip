@@ -1,0 +1,205 @@
+// Lim-Lee comb fixed-base exponentiation on gfx950 for bases shared by many
+// exponents: the ring-Pedersen T^Z_k checks (ring_pedersen_proof.rs:144, M =
+// 256 exponents per T) of collect() and of many sessions at once (BASELINE
+// configs[4]), and the stand-alone fsdkr_fixed_base_modexp.  Results are
+// bit-identical to base^exp mod N; only the order of the Montgomery products
+// changes (fixedbase.h: the exponent as an h x v x b bit array).
+//
+// Per base: the squaring chain P_m = base^(2^(m b)) (fb_table_kernel, or the
+// BGMW table chain every pstep-th entry), then comb_build_kernel fills the v
+// tables of 2^h products one popcount level at a time (G[u] = G[u - top] *
+// P_top), comb_sched_kernel transposes every exponent into its v b table
+// indices, and comb_exp_kernel runs b - 1 squarings and v b products per
+// exponent in lockstep (every instance has the same schedule shape).
+#include "fixedbase.h"
+#include "mont29.hpp"
+
+namespace fsdkr {
+
+// One popcount level of every base's v tables.  Level 1 lists u = 0 (the
+// Montgomery one) and the single bits (copies of chain entries); level p >= 2
+// lists the u of popcount p: G[u] = G[u without its top bit] * P_top.
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK) void comb_build_kernel(const CombBuildArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = cons_stride(KD);
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * IPB + li;
+  const uint32_t per_base = a.v * a.nu;
+  if (inst >= a.nbase * per_base) return;
+  const uint32_t base = inst / per_base, rem = inst - base * per_base;
+  const uint32_t j = rem / a.nu, u = a.ulist[rem - j * a.nu];
+  const uint32_t TS = 1u << a.h;
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[base] * STRIDE;
+  uint32_t* tab = a.comb + ((size_t)base * a.v + j) * TS * KD;
+  auto chain = [&](uint32_t i) {   // P_{i v + j}
+    return a.chain + ((size_t)a.ptoff[base] + (size_t)(i * a.v + j) * a.pstep) * KD;
+  };
+  uint32_t* dst = tab + (size_t)u * KD;
+  if (u == 0 || (u & (u - 1)) == 0) {   // copies: R mod N, or a chain entry
+    const uint32_t* src = u == 0 ? C + KD : chain(__builtin_ctz(u));
+#pragma unroll
+    for (int k = 0; k < L; ++k) dst[k * G + g] = src[k * G + g];
+    return;
+  }
+  uint32_t* stream = lds + li * KD;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int k = 0; k < L; ++k) M.n[k] = C[g * L + k];
+  M.ninv = C[3 * KD];
+  const uint32_t top = 31u - __builtin_clz(u);
+  const uint32_t* prev = tab + (size_t)(u ^ (1u << top)) * KD;
+  const uint32_t* P = chain(top);
+  uint32_t acc[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) acc[k] = prev[g * L + k];
+#pragma unroll
+  for (int k = 0; k < L; ++k) stream[k * G + g] = P[k * G + g];
+  __builtin_amdgcn_wave_barrier();
+  M.mul(acc, acc, stream);
+#pragma unroll
+  for (int k = 0; k < L; ++k) dst[g * L + k] = acc[k];
+}
+
+// One wave64 per exponent: its words into LDS (coalesced), then the lanes write
+// the v b table indices in step order s = (b - 1 - k) v + j (coalesced u16 rows).
+constexpr int COMB_SCHED_IPB = 4;
+constexpr uint32_t COMB_MAX_WORDS = 256;   // exponents of up to 8192 bits (host-checked)
+__global__ __launch_bounds__(64 * COMB_SCHED_IPB) void comb_sched_kernel(const CombSchedArgs a) {
+  __shared__ uint32_t e_lds[COMB_SCHED_IPB][COMB_MAX_WORDS];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.x * COMB_SCHED_IPB + wv;   // wave-uniform
+  if (i >= a.count) return;
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[i]);
+  const uint32_t elen = a.exp_len[i];
+  const uint32_t words = (a.h * a.v * a.b + 31) / 32;   // bits past h v b are zero (host-checked)
+  uint32_t* e = e_lds[wv];
+  for (uint32_t q = lane; q < words; q += 64) e[q] = q < elen ? E[q] : 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t steps = a.v * a.b;
+  uint16_t* S = a.sched + (size_t)i * steps;
+  for (uint32_t s = lane; s < steps; s += 64) {
+    const uint32_t k = a.b - 1 - s / a.v, j = s % a.v;
+    uint32_t u = 0;
+    for (uint32_t r = 0; r < a.h; ++r) {
+      const uint32_t t = (r * a.v + j) * a.b + k;
+      u |= ((e[t >> 5] >> (t & 31)) & 1u) << r;
+    }
+    S[s] = (uint16_t)u;
+  }
+}
+
+// base^e from the instance's tables: acc = G[0][u_0], then per step a product by
+// G[j][u] (a squaring first at every j = 0 after the first column), lockstep.
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = cons_stride(KD);
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * (blockDim.x / G) + li;
+  if (inst >= a.count) return;
+  uint32_t* stream = lds + li * KD;
+  const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int k = 0; k < L; ++k) M.n[k] = C[g * L + k];
+  M.ninv = C[3 * KD];
+  const uint32_t TS = 1u << a.h;
+  const uint32_t* tab = a.comb + (size_t)a.ibase[inst] * a.v * TS * KD;
+  const uint16_t* S = a.sched + (size_t)inst * a.steps;
+  uint32_t acc[L];
+  {
+    const uint32_t* E0 = tab + (size_t)S[0] * KD;
+#pragma unroll
+    for (int k = 0; k < L; ++k) acc[k] = E0[g * L + k];
+  }
+  uint32_t j = 0;
+  for (uint32_t st = 1; st < a.steps; ++st) {
+    if (++j == a.v) {   // next column: square first
+      j = 0;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < L; ++k) stream[g * L + k] = acc[k];
+      __builtin_amdgcn_wave_barrier();
+      M.sqr(acc, acc, stream);
+    }
+    const uint32_t* P = tab + ((size_t)j * TS + S[st]) * KD;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < L; ++k) stream[k * G + g] = P[k * G + g];   // coalesced over the group
+    __builtin_amdgcn_wave_barrier();
+    M.mul(acc, acc, stream);
+  }
+  // leave Montgomery form: acc * 1 / R, then exact reduction
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < L; ++k) stream[g * L + k] = (g == 0 && k == 0) ? 1u : 0u;
+  __builtin_amdgcn_wave_barrier();
+  M.mul(acc, acc, stream);
+  M.carry_exact(acc);
+  M.sub_if_ge(acc);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k = 0; k < L; ++k) stream[g * L + k] = acc[k];
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* O = reinterpret_cast<uint32_t*>(a.out_ptr[inst]);
+  constexpr int LO = K32 / G;
+#pragma unroll
+  for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
+}
+
+// ---- launchers ------------------------------------------------------------------
+template <int KD, int G, int K32>
+static hipError_t build_launch(const CombBuildArgs& a, hipStream_t st) {
+  constexpr uint32_t IPB = BLOCK / G;
+  const size_t n = (size_t)a.nbase * a.v * a.nu;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL((comb_build_kernel<KD, G, K32>), dim3((uint32_t)((n + IPB - 1) / IPB)), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+template <int KD, int G, int K32>
+static hipError_t exp_launch(const CombExpArgs& a, hipStream_t st) {
+  const uint32_t bs = a.count * G <= 256u * 4u * 64u ? 64u : (uint32_t)BLOCK, ipb = bs / G;
+  hipLaunchKernelGGL((comb_exp_kernel<KD, G, K32>), dim3((a.count + ipb - 1) / ipb), dim3(bs), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_comb_build(uint32_t k32, const CombBuildArgs& a, hipStream_t st) {
+  switch (k32) {
+    case 64: return build_launch<72, 4, 64>(a, st);
+    case 96: return build_launch<108, 4, 96>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_comb_sched(const CombSchedArgs& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  if ((a.h * a.v * a.b + 31) / 32 > COMB_MAX_WORDS || a.h > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(comb_sched_kernel, dim3((a.count + COMB_SCHED_IPB - 1) / COMB_SCHED_IPB),
+                     dim3(64 * COMB_SCHED_IPB), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_comb_exp(uint32_t k32, const CombExpArgs& a, int group, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  if (!a.steps) return hipErrorInvalidValue;
+  switch (k32) {
+    case 64: return group == 8 ? exp_launch<72, 8, 64>(a, st) : exp_launch<72, 4, 64>(a, st);
+    case 96: return exp_launch<108, 4, 96>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace fsdkr

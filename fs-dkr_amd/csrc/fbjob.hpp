@@ -130,6 +130,40 @@ struct FbPre {
 };
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
               hipStream_t table_st = nullptr, const FbPre* pre = nullptr);
+
+// Lim-Lee comb job (comb.hip) over `nbase` bases whose squaring chains are
+// already laid out in `chain` (P_m of base q at entry ptoff[q] + m * pstep):
+// the u order of the table levels (level 1: 0 and the single bits, then by
+// popcount) and the byte sizes of its scratch.
+struct CombJob {
+  CombParams p;
+  uint32_t k32 = 0, nbase = 0, count = 0;
+  std::vector<uint16_t> ulist;
+  std::vector<uint32_t> level_off;   // [h + 1]: level p's u values at [level_off[p-1], level_off[p])
+  void init(const CombParams& pp, uint32_t k, uint32_t nb, uint32_t cnt);
+  size_t table_bytes() const { return (size_t)nbase * p.entries_per_base() * shape_digits(k32) * 4; }
+  size_t sched_bytes() const { return (size_t)count * p.steps() * 2; }
+};
+// Device inputs of a CombJob: per base ptoff / mod_idx, per instance exponent
+// address / limbs, table set, modulus row, destination; the ulist upload; scratch.
+struct CombDev {
+  const uint32_t *ptoff, *bmod;
+  const uint64_t* eptr;
+  const uint32_t *elen, *ibase, *imod;
+  const uint64_t* optr;
+  const uint16_t* ulist;
+  uint32_t* comb;
+  uint16_t* sched;
+};
+// schedules on st, then (after chain_ready, if given) the table levels and the
+// exponentiations, all on st
+int comb_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
+                hipStream_t st, hipEvent_t chain_ready, const char* tag);
+// device bytes the comb tables may take (a fraction of the free memory)
+size_t comb_mem_cap(Ctx* c);
+// FSDKR_FB_COMB: 0 = BGMW only, 2 = the comb whenever it is possible, else
+// (default, 1) the comb where comb_choose finds it cheaper
+int comb_mode();
 // upload + launch + wait (stand-alone callers)
 int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag);
 

@@ -58,8 +58,146 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
   return rc;
 }
 
+CombParams comb_choose(uint32_t bits, uint32_t w, uint32_t avail, double per_base, size_t nbases, size_t entry_bytes,
+                       size_t cap) {
+  CombParams best;
+  if (bits < 64 || per_base < 8.0) return best;
+  const uint32_t wb = fb_window(bits);
+  double best_cost = 0.9 * ((double)((bits + wb - 1) / wb) + (double)((1u << wb) - 1));
+  const uint32_t step = w ? w : 1u;
+  for (uint32_t h = 2; h <= 12; ++h)
+    for (uint32_t v = 1; v <= 8; ++v) {
+      const uint32_t hv = h * v;
+      uint32_t b = (bits + hv - 1) / hv;
+      b = (b + step - 1) / step * step;
+      if ((hv * b + 31) / 32 > 256) continue;                         // comb_sched's exponent window
+      if (avail && (uint64_t)(hv - 1) * (b / step) >= avail) continue;   // chain entries the tables need
+      if (nbases * ((size_t)v << h) * entry_bytes > cap) continue;
+      const double cost = (double)(b - 1) + (double)v * b + (double)v * (double)((1u << h) - 1 - h) / per_base;
+      if (cost < best_cost) {
+        best_cost = cost;
+        best.h = h;
+        best.v = v;
+        best.b = b;
+        best.pstep = w ? b / w : 1u;
+      }
+    }
+  return best;
+}
+
+void CombJob::init(const CombParams& pp, uint32_t k, uint32_t nb, uint32_t cnt) {
+  p = pp;
+  k32 = k;
+  nbase = nb;
+  count = cnt;
+  ulist.clear();
+  level_off.assign(1, 0);
+  ulist.push_back(0);
+  for (uint32_t i = 0; i < p.h; ++i) ulist.push_back((uint16_t)(1u << i));
+  level_off.push_back((uint32_t)ulist.size());
+  for (uint32_t pc = 2; pc <= p.h; ++pc) {
+    for (uint32_t u = 1; u < (1u << p.h); ++u)
+      if ((uint32_t)__builtin_popcount(u) == pc) ulist.push_back((uint16_t)u);
+    level_off.push_back((uint32_t)ulist.size());
+  }
+}
+
+size_t comb_mem_cap(Ctx* c) {
+  size_t free_b = 0, total_b = 0;
+  if (c->hip_check(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo")) return 0;
+  return std::min(free_b / 3, (size_t)32 << 30);
+}
+
+int comb_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
+                hipStream_t st, hipEvent_t chain_ready, const char* tag) {
+  if (!j.count) return FSDKR_OK;
+  const CombParams& p = j.p;
+  int rc;
+  CombSchedArgs sa{d.eptr, d.elen, d.sched, p.h, p.v, p.b, j.count};
+  if ((rc = c->hip_check(launch_comb_sched(sa, st), "comb_sched launch"))) return rc;
+  if (chain_ready) (void)hipStreamWaitEvent(st, chain_ready, 0);
+  size_t m = c->tbeg("comb_build", st);
+  for (uint32_t lv = 1; lv <= p.h; ++lv) {
+    const uint32_t o = j.level_off[lv - 1], nu = j.level_off[lv] - o;
+    CombBuildArgs ba{chain, d.ptoff, d.bmod, consts, d.comb, d.ulist + o, nu, p.h, p.v, p.pstep, j.nbase};
+    if ((rc = c->hip_check(launch_comb_build(j.k32, ba, st), "comb_build launch"))) return rc;
+  }
+  c->tend(m, st);
+  CombExpArgs ea{d.comb, d.ibase, d.imod, d.optr, consts, d.sched, p.h, p.v, p.steps(), j.count};
+  m = c->tbeg("comb_exp", st);
+  rc = c->hip_check(launch_comb_exp(j.k32, ea, fb_group(c, j.count), st), tag);
+  c->tend(m, st);
+  return rc;
+}
+
+int comb_mode() {
+  const char* e = getenv("FSDKR_FB_COMB");
+  return e ? atoi(e) : 1;
+}
+
+// Stand-alone fixed-base job as a comb: the chains P_m = b^(2^(m b)) (fb_table
+// with window b, h v entries per base), then comb_launch.  false: not taken.
+static bool comb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag, int* rc_out) {
+  const int mode = comb_mode();
+  if (mode == 0 || (j.k32 != 64 && j.k32 != 96)) return false;
+  uint32_t bits = 1;
+  for (uint32_t b : j.b_bits) bits = std::max(bits, b);
+  const int KD = shape_digits(j.k32);
+  const double per_base = mode == 2 ? 1e9 : (double)j.count() / (double)j.bases();
+  CombParams p = comb_choose(bits, 0, 0, per_base, j.bases(), (size_t)KD * 4, comb_mem_cap(c));
+  if (!p.h) return false;
+  CombJob cj;
+  cj.init(p, j.k32, (uint32_t)j.bases(), (uint32_t)j.count());
+  const uint32_t nb = cj.nbase, ni = cj.count, hv = p.h * p.v;
+  std::vector<uint32_t> ptoff(nb), bh(nb, hv), ibase(ni);
+  for (uint32_t q = 0; q < nb; ++q) ptoff[q] = q * hv;
+  for (uint32_t i = 0; i < ni; ++i) ibase[i] = j.e_base[i];
+  std::vector<uint8_t> img;
+  auto put = [&](const void* src, size_t bytes) {
+    const size_t o = (img.size() + 255) & ~(size_t)255;
+    img.resize(o + ((bytes + 255) & ~(size_t)255) + 256, 0);
+    if (bytes) memcpy(img.data() + o, src, bytes);
+    return o;
+  };
+  const size_t o_bptr = put(j.b_ptr.data(), nb * 8), o_blen = put(j.b_len.data(), nb * 4),
+               o_bmod = put(j.b_mod.data(), nb * 4), o_ptoff = put(ptoff.data(), nb * 4), o_bh = put(bh.data(), nb * 4),
+               o_eptr = put(j.e_ptr.data(), (size_t)ni * 8), o_elen = put(j.e_len.data(), (size_t)ni * 4),
+               o_ibase = put(ibase.data(), (size_t)ni * 4), o_imod = put(j.e_mod.data(), (size_t)ni * 4),
+               o_optr = put(j.o_ptr.data(), (size_t)ni * 8), o_ul = put(cj.ulist.data(), cj.ulist.size() * 2);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_chain = al(img.size()), o_comb = o_chain + al((size_t)nb * hv * KD * 4),
+               o_sched = o_comb + al(cj.table_bytes()), total = o_sched + al(cj.sched_bytes());
+  std::string name = std::string("comb_") + tag;
+  uint8_t* dev = (uint8_t*)c->buf(name.c_str(), total);
+  if (!dev) {
+    c->fail("%s: device allocation failed (%zu bytes)", tag, total);
+    *rc_out = FSDKR_E_OOM;
+    return true;
+  }
+  int rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, c->stream), "H2D comb");
+  auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
+  auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
+  uint32_t* chain = reinterpret_cast<uint32_t*>(dev + o_chain);
+  if (!rc) {
+    FbTableArgs ta{U64(o_bptr), U32(o_blen), U32(o_bmod), U32(o_ptoff), U32(o_bh), consts, chain, p.b, nb, 0};
+    rc = c->hip_check(launch_fb_table(j.k32, ta, c->stream), "comb chain launch");
+  }
+  if (!rc) {
+    CombDev d{U32(o_ptoff), U32(o_bmod), U64(o_eptr), U32(o_elen), U32(o_ibase), U32(o_imod), U64(o_optr),
+              reinterpret_cast<const uint16_t*>(dev + o_ul), reinterpret_cast<uint32_t*>(dev + o_comb),
+              reinterpret_cast<uint16_t*>(dev + o_sched)};
+    rc = comb_launch(c, cj, d, chain, consts, c->stream, nullptr, tag);
+  }
+  // `img` is a local host buffer: the async copy must finish before it goes away
+  if (!rc) rc = c->hip_check(hipStreamSynchronize(c->stream), "sync comb");
+  *rc_out = rc;
+  return true;
+}
+
 int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag) {
   if (j.count() == 0) return FSDKR_OK;
+  int crc = 0;
+  if (comb_run(c, j, consts, tag, &crc)) return crc;
   const int KD = shape_digits(j.k32);
   std::vector<uint8_t> img;
   j.pack(img);

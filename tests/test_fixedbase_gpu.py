@@ -78,3 +78,50 @@ def test_fixed_base_window_widths(gpu_ctx, top_bits):
     want = [pow(bases[b], e, mods[[0, 1, 0][b]]) for b, e in zip(bidx, exps)]
     bad = [k for k in range(len(want)) if out[k] != want[k]]
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+@pytest.fixture
+def comb_mode():
+    """FSDKR_FB_COMB for the duration of a test (read by the library per call)."""
+    import os
+    old = os.environ.get("FSDKR_FB_COMB")
+
+    def set_mode(m):
+        os.environ["FSDKR_FB_COMB"] = str(m)
+    yield set_mode
+    if old is None:
+        os.environ.pop("FSDKR_FB_COMB", None)
+    else:
+        os.environ["FSDKR_FB_COMB"] = old
+
+
+@pytest.mark.parametrize("limbs", [64, 96])
+@pytest.mark.parametrize("mode", [0, 2])
+def test_comb_matches_pow(gpu_ctx, comb_mode, limbs, mode):
+    """Lim-Lee comb (comb.hip, forced by FSDKR_FB_COMB=2) and BGMW (=0) on the
+    mixed case: zero / one / unreduced bases, half-width modulus, exponents of
+    0 .. 2816 bits including all-ones rows and columns of the bit array."""
+    comb_mode(mode)
+    bases, bmod, mods, bidx, exps = _case(limbs, 3000 + limbs + mode, per_base=48)
+    out = gpu_ctx.fixed_base_modexp(bases, bmod, mods, bidx, exps, limbs)
+    want = [pow(bases[b], e, mods[bmod[b]]) for b, e in zip(bidx, exps)]
+    bad = [k for k in range(len(want)) if out[k] != want[k]]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("limbs", [64, 96])
+def test_comb_ring_pedersen_shape(gpu_ctx, comb_mode, limbs):
+    """M = 256 exponents of the modulus' size per base (ring-Pedersen T^Z): the
+    default mode takes the comb here; every result checked."""
+    comb_mode(1)
+    rnd = random.Random(limbs)
+    bits = 32 * limbs
+    mods = [rnd.getrandbits(bits) | 1 | (1 << (bits - 1)) for _ in range(3)]
+    bases = [rnd.getrandbits(bits) % mods[k] for k in range(3)]
+    bidx = [k // 256 for k in range(3 * 256)]
+    exps = [rnd.getrandbits(bits) for _ in bidx]
+    exps[5], exps[300], exps[600] = 0, (1 << bits) - 1, 1
+    out = gpu_ctx.fixed_base_modexp(bases, [0, 1, 2], mods, bidx, exps, limbs)
+    want = [pow(bases[b], e, mods[b]) for b, e in zip(bidx, exps)]
+    bad = [k for k in range(len(want)) if out[k] != want[k]]
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
