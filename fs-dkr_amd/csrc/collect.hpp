@@ -301,6 +301,7 @@ struct CollectPlan {
   uint32_t* fb_table = nullptr;
   uint16_t* fb_sched = nullptr;
   uint32_t* fb_nsteps = nullptr;
+  uint8_t* fb_comb = nullptr;   // comb scratch of fb's comb groups (FbJob::plan_comb)
   bool launched = false;
 };
 

@@ -110,7 +110,7 @@ int collect_launch_impl(Ctx* c) {
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
-    FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps};
+    FbDev fd{dev + pl.d_FB, pl.fb_table, pl.fb_sched, pl.fb_nsteps, pl.fb_comb};
     hipStream_t ts = c->side_stream(8);   // own stream: the chain starts beside fb_sched
     (void)hipStreamWaitEvent(ts, consts_ready, 0);
     if ((rc = fb_launch(c, pl.fb, fd, cons_nl, ss, "fb collect", ts, pl.fb_hit ? &pl.fb_pre : nullptr)) ||

@@ -545,6 +545,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       ((size_t)7 * P + 4 * (size_t)J + (size_t)Mt * CK_M2) * 32 + (size_t)3 * P * 4 +    // modexp jobs (+ GA out_idx)
       (size_t)n * 63 * 36 +                                                                // GA pads
       (2 * (size_t)n + Mt) * 24 + (4 * (size_t)P + (size_t)Mt * M) * 32 + 24 * 512 +      // fixed-base job
+      (2 * (size_t)n + Mt) * 8 + (4 * (size_t)P + (size_t)Mt * M) * 4 + 4 * (8192 + 2048) +   // its comb groups
       4 * (size_t)P * 8 + 4 * (size_t)P * 16 +                                            // binom, inverses
       n_eqall * (sizeof(EqOperand) + 4) + 2 * (size_t)P * sizeof(Prod3Operand) + 4 * (size_t)P +
       2 * (size_t)P * 8 + P + (size_t)n_p2 * sizeof(Pow2Op) + 32 * 256 + 64 * 1024;
@@ -725,6 +726,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       reinterpret_cast<GaPre*>(c->ga_pre)->fb_valid = false;   // consumed
     }
   }
+  FB.plan_comb(comb_mem_cap(c));   // Lim-Lee combs per base class when they beat BGMW (comb.hip)
   clk.lap("desc fb finalize");
   FB.pack(desc);   // FbJob offsets are positions in `desc`, i.e. relative to desc_base
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N
@@ -903,8 +905,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   // fixed-base scratch (power tables, schedules, step counts): its own context buffer
   {
     const int KD = shape_digits(nl);
-    const size_t tb = Img::al(FB.table_bytes(KD)), sb = Img::al(FB.sched_bytes());
-    uint8_t* fbs = (uint8_t*)c->buf("collect_fb", tb + sb + FB.nsteps_bytes() + 256);
+    const size_t tb = Img::al(FB.table_bytes(KD)), sb = Img::al(FB.sched_bytes()), nb = Img::al(FB.nsteps_bytes());
+    uint8_t* fbs = (uint8_t*)c->buf("collect_fb", tb + sb + nb + FB.comb_scratch + 256);
     if (!fbs) {
       c->fail("fsdkr_verify_collect: fixed-base scratch allocation failed");
       return FSDKR_E_OOM;
@@ -912,6 +914,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     pl.fb_table = (uint32_t*)fbs;
     pl.fb_sched = (uint16_t*)(fbs + tb);
     pl.fb_nsteps = (uint32_t*)(fbs + tb + sb);
+    pl.fb_comb = FB.cgroups.empty() ? nullptr : fbs + tb + sb + nb;
   }
   pl.d_FB = desc_base;
   clk.lap("descriptors");

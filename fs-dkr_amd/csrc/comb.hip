@@ -40,6 +40,9 @@ __global__ __launch_bounds__(BLOCK) void comb_build_kernel(const CombBuildArgs a
     return a.chain + ((size_t)a.ptoff[base] + (size_t)(i * a.v + j) * a.pstep) * KD;
   };
   uint32_t* dst = tab + (size_t)u * KD;
+  if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
   if (u == 0 || (u & (u - 1)) == 0) {   // copies: R mod N, or a chain entry
     const uint32_t* src = u == 0 ? C + KD : chain(__builtin_ctz(u));
 #pragma unroll
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(64 * COMB_SCHED_IPB) void comb_sched_kernel(const C
 // base^e from the instance's tables: acc = G[0][u_0], then per step a product by
 // G[j][u] (a squaring first at every j = 0 after the first column), lockstep.
 template <int KD, int G, int K32>
-__global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs a) {
+__global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs args) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
@@ -107,10 +110,17 @@ __global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs a) {
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
-  const uint32_t inst = blockIdx.x * (blockDim.x / G) + li;
+  uint32_t gk = 0;   // the block's group (block-uniform)
+  for (uint32_t k = 1; k < args.ngroups; ++k)
+    if (blockIdx.x >= args.g[k].block0) gk = k;
+  const CombGroupDev& a = args.g[gk];
+  const uint32_t inst = (blockIdx.x - a.block0) * (blockDim.x / G) + li;
   if (inst >= a.count) return;
+  if (args.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (args.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (args.prio == 1) __builtin_amdgcn_s_setprio(1);
   uint32_t* stream = lds + li * KD;
-  const uint32_t* C = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  const uint32_t* C = args.consts + (size_t)a.mod_idx[inst] * STRIDE;
   MT M;
   M.init_lane(g);
 #pragma unroll
@@ -170,9 +180,17 @@ static hipError_t build_launch(const CombBuildArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 template <int KD, int G, int K32>
-static hipError_t exp_launch(const CombExpArgs& a, hipStream_t st) {
-  const uint32_t bs = a.count * G <= 256u * 4u * 64u ? 64u : (uint32_t)BLOCK, ipb = bs / G;
-  hipLaunchKernelGGL((comb_exp_kernel<KD, G, K32>), dim3((a.count + ipb - 1) / ipb), dim3(bs), 0, st, a);
+static hipError_t exp_launch(CombExpArgs& a, hipStream_t st) {
+  uint64_t lanes = 0;
+  for (uint32_t k = 0; k < a.ngroups; ++k) lanes += (uint64_t)a.g[k].count * G;
+  const uint32_t bs = lanes <= 256u * 4u * 64u ? 64u : (uint32_t)BLOCK, ipb = bs / G;
+  uint32_t blocks = 0;
+  for (uint32_t k = 0; k < a.ngroups; ++k) {
+    a.g[k].block0 = blocks;
+    blocks += (a.g[k].count + ipb - 1) / ipb;
+  }
+  if (!blocks) return hipSuccess;
+  hipLaunchKernelGGL((comb_exp_kernel<KD, G, K32>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
@@ -192,9 +210,10 @@ hipError_t launch_comb_sched(const CombSchedArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_comb_exp(uint32_t k32, const CombExpArgs& a, int group, hipStream_t st) {
-  if (!a.count) return hipSuccess;
-  if (!a.steps) return hipErrorInvalidValue;
+hipError_t launch_comb_exp(uint32_t k32, CombExpArgs& a, int group, hipStream_t st) {
+  if (a.ngroups == 0 || a.ngroups > (uint32_t)kCombGroups) return hipErrorInvalidValue;
+  for (uint32_t k = 0; k < a.ngroups; ++k)
+    if (!a.g[k].steps) return hipErrorInvalidValue;
   switch (k32) {
     case 64: return group == 8 ? exp_launch<72, 8, 64>(a, st) : exp_launch<72, 4, 64>(a, st);
     case 96: return exp_launch<108, 4, 96>(a, st);

@@ -14,6 +14,19 @@
 
 namespace fsdkr {
 
+// Lim-Lee comb job (comb.hip) over `nbase` bases whose squaring chains are
+// already laid out in `chain` (P_m of base q at entry ptoff[q] + m * pstep):
+// the u order of the table levels (level 1: 0 and the single bits, then by
+// popcount) and the byte sizes of its scratch.
+struct CombJob {
+  CombParams p;
+  uint32_t k32 = 0, nbase = 0, count = 0;
+  std::vector<uint16_t> ulist;
+  std::vector<uint32_t> level_off;   // [h + 1]: level p's u values at [level_off[p-1], level_off[p])
+  void init(const CombParams& pp, uint32_t k, uint32_t nb, uint32_t cnt);
+  size_t table_bytes() const { return (size_t)nbase * p.entries_per_base() * shape_digits(k32) * 4; }
+  size_t sched_bytes() const { return (size_t)count * p.steps() * 2; }
+};
 struct FbJob {
   uint32_t k32 = 0;
   uint32_t table_prio = 3;   // s_setprio of the table chain (a long serial chain, few waves)
@@ -27,6 +40,20 @@ struct FbJob {
   uint32_t w = 1, stride = 0;
   size_t entries = 0;
   std::vector<uint32_t> b_h, b_toff, i_h, i_toff;
+  // comb plan (plan_comb, after finalize): the instances grouped by base class
+  // (runs of bases with one exponent bound, e.g. collect()'s [h1_i | T_m | h2_i]),
+  // each group a Lim-Lee comb over its bases' BGMW chains (P_m = entry m pstep)
+  struct CombGrp {
+    uint32_t b0 = 0, b1 = 0;   // bases [b0, b1)
+    size_t i0 = 0, i1 = 0;     // instances [i0, i1)
+    CombJob cj;
+    size_t o_ptoff = 0, o_bmod = 0, o_ibase = 0, o_ul = 0;   // packed image offsets
+    size_t s_comb = 0, s_sched = 0;                           // comb scratch offsets
+  };
+  std::vector<CombGrp> cgroups;   // non-empty: fb_launch runs the job as combs
+  size_t comb_scratch = 0;
+  // plan the comb groups (reorders the instances by group); false: BGMW
+  bool plan_comb(size_t cap);
 
   uint32_t add_base(uint64_t ptr, uint32_t len, uint32_t mod) {
     b_ptr.push_back(ptr);
@@ -104,6 +131,20 @@ struct FbJob {
     off.i_toff = put(i_toff.data(), i_toff.size() * 4);
     off.e_mod = put(e_mod.data(), e_mod.size() * 4);
     off.o_ptr = put(o_ptr.data(), o_ptr.size() * 8);
+    for (CombGrp& g : cgroups) {
+      std::vector<uint32_t> ib(g.i1 - g.i0);
+      for (size_t i = g.i0; i < g.i1; ++i) ib[i - g.i0] = e_base[i] - g.b0;
+      g.o_ptoff = put(b_toff.data() + g.b0, (size_t)(g.b1 - g.b0) * 4);
+      g.o_bmod = put(b_mod.data() + g.b0, (size_t)(g.b1 - g.b0) * 4);
+      g.o_ibase = put(ib.data(), ib.size() * 4);
+      g.o_ul = put(g.cj.ulist.data(), g.cj.ulist.size() * 2);
+    }
+  }
+  // bytes pack() adds for the comb groups (an upper bound, alignment included)
+  size_t comb_desc_bytes() const {
+    size_t s = 0;
+    for (const CombGrp& g : cgroups) s += (size_t)(g.b1 - g.b0) * 8 + (g.i1 - g.i0) * 4 + g.cj.ulist.size() * 2 + 4 * 512;
+    return s;
   }
   // scratch the kernels write: table, schedules, step counts
   size_t table_bytes(int KD) const { return entries * (size_t)KD * 4; }
@@ -117,6 +158,7 @@ struct FbDev {
   uint32_t* table = nullptr;
   uint16_t* sched = nullptr;
   uint32_t* nsteps = nullptr;
+  uint8_t* comb = nullptr;        // comb scratch (FbJob::comb_scratch bytes) when cgroups is set
 };
 
 // table, schedule and exponent kernels.  table_st: stream of the table chain
@@ -131,19 +173,6 @@ struct FbPre {
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
               hipStream_t table_st = nullptr, const FbPre* pre = nullptr);
 
-// Lim-Lee comb job (comb.hip) over `nbase` bases whose squaring chains are
-// already laid out in `chain` (P_m of base q at entry ptoff[q] + m * pstep):
-// the u order of the table levels (level 1: 0 and the single bits, then by
-// popcount) and the byte sizes of its scratch.
-struct CombJob {
-  CombParams p;
-  uint32_t k32 = 0, nbase = 0, count = 0;
-  std::vector<uint16_t> ulist;
-  std::vector<uint32_t> level_off;   // [h + 1]: level p's u values at [level_off[p-1], level_off[p])
-  void init(const CombParams& pp, uint32_t k, uint32_t nb, uint32_t cnt);
-  size_t table_bytes() const { return (size_t)nbase * p.entries_per_base() * shape_digits(k32) * 4; }
-  size_t sched_bytes() const { return (size_t)count * p.steps() * 2; }
-};
 // Device inputs of a CombJob: per base ptoff / mod_idx, per instance exponent
 // address / limbs, table set, modulus row, destination; the ulist upload; scratch.
 struct CombDev {

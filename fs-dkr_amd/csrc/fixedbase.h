@@ -82,6 +82,7 @@ struct CombBuildArgs {          // one popcount level of the tables
   uint32_t* comb;               // [nbase][v][2^h][KD]
   const uint16_t* ulist;        // [nu] the level's u values (level 1: 0 and the single bits)
   uint32_t nu, h, v, pstep, nbase;
+  uint32_t prio;                // s_setprio of the level's waves (short, latency-bound launches)
 };
 struct CombSchedArgs {          // per instance, step s = (b - 1 - k) v + j: u_jk (u16)
   const uint64_t* exp_ptr;      // [count]
@@ -89,17 +90,27 @@ struct CombSchedArgs {          // per instance, step s = (b - 1 - k) v + j: u_j
   uint16_t* sched;              // [count][v b]
   uint32_t h, v, b, count;
 };
-struct CombExpArgs {
-  const uint32_t* comb;
-  const uint32_t* ibase;        // [count] base (table set) of the instance
+// One comb_exp launch over up to kCombGroups instance groups (each with its own
+// tables and (h, v, b)): group k owns blocks [block0, next group's block0), so
+// every wave runs one group's schedule shape in lockstep.
+constexpr int kCombGroups = 4;
+struct CombGroupDev {
+  const uint32_t* comb;         // the group's tables [nbase][v][2^h][KD]
+  const uint16_t* sched;        // [count][steps]
+  const uint32_t* ibase;        // [count] base (table set) of the instance, group-local
   const uint32_t* mod_idx;      // [count]
   const uint64_t* out_ptr;      // [count] destination (K32 limbs)
+  uint32_t h, v, steps, count, block0;
+};
+struct CombExpArgs {
+  CombGroupDev g[kCombGroups];
+  uint32_t ngroups;
   const uint32_t* consts;
-  const uint16_t* sched;
-  uint32_t h, v, steps, count;
+  uint32_t prio;
 };
 hipError_t launch_comb_build(uint32_t k32, const CombBuildArgs& a, hipStream_t st);
 hipError_t launch_comb_sched(const CombSchedArgs& a, hipStream_t st);
-hipError_t launch_comb_exp(uint32_t k32, const CombExpArgs& a, int group, hipStream_t st);
+// fills the groups' block0 (blocks of the launch's size) and launches
+hipError_t launch_comb_exp(uint32_t k32, CombExpArgs& a, int group, hipStream_t st);
 
 }  // namespace fsdkr

@@ -20,9 +20,13 @@ static int fb_group(Ctx* c, size_t count) {
   return count * 8 <= kLaneCapacity ? 8 : 4;
 }
 
+static int comb_path(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st,
+                     const char* tag, const uint32_t* chain, hipEvent_t ready);
+
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
               hipStream_t table_st, const FbPre* pre) {
   if (j.count() == 0) return FSDKR_OK;
+  const bool comb = !j.cgroups.empty() && d.comb;
   const uint8_t* I = d.img;
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(I + o); };
@@ -45,6 +49,11 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
         return rc;
       own = true;
     }
+  }
+  if (comb) {
+    rc = comb_path(c, j, d, consts, st, tag, pre ? pre->table : d.table, ready);
+    if (own) (void)hipEventDestroy(ready);
+    return rc;
   }
   FbSchedArgs sa{U64(j.off.e_ptr), U32(j.off.e_len), U32(j.off.i_h), d.sched, d.nsteps, j.stride, j.w, ni};
   if ((rc = c->hip_check(launch_fb_sched(sa, st), "fb_sched launch"))) return rc;
@@ -108,26 +117,156 @@ size_t comb_mem_cap(Ctx* c) {
   return std::min(free_b / 3, (size_t)32 << 30);
 }
 
+static int comb_sched_launch(Ctx* c, const CombJob& j, const CombDev& d, hipStream_t st) {
+  CombSchedArgs sa{d.eptr, d.elen, d.sched, j.p.h, j.p.v, j.p.b, j.count};
+  return c->hip_check(launch_comb_sched(sa, st), "comb_sched launch");
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* e = getenv(name);
+  return e && *e ? (uint32_t)atoi(e) : dflt;
+}
+
+static int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain,
+                             const uint32_t* consts, hipStream_t st) {
+  static const uint32_t prio = env_u32("FSDKR_COMB_BUILD_PRIO", 3);
+  for (uint32_t lv = 1; lv <= j.p.h; ++lv) {
+    const uint32_t o = j.level_off[lv - 1], nu = j.level_off[lv] - o;
+    CombBuildArgs ba{chain, d.ptoff, d.bmod, consts, d.comb, d.ulist + o, nu, j.p.h, j.p.v, j.p.pstep, j.nbase, prio};
+    int rc = c->hip_check(launch_comb_build(j.k32, ba, st), "comb_build launch");
+    if (rc) return rc;
+  }
+  return FSDKR_OK;
+}
+
+// one comb_exp launch over n jobs of the same width
+static int comb_exp_launch(Ctx* c, const CombJob* const* jobs, const CombDev* devs, uint32_t n,
+                           const uint32_t* consts, hipStream_t st, const char* tag) {
+  static const uint32_t prio = env_u32("FSDKR_COMB_EXP_PRIO", 0);
+  CombExpArgs ea{};
+  ea.consts = consts;
+  ea.prio = prio;
+  size_t total = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const CombJob& j = *jobs[k];
+    const CombDev& d = devs[k];
+    if (!j.count) continue;
+    ea.g[ea.ngroups++] = CombGroupDev{d.comb, d.sched, d.ibase, d.imod, d.optr, j.p.h, j.p.v, j.p.steps(), j.count, 0};
+    total += j.count;
+  }
+  if (!ea.ngroups) return FSDKR_OK;
+  size_t m = c->tbeg("comb_exp", st);
+  int rc = c->hip_check(launch_comb_exp(jobs[0]->k32, ea, fb_group(c, total), st), tag);
+  c->tend(m, st);
+  return rc;
+}
+
 int comb_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
                 hipStream_t st, hipEvent_t chain_ready, const char* tag) {
   if (!j.count) return FSDKR_OK;
-  const CombParams& p = j.p;
   int rc;
-  CombSchedArgs sa{d.eptr, d.elen, d.sched, p.h, p.v, p.b, j.count};
-  if ((rc = c->hip_check(launch_comb_sched(sa, st), "comb_sched launch"))) return rc;
+  if ((rc = comb_sched_launch(c, j, d, st))) return rc;
   if (chain_ready) (void)hipStreamWaitEvent(st, chain_ready, 0);
   size_t m = c->tbeg("comb_build", st);
-  for (uint32_t lv = 1; lv <= p.h; ++lv) {
-    const uint32_t o = j.level_off[lv - 1], nu = j.level_off[lv] - o;
-    CombBuildArgs ba{chain, d.ptoff, d.bmod, consts, d.comb, d.ulist + o, nu, p.h, p.v, p.pstep, j.nbase};
-    if ((rc = c->hip_check(launch_comb_build(j.k32, ba, st), "comb_build launch"))) return rc;
+  rc = comb_build_launch(c, j, d, chain, consts, st);
+  c->tend(m, st);
+  if (rc) return rc;
+  const CombJob* jp = &j;
+  return comb_exp_launch(c, &jp, &d, 1, consts, st, tag);
+}
+
+// The job's comb groups: every schedule first (they need only the exponents),
+// then, once the chains exist, every group's table levels and one comb_exp launch.
+static int comb_path(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st,
+                     const char* tag, const uint32_t* chain, hipEvent_t ready) {
+  const uint8_t* I = d.img;
+  auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
+  auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(I + o); };
+  const size_t ng = j.cgroups.size();
+  std::vector<CombDev> devs(ng);
+  std::vector<const CombJob*> jobs(ng);
+  int rc;
+  for (size_t k = 0; k < ng; ++k) {
+    const FbJob::CombGrp& g = j.cgroups[k];
+    devs[k] = CombDev{U32(g.o_ptoff), U32(g.o_bmod), U64(j.off.e_ptr) + g.i0, U32(j.off.e_len) + g.i0,
+                      U32(g.o_ibase), U32(j.off.e_mod) + g.i0, U64(j.off.o_ptr) + g.i0,
+                      reinterpret_cast<const uint16_t*>(I + g.o_ul), reinterpret_cast<uint32_t*>(d.comb + g.s_comb),
+                      reinterpret_cast<uint16_t*>(d.comb + g.s_sched)};
+    jobs[k] = &g.cj;
+    if ((rc = comb_sched_launch(c, g.cj, devs[k], st))) return rc;
   }
+  if (ready) (void)hipStreamWaitEvent(st, ready, 0);
+  size_t m = c->tbeg("comb_build", st);
+  for (size_t k = 0; k < ng; ++k)
+    if ((rc = comb_build_launch(c, j.cgroups[k].cj, devs[k], chain, consts, st))) return rc;
   c->tend(m, st);
-  CombExpArgs ea{d.comb, d.ibase, d.imod, d.optr, consts, d.sched, p.h, p.v, p.steps(), j.count};
-  m = c->tbeg("comb_exp", st);
-  rc = c->hip_check(launch_comb_exp(j.k32, ea, fb_group(c, j.count), st), tag);
-  c->tend(m, st);
-  return rc;
+  return comb_exp_launch(c, jobs.data(), devs.data(), (uint32_t)ng, consts, st, tag);
+}
+
+bool FbJob::plan_comb(size_t cap) {
+  cgroups.clear();
+  comb_scratch = 0;
+  const int mode = comb_mode();
+  if (mode == 0 || (k32 != 64 && k32 != 96) || count() == 0) return false;
+  // groups: runs of consecutive bases with one exponent bound (hence one chain height)
+  std::vector<uint32_t> gid(bases());
+  std::vector<CombGrp> gs;
+  for (uint32_t b = 0; b < bases(); ++b) {
+    if (gs.empty() || b_bits[b] != b_bits[gs.back().b0] || b_h[b] != b_h[gs.back().b0]) {
+      gs.emplace_back();
+      gs.back().b0 = b;
+    }
+    gs.back().b1 = b + 1;
+    gid[b] = (uint32_t)gs.size() - 1;
+  }
+  // instances grouped by their base's group (stable)
+  std::vector<size_t> cnt(gs.size() + 1, 0);
+  for (uint32_t b : e_base) ++cnt[gid[b] + 1];
+  for (size_t k = 1; k <= gs.size(); ++k) cnt[k] += cnt[k - 1];
+  std::vector<size_t> pos(cnt.begin(), cnt.end() - 1);
+  bool sorted = true;
+  for (size_t i = 1; i < count() && sorted; ++i) sorted = gid[e_base[i]] >= gid[e_base[i - 1]];
+  if (!sorted) {
+    std::vector<size_t> perm(count());
+    for (size_t i = 0; i < count(); ++i) perm[pos[gid[e_base[i]]]++] = i;
+    auto apply = [&](auto& v) {
+      auto t = v;
+      for (size_t i = 0; i < count(); ++i) t[i] = v[perm[i]];
+      v.swap(t);
+    };
+    apply(e_ptr);
+    apply(o_ptr);
+    apply(e_len);
+    apply(e_base);
+    apply(e_mod);
+    for (size_t i = 0; i < count(); ++i) {
+      i_h[i] = b_h[e_base[i]];
+      i_toff[i] = b_toff[e_base[i]];
+    }
+  }
+  const size_t KD = (size_t)shape_digits(k32);
+  size_t used = 0, ng = 0;
+  for (size_t k = 0; k < gs.size(); ++k) {
+    CombGrp& g = gs[k];
+    g.i0 = cnt[k];
+    g.i1 = cnt[k + 1];
+    if (g.i1 == g.i0) continue;   // bases without instances need no tables
+    const uint32_t nb = g.b1 - g.b0;
+    const double per_base = mode == 2 ? 1e9 : (double)(g.i1 - g.i0) / nb;
+    const CombParams p = comb_choose(b_bits[g.b0], w, b_h[g.b0], per_base, nb, KD * 4, cap - used);
+    if (!p.h || ++ng > (size_t)kCombGroups) return false;
+    g.cj.init(p, k32, nb, (uint32_t)(g.i1 - g.i0));
+    used += g.cj.table_bytes();
+  }
+  for (CombGrp& g : gs) {
+    if (g.i1 == g.i0) continue;
+    g.s_comb = comb_scratch;
+    comb_scratch += (g.cj.table_bytes() + 255) & ~(size_t)255;
+    g.s_sched = comb_scratch;
+    comb_scratch += (g.cj.sched_bytes() + 255) & ~(size_t)255;
+    cgroups.push_back(std::move(g));
+  }
+  return true;
 }
 
 int comb_mode() {
