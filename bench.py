@@ -72,23 +72,59 @@ def collect_work(R, J, n, M=256, k=64):
         J * 2 * (w_modexp(k, b + 512) + w_modexp(k, 256))
 
 
-def collect_issued(R, J, n, M=256, w=6, k=64):
+def fb_window(bits):
+    """fixedbase.hip fb_window: the BGMW window minimising ceil(bits/w) + 2^w - 1."""
+    return min(range(1, 9), key=lambda w: ((bits + w - 1) // w + (1 << w) - 1, w))
+
+
+def comb_cost(bits, w, avail, per_base):
+    """fixedbase_host.cpp comb_choose (no memory cap): products per exponent of
+    the cheapest Lim-Lee comb (h, v, b) over a chain with entries every w
+    squarings (avail of them per base) and the table products per base, or None
+    when BGMW stays (the comb must beat it by 10 %)."""
+    if bits < 64 or per_base < 8:
+        return None
+    wb = fb_window(bits)
+    best, best_cost = None, 0.9 * ((bits + wb - 1) // wb + (1 << wb) - 1)
+    for h in range(2, 13):
+        for v in range(1, 9):
+            hv = h * v
+            b = -(-bits // hv)
+            b = -(-b // w) * w
+            if (hv * b + 31) // 32 > 256 or (hv - 1) * (b // w) >= avail:
+                continue
+            cost = (b - 1) + v * b + v * ((1 << h) - 1 - h) / per_base
+            if cost < best_cost:
+                best_cost, best = cost, ((b - 1) + v * b, v * ((1 << h) - 1 - h))
+    return best
+
+
+def collect_issued(R, J, n, M=256, k=64):
     """MACs the GPU actually issues per collect: collect_work with the bases
     shared across exponents (h1_i, h2_i per receiver, ring-Pedersen T per
-    message) evaluated by fixed-base BGMW windowing (fixedbase.hip): ceil(L/w) +
-    2^w - 1 products per exponent plus one L-squaring table chain per base.
-    Reported beside the algorithmic figure so the saving is not read as kernel
-    efficiency.  k = limbs of N."""
+    message) evaluated as fixed-base exponentiations: one squaring chain per base
+    (entries every w bits), then per base class either a Lim-Lee comb (comb.hip:
+    b - 1 + v b products per exponent plus v (2^h - 1 - h) table products per
+    base) or BGMW windowing (ceil(L/w) + 2^w - 1 products per exponent), as
+    FbJob::plan_comb / fsdkr_collect_prestart_rp choose.  Reported beside the
+    algorithmic figure so the saving is not read as kernel efficiency (SURVEY
+    §8d).  k = limbs of N (configs[4]'s prestarted T^Z exponents make the same
+    choice: M per base)."""
     mm = 2 * k * k + k
     b = 32 * k
     s1, s3 = 769, b + 768
+    w = fb_window(max(s1, s3, b))
 
-    def fb(bits):
-        return ((bits + w - 1) // w + (1 << w) - 1) * mm
+    def fb(bits, exps, bases):
+        """products of `exps` exponents of up to `bits` bits over `bases` bases"""
+        c = comb_cost(bits, w, -(-bits // w), exps / max(bases, 1))
+        if c is None:
+            return exps * ((bits + w - 1) // w + (1 << w) - 1)
+        return exps * c[0] + bases * c[1]
 
     var = collect_work(R, J, n, M, k)
     var -= R * n * 2 * (w_modexp(k, s1) + w_modexp(k, s3)) + (R + J) * M * w_modexp(k, b)
-    fixed = R * n * 2 * (fb(s1) + fb(s3)) + (R + J) * M * fb(b)
+    fixed = (fb(s1, 2 * R * n, n) + fb(s3, 2 * R * n, n) + fb(b, (R + J) * M, R + J)) * mm
     tables = (n * (s1 + s3) + (R + J) * b) * mm
     return var + fixed + tables
 

@@ -26,6 +26,7 @@ void free_ga_pre(Ctx* c) {
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
   if (g && g->ck_done) (void)hipEventDestroy(g->ck_done);
   if (g && g->tz_done) (void)hipEventDestroy(g->tz_done);
+  if (g && g->comb_done) (void)hipEventDestroy(g->comb_done);
   delete g;
   c->ga_pre = nullptr;
 }

@@ -331,6 +331,10 @@ struct GaPre {
   uint32_t Mt = 0, fb_w = 0, bits_h1 = 0, bits_h2 = 0, bits_z = 0, fb_entries = 0;
   uint32_t* fb_table = nullptr;
   hipEvent_t fb_done = nullptr;     // every table built
+  // Lim-Lee comb tables of the base classes (FbJob::plan_comb), built on the
+  // chains' stream after them: prepare's and prestart_rp's combs take them
+  std::vector<CombPre> comb_pre;
+  hipEvent_t comb_done = nullptr;
   // correct-key sigma_k^n mod n of every message (prepare's GC job), when stage 1
   // packed ck_n and ck_sigma: rows at width ck_l, in prepare's message order
   bool ck_valid = false;

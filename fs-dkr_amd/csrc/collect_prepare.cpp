@@ -726,7 +726,10 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       reinterpret_cast<GaPre*>(c->ga_pre)->fb_valid = false;   // consumed
     }
   }
-  FB.plan_comb(comb_mem_cap(c));   // Lim-Lee combs per base class when they beat BGMW (comb.hip)
+  // Lim-Lee combs per base class when they beat BGMW (comb.hip), over the
+  // prestart's comb tables when it built them for the same classes
+  FB.plan_comb(comb_mem_cap(c), pl.fb_hit && gp ? &gp->comb_pre : nullptr);
+  if (pl.fb_hit && gp) pl.fb_pre.comb_ready = gp->comb_done;
   clk.lap("desc fb finalize");
   FB.pack(desc);   // FbJob offsets are positions in `desc`, i.e. relative to desc_base
   // binom descriptors: PDL B = 1 + s1*N (small s1) | Alice gs1 = 1 + s1A*N

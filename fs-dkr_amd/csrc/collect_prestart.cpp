@@ -65,18 +65,71 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
   const FbLayout L = fb_layout(n, Mt, w, bh1, bh2, bz);
   const uint32_t nb = 2 * n + Mt, entries = L.entries, nmod = n + Mt;
   const int KD = shape_digits(nl);
+  // the Lim-Lee comb tables of every base class, as prepare's FbJob::plan_comb
+  // will choose them (runs of bases with one bound; instances per base: 2 R_s for
+  // h1_i / h2_i, M for T_m), built behind the chains on their stream
+  std::vector<uint32_t> bbits(nb), bcnt(nb, M);
+  for (uint32_t r = 0; r < n; ++r) {
+    bbits[r] = bh1;
+    bbits[n + Mt + r] = bh2;
+  }
+  for (uint32_t m = 0; m < Mt; ++m) bbits[n + m] = bz;
+  for (const GaPre::Sess& x : g.sess)
+    for (uint32_t i = 0; i < x.n; ++i) bcnt[x.rbase + i] = bcnt[n + Mt + x.rbase + i] = 2 * x.R;
+  struct PreRun {
+    uint32_t b0, b1;
+    CombJob cj;
+    size_t o_pt = 0, o_bm = 0, o_ul = 0, s_tab = 0;
+  };
+  std::vector<PreRun> runs;
+  size_t comb_bytes = 0, comb_desc = 0;
+  if (comb_mode() != 0 && (nl == 64 || nl == 96)) {
+    for (const auto& r : base_runs(bbits.data(), L.h.data(), nb)) {
+      double tot = 0;
+      for (uint32_t b = r.first; b < r.second; ++b) tot += bcnt[b];
+      const uint32_t nbr = r.second - r.first;
+      const CombParams p = comb_choose(bbits[r.first], w, L.h[r.first], comb_mode() == 2 ? 1e9 : tot / nbr, nbr,
+                                       (size_t)KD * 4, comb_mem_cap(c));
+      if (!p.h) continue;
+      runs.push_back(PreRun{r.first, r.second, CombJob()});
+      runs.back().cj.init(p, nl, nbr, 0);
+      runs.back().s_tab = comb_bytes;
+      comb_bytes += Img::al(runs.back().cj.table_bytes());
+      comb_desc += Img::al((size_t)nbr * 4) * 2 + Img::al(runs.back().cj.ulist.size() * 2);
+    }
+    if (comb_bytes > comb_mem_cap(c)) {
+      runs.clear();
+      comb_bytes = comb_desc = 0;
+    }
+  }
   auto al = Img::al;
   const size_t o_mod = 0, o_h1 = al((size_t)nmod * nl * 4), o_h2 = o_h1 + al((size_t)n * nl * 4),
                o_T = o_h2 + al((size_t)n * nl * 4), o_bp = o_T + al((size_t)Mt * nl * 4),
                o_bl = o_bp + al((size_t)nb * 8), o_bm = o_bl + al((size_t)nb * 4), o_bt = o_bm + al((size_t)nb * 4),
-               o_bh = o_bt + al((size_t)nb * 4), o_tab = o_bh + al((size_t)nb * 4);
+               o_bh = o_bt + al((size_t)nb * 4), o_cd = o_bh + al((size_t)nb * 4), o_tab = o_cd + comb_desc;
   const size_t total = o_tab + (size_t)entries * KD * 4;
   uint8_t* dev = (uint8_t*)c->buf("collect_fb_pre", total);
-  if (!dev) {
-    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
+  uint8_t* cdev = comb_bytes ? (uint8_t*)c->buf("collect_comb_pre", comb_bytes) : nullptr;
+  if (!dev || (comb_bytes && !cdev)) {
+    c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total + comb_bytes);
     return FSDKR_E_OOM;
   }
   std::vector<uint8_t> img(o_tab, 0);
+  {
+    size_t o = o_cd;
+    for (PreRun& r : runs) {
+      const size_t nbr = r.b1 - r.b0;
+      r.o_pt = o;
+      memcpy(img.data() + o, L.toff.data() + r.b0, nbr * 4);
+      o += al(nbr * 4);
+      r.o_bm = o;
+      memcpy(img.data() + o, L.mod.data() + r.b0, nbr * 4);
+      o += al(nbr * 4);
+      r.o_ul = o;
+      memcpy(img.data() + o, r.cj.ulist.data(), r.cj.ulist.size() * 2);
+      o += al(r.cj.ulist.size() * 2);
+    }
+  }
   uint32_t* mods = reinterpret_cast<uint32_t*>(img.data() + o_mod);   // [Ntilde_i | RP modulus_m]
   uint32_t* H1 = reinterpret_cast<uint32_t*>(img.data() + o_h1);
   uint32_t* H2 = reinterpret_cast<uint32_t*>(img.data() + o_h2);
@@ -126,6 +179,18 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
   FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
   if ((rc = c->hip_check(launch_fb_table(nl, tall, ts), "prestart fb_table"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.fb_done, ts), "event record"))) return rc;
+  g.comb_pre.clear();
+  for (const PreRun& r : runs) {
+    CombDev d{U32(r.o_pt), U32(r.o_bm), nullptr, nullptr, nullptr, nullptr, nullptr,
+              reinterpret_cast<const uint16_t*>(dev + r.o_ul), reinterpret_cast<uint32_t*>(cdev + r.s_tab), nullptr};
+    if ((rc = comb_build_launch(c, r.cj, d, g.fb_table, cons, ts))) return rc;
+    g.comb_pre.push_back(CombPre{r.b0, r.b1, r.cj.p, d.comb});
+  }
+  if (!runs.empty()) {
+    if (!g.comb_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.comb_done, hipEventDisableTiming), "event")))
+      return rc;
+    if ((rc = c->hip_check(hipEventRecord(g.comb_done, ts), "event record"))) return rc;
+  }
   g.ntilde.assign(mods, mods + (size_t)n * nl);
   g.h1.assign(H1, H1 + (size_t)n * nl);
   g.h2.assign(H2, H2 + (size_t)n * nl);
@@ -239,6 +304,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
   g.valid = false;
   g.fb_valid = false;
+  g.comb_pre.clear();
   g.ck_valid = false;
   g.tz_valid = false;
   *n_out = *P_out = 0;
@@ -576,7 +642,12 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
     CombDev cd{U32(c_ptoff), U32(c_bmod), U64(TZ.off.e_ptr), U32(TZ.off.e_len), U32(c_ibase), U32(TZ.off.e_mod),
                U64(TZ.off.o_ptr), reinterpret_cast<const uint16_t*>(D + c_ul),
                reinterpret_cast<uint32_t*>(dev + o_comb), reinterpret_cast<uint16_t*>(dev + o_sched0)};
-    if ((rc = comb_launch(c, CJ, cd, g.fb_table, g.fb_cons, zs, g.fb_done, "comb rp prestart"))) return rc;
+    const uint32_t* pre_tab = nullptr;   // the T class's tables from the prestart, when they match
+    for (const CombPre& q : g.comb_pre)
+      if (q.b0 == n && q.b1 == n + Mt && same_params(q.p, cp)) pre_tab = q.tables;
+    if ((rc = comb_launch(c, CJ, cd, g.fb_table, g.fb_cons, zs, pre_tab ? g.comb_done : g.fb_done, "comb rp prestart",
+                          pre_tab)))
+      return rc;
   } else {
     FbDev fd{dev + o_desc, nullptr, reinterpret_cast<uint16_t*>(dev + o_sched0),
              reinterpret_cast<uint32_t*>(dev + o_nsteps)};

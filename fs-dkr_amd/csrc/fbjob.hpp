@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #include "ctx.hpp"
@@ -27,6 +28,27 @@ struct CombJob {
   size_t table_bytes() const { return (size_t)nbase * p.entries_per_base() * shape_digits(k32) * 4; }
   size_t sched_bytes() const { return (size_t)count * p.steps() * 2; }
 };
+// Comb tables built ahead (fsdkr_collect_prestart) for the bases [b0, b1) of a
+// job laid out like collect()'s FbJob, with parameters p.
+struct CombPre {
+  uint32_t b0 = 0, b1 = 0;
+  CombParams p;
+  const uint32_t* tables = nullptr;
+};
+inline bool same_params(const CombParams& a, const CombParams& b) {
+  return a.h == b.h && a.v == b.v && a.b == b.b && a.pstep == b.pstep;
+}
+// base classes of a fixed-base job: runs of consecutive bases with one exponent
+// bound and chain height ([first, last) pairs)
+inline std::vector<std::pair<uint32_t, uint32_t>> base_runs(const uint32_t* bits, const uint32_t* h, uint32_t nb) {
+  std::vector<std::pair<uint32_t, uint32_t>> r;
+  for (uint32_t b = 0; b < nb; ++b) {
+    if (r.empty() || bits[b] != bits[r.back().first] || h[b] != h[r.back().first]) r.emplace_back(b, b);
+    r.back().second = b + 1;
+  }
+  return r;
+}
+
 struct FbJob {
   uint32_t k32 = 0;
   uint32_t table_prio = 3;   // s_setprio of the table chain (a long serial chain, few waves)
@@ -47,13 +69,16 @@ struct FbJob {
     uint32_t b0 = 0, b1 = 0;   // bases [b0, b1)
     size_t i0 = 0, i1 = 0;     // instances [i0, i1)
     CombJob cj;
+    const uint32_t* pre_tables = nullptr;                     // built ahead (CombPre): no table levels
     size_t o_ptoff = 0, o_bmod = 0, o_ibase = 0, o_ul = 0;   // packed image offsets
     size_t s_comb = 0, s_sched = 0;                           // comb scratch offsets
   };
   std::vector<CombGrp> cgroups;   // non-empty: fb_launch runs the job as combs
   size_t comb_scratch = 0;
-  // plan the comb groups (reorders the instances by group); false: BGMW
-  bool plan_comb(size_t cap);
+  // plan the comb groups (reorders the instances by group); false: BGMW.  pre:
+  // tables built ahead for these bases (a group with the same bases and
+  // parameters takes them)
+  bool plan_comb(size_t cap, const std::vector<CombPre>* pre = nullptr);
 
   uint32_t add_base(uint64_t ptr, uint32_t len, uint32_t mod) {
     b_ptr.push_back(ptr);
@@ -169,6 +194,7 @@ struct FbPre {
   const uint32_t* table = nullptr;
   uint32_t entries = 0;
   hipEvent_t ready = nullptr;
+  hipEvent_t comb_ready = nullptr;   // the CombPre tables (FbJob::CombGrp::pre_tables) exist
 };
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
               hipStream_t table_st = nullptr, const FbPre* pre = nullptr);
@@ -185,9 +211,12 @@ struct CombDev {
   uint16_t* sched;
 };
 // schedules on st, then (after chain_ready, if given) the table levels and the
-// exponentiations, all on st
+// exponentiations, all on st; pre_tables: the tables exist (at chain_ready), no levels
 int comb_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
-                hipStream_t st, hipEvent_t chain_ready, const char* tag);
+                hipStream_t st, hipEvent_t chain_ready, const char* tag, const uint32_t* pre_tables = nullptr);
+// the table levels alone (a prestart builds them ahead of the exponents)
+int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
+                      hipStream_t st);
 // device bytes the comb tables may take (a fraction of the free memory)
 size_t comb_mem_cap(Ctx* c);
 // FSDKR_FB_COMB: 0 = BGMW only, 2 = the comb whenever it is possible, else

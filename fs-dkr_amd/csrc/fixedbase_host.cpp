@@ -21,7 +21,7 @@ static int fb_group(Ctx* c, size_t count) {
 }
 
 static int comb_path(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st,
-                     const char* tag, const uint32_t* chain, hipEvent_t ready);
+                     const char* tag, const uint32_t* chain, hipEvent_t ready, hipEvent_t comb_ready);
 
 int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st, const char* tag,
               hipStream_t table_st, const FbPre* pre) {
@@ -51,7 +51,7 @@ int fb_launch(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hi
     }
   }
   if (comb) {
-    rc = comb_path(c, j, d, consts, st, tag, pre ? pre->table : d.table, ready);
+    rc = comb_path(c, j, d, consts, st, tag, pre ? pre->table : d.table, ready, pre ? pre->comb_ready : nullptr);
     if (own) (void)hipEventDestroy(ready);
     return rc;
   }
@@ -111,10 +111,16 @@ void CombJob::init(const CombParams& pp, uint32_t k, uint32_t nb, uint32_t cnt) 
   }
 }
 
+// fixed once per process, so a prestart and the prepare after it choose the same
+// parameters for the same base classes
 size_t comb_mem_cap(Ctx* c) {
-  size_t free_b = 0, total_b = 0;
-  if (c->hip_check(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo")) return 0;
-  return std::min(free_b / 3, (size_t)32 << 30);
+  static size_t cap = 0;
+  if (!cap) {
+    size_t free_b = 0, total_b = 0;
+    if (c->hip_check(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo")) return 0;
+    cap = std::min(free_b / 4, (size_t)24 << 30);
+  }
+  return cap;
 }
 
 static int comb_sched_launch(Ctx* c, const CombJob& j, const CombDev& d, hipStream_t st) {
@@ -127,8 +133,8 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
   return e && *e ? (uint32_t)atoi(e) : dflt;
 }
 
-static int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain,
-                             const uint32_t* consts, hipStream_t st) {
+int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
+                      hipStream_t st) {
   static const uint32_t prio = env_u32("FSDKR_COMB_BUILD_PRIO", 3);
   for (uint32_t lv = 1; lv <= j.p.h; ++lv) {
     const uint32_t o = j.level_off[lv - 1], nu = j.level_off[lv] - o;
@@ -162,23 +168,28 @@ static int comb_exp_launch(Ctx* c, const CombJob* const* jobs, const CombDev* de
 }
 
 int comb_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
-                hipStream_t st, hipEvent_t chain_ready, const char* tag) {
+                hipStream_t st, hipEvent_t chain_ready, const char* tag, const uint32_t* pre_tables) {
   if (!j.count) return FSDKR_OK;
   int rc;
   if ((rc = comb_sched_launch(c, j, d, st))) return rc;
   if (chain_ready) (void)hipStreamWaitEvent(st, chain_ready, 0);
-  size_t m = c->tbeg("comb_build", st);
-  rc = comb_build_launch(c, j, d, chain, consts, st);
-  c->tend(m, st);
-  if (rc) return rc;
+  CombDev dd = d;
+  if (pre_tables) {
+    dd.comb = const_cast<uint32_t*>(pre_tables);
+  } else {
+    size_t m = c->tbeg("comb_build", st);
+    rc = comb_build_launch(c, j, d, chain, consts, st);
+    c->tend(m, st);
+    if (rc) return rc;
+  }
   const CombJob* jp = &j;
-  return comb_exp_launch(c, &jp, &d, 1, consts, st, tag);
+  return comb_exp_launch(c, &jp, &dd, 1, consts, st, tag);
 }
 
 // The job's comb groups: every schedule first (they need only the exponents),
 // then, once the chains exist, every group's table levels and one comb_exp launch.
 static int comb_path(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* consts, hipStream_t st,
-                     const char* tag, const uint32_t* chain, hipEvent_t ready) {
+                     const char* tag, const uint32_t* chain, hipEvent_t ready, hipEvent_t comb_ready) {
   const uint8_t* I = d.img;
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(I + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(I + o); };
@@ -190,20 +201,25 @@ static int comb_path(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* con
     const FbJob::CombGrp& g = j.cgroups[k];
     devs[k] = CombDev{U32(g.o_ptoff), U32(g.o_bmod), U64(j.off.e_ptr) + g.i0, U32(j.off.e_len) + g.i0,
                       U32(g.o_ibase), U32(j.off.e_mod) + g.i0, U64(j.off.o_ptr) + g.i0,
-                      reinterpret_cast<const uint16_t*>(I + g.o_ul), reinterpret_cast<uint32_t*>(d.comb + g.s_comb),
+                      reinterpret_cast<const uint16_t*>(I + g.o_ul),
+                      g.pre_tables ? const_cast<uint32_t*>(g.pre_tables) : reinterpret_cast<uint32_t*>(d.comb + g.s_comb),
                       reinterpret_cast<uint16_t*>(d.comb + g.s_sched)};
     jobs[k] = &g.cj;
     if ((rc = comb_sched_launch(c, g.cj, devs[k], st))) return rc;
   }
   if (ready) (void)hipStreamWaitEvent(st, ready, 0);
+  bool any_pre = false;
+  for (const FbJob::CombGrp& g : j.cgroups) any_pre = any_pre || g.pre_tables;
+  if (any_pre && comb_ready) (void)hipStreamWaitEvent(st, comb_ready, 0);
   size_t m = c->tbeg("comb_build", st);
   for (size_t k = 0; k < ng; ++k)
-    if ((rc = comb_build_launch(c, j.cgroups[k].cj, devs[k], chain, consts, st))) return rc;
+    if (!j.cgroups[k].pre_tables && (rc = comb_build_launch(c, j.cgroups[k].cj, devs[k], chain, consts, st)))
+      return rc;
   c->tend(m, st);
   return comb_exp_launch(c, jobs.data(), devs.data(), (uint32_t)ng, consts, st, tag);
 }
 
-bool FbJob::plan_comb(size_t cap) {
+bool FbJob::plan_comb(size_t cap, const std::vector<CombPre>* pre) {
   cgroups.clear();
   comb_scratch = 0;
   const int mode = comb_mode();
@@ -211,13 +227,11 @@ bool FbJob::plan_comb(size_t cap) {
   // groups: runs of consecutive bases with one exponent bound (hence one chain height)
   std::vector<uint32_t> gid(bases());
   std::vector<CombGrp> gs;
-  for (uint32_t b = 0; b < bases(); ++b) {
-    if (gs.empty() || b_bits[b] != b_bits[gs.back().b0] || b_h[b] != b_h[gs.back().b0]) {
-      gs.emplace_back();
-      gs.back().b0 = b;
-    }
-    gs.back().b1 = b + 1;
-    gid[b] = (uint32_t)gs.size() - 1;
+  for (const auto& r : base_runs(b_bits.data(), b_h.data(), (uint32_t)bases())) {
+    gs.emplace_back();
+    gs.back().b0 = r.first;
+    gs.back().b1 = r.second;
+    for (uint32_t b = r.first; b < r.second; ++b) gid[b] = (uint32_t)gs.size() - 1;
   }
   // instances grouped by their base's group (stable)
   std::vector<size_t> cnt(gs.size() + 1, 0);
@@ -253,15 +267,18 @@ bool FbJob::plan_comb(size_t cap) {
     if (g.i1 == g.i0) continue;   // bases without instances need no tables
     const uint32_t nb = g.b1 - g.b0;
     const double per_base = mode == 2 ? 1e9 : (double)(g.i1 - g.i0) / nb;
-    const CombParams p = comb_choose(b_bits[g.b0], w, b_h[g.b0], per_base, nb, KD * 4, cap - used);
+    const CombParams p = comb_choose(b_bits[g.b0], w, b_h[g.b0], per_base, nb, KD * 4, cap);
     if (!p.h || ++ng > (size_t)kCombGroups) return false;
     g.cj.init(p, k32, nb, (uint32_t)(g.i1 - g.i0));
-    used += g.cj.table_bytes();
+    for (size_t q = 0; pre && q < pre->size() && !g.pre_tables; ++q)
+      if ((*pre)[q].b0 == g.b0 && (*pre)[q].b1 == g.b1 && same_params((*pre)[q].p, p)) g.pre_tables = (*pre)[q].tables;
+    if (!g.pre_tables) used += g.cj.table_bytes();
+    if (used > cap) return false;
   }
   for (CombGrp& g : gs) {
     if (g.i1 == g.i0) continue;
     g.s_comb = comb_scratch;
-    comb_scratch += (g.cj.table_bytes() + 255) & ~(size_t)255;
+    if (!g.pre_tables) comb_scratch += (g.cj.table_bytes() + 255) & ~(size_t)255;
     g.s_sched = comb_scratch;
     comb_scratch += (g.cj.sched_bytes() + 255) & ~(size_t)255;
     cgroups.push_back(std::move(g));
