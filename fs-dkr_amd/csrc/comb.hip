@@ -16,9 +16,25 @@
 
 namespace fsdkr {
 
-// One popcount level of every base's v tables.  Level 1 lists u = 0 (the
-// Montgomery one) and the single bits (copies of chain entries); level p >= 2
-// lists the u of popcount p: G[u] = G[u without its top bit] * P_top.
+// Level 1 of every base's v tables: u = 0 (the Montgomery one) and the single
+// bits (copies of chain entries).  No LDS: it fits beside running launches.
+template <int KD>
+__global__ __launch_bounds__(BLOCK) void comb_copy_kernel(const CombBuildArgs a) {
+  const uint32_t per_base = a.v * a.nu;
+  const uint64_t t = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint64_t inst = t / KD;
+  if (inst >= (uint64_t)a.nbase * per_base) return;
+  const uint32_t k = (uint32_t)(t - inst * KD);
+  const uint32_t base = (uint32_t)(inst / per_base), rem = (uint32_t)(inst - (uint64_t)base * per_base);
+  const uint32_t j = rem / a.nu, u = a.ulist[rem - j * a.nu];
+  if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  const uint32_t* src = u == 0 ? a.consts + (size_t)a.mod_idx[base] * cons_stride(KD) + KD
+                               : a.chain + ((size_t)a.ptoff[base] + (size_t)(__builtin_ctz(u) * a.v + j) * a.pstep) * KD;
+  a.comb[(((size_t)base * a.v + j) * ((size_t)1 << a.h) + u) * KD + k] = src[k];
+}
+
+// One popcount level p >= 2 of every base's v tables: the u of popcount p,
+// G[u] = G[u without its top bit] * P_top.
 template <int KD, int G, int K32>
 __global__ __launch_bounds__(BLOCK) void comb_build_kernel(const CombBuildArgs a) {
   using MT = Mont29<KD, G>;
@@ -36,19 +52,9 @@ __global__ __launch_bounds__(BLOCK) void comb_build_kernel(const CombBuildArgs a
   const uint32_t TS = 1u << a.h;
   const uint32_t* C = a.consts + (size_t)a.mod_idx[base] * STRIDE;
   uint32_t* tab = a.comb + ((size_t)base * a.v + j) * TS * KD;
-  auto chain = [&](uint32_t i) {   // P_{i v + j}
-    return a.chain + ((size_t)a.ptoff[base] + (size_t)(i * a.v + j) * a.pstep) * KD;
-  };
-  uint32_t* dst = tab + (size_t)u * KD;
   if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
-  if (u == 0 || (u & (u - 1)) == 0) {   // copies: R mod N, or a chain entry
-    const uint32_t* src = u == 0 ? C + KD : chain(__builtin_ctz(u));
-#pragma unroll
-    for (int k = 0; k < L; ++k) dst[k * G + g] = src[k * G + g];
-    return;
-  }
   uint32_t* stream = lds + li * KD;
   MT M;
   M.init_lane(g);
@@ -57,7 +63,7 @@ __global__ __launch_bounds__(BLOCK) void comb_build_kernel(const CombBuildArgs a
   M.ninv = C[3 * KD];
   const uint32_t top = 31u - __builtin_clz(u);
   const uint32_t* prev = tab + (size_t)(u ^ (1u << top)) * KD;
-  const uint32_t* P = chain(top);
+  const uint32_t* P = a.chain + ((size_t)a.ptoff[base] + (size_t)(top * a.v + j) * a.pstep) * KD;
   uint32_t acc[L];
 #pragma unroll
   for (int k = 0; k < L; ++k) acc[k] = prev[g * L + k];
@@ -66,7 +72,7 @@ __global__ __launch_bounds__(BLOCK) void comb_build_kernel(const CombBuildArgs a
   __builtin_amdgcn_wave_barrier();
   M.mul(acc, acc, stream);
 #pragma unroll
-  for (int k = 0; k < L; ++k) dst[g * L + k] = acc[k];
+  for (int k = 0; k < L; ++k) tab[(size_t)u * KD + g * L + k] = acc[k];
 }
 
 // One wave64 per exponent: its words into LDS (coalesced), then the lanes write
@@ -176,7 +182,12 @@ static hipError_t build_launch(const CombBuildArgs& a, hipStream_t st) {
   constexpr uint32_t IPB = BLOCK / G;
   const size_t n = (size_t)a.nbase * a.v * a.nu;
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL((comb_build_kernel<KD, G, K32>), dim3((uint32_t)((n + IPB - 1) / IPB)), dim3(BLOCK), 0, st, a);
+  if (a.nu && a.ulist_level1) {   // copies: one thread per word
+    const size_t words = n * KD;
+    hipLaunchKernelGGL((comb_copy_kernel<KD>), dim3((uint32_t)((words + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((comb_build_kernel<KD, G, K32>), dim3((uint32_t)((n + IPB - 1) / IPB)), dim3(BLOCK), 0, st, a);
+  }
   return hipGetLastError();
 }
 template <int KD, int G, int K32>

@@ -83,6 +83,7 @@ struct CombBuildArgs {          // one popcount level of the tables
   const uint16_t* ulist;        // [nu] the level's u values (level 1: 0 and the single bits)
   uint32_t nu, h, v, pstep, nbase;
   uint32_t prio;                // s_setprio of the level's waves (short, latency-bound launches)
+  uint32_t ulist_level1;        // 1: level 1 (u = 0 and the single bits: copies), else products
 };
 struct CombSchedArgs {          // per instance, step s = (b - 1 - k) v + j: u_jk (u16)
   const uint64_t* exp_ptr;      // [count]

@@ -128,17 +128,15 @@ static int comb_sched_launch(Ctx* c, const CombJob& j, const CombDev& d, hipStre
   return c->hip_check(launch_comb_sched(sa, st), "comb_sched launch");
 }
 
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* e = getenv(name);
-  return e && *e ? (uint32_t)atoi(e) : dflt;
-}
-
 int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t* chain, const uint32_t* consts,
                       hipStream_t st) {
-  static const uint32_t prio = env_u32("FSDKR_COMB_BUILD_PRIO", 3);
+  // the levels are short launches on the exponents' critical path: at issue
+  // priority 3 the n = 64 call took 48.2 ms, at 0 51.1 (profiles/r04/r04m_ab_comb_v*)
+  constexpr uint32_t prio = 3;
   for (uint32_t lv = 1; lv <= j.p.h; ++lv) {
     const uint32_t o = j.level_off[lv - 1], nu = j.level_off[lv] - o;
-    CombBuildArgs ba{chain, d.ptoff, d.bmod, consts, d.comb, d.ulist + o, nu, j.p.h, j.p.v, j.p.pstep, j.nbase, prio};
+    CombBuildArgs ba{chain, d.ptoff, d.bmod, consts, d.comb, d.ulist + o, nu, j.p.h, j.p.v, j.p.pstep, j.nbase, prio,
+                     lv == 1 ? 1u : 0u};
     int rc = c->hip_check(launch_comb_build(j.k32, ba, st), "comb_build launch");
     if (rc) return rc;
   }
@@ -148,10 +146,8 @@ int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t
 // one comb_exp launch over n jobs of the same width
 static int comb_exp_launch(Ctx* c, const CombJob* const* jobs, const CombDev* devs, uint32_t n,
                            const uint32_t* consts, hipStream_t st, const char* tag) {
-  static const uint32_t prio = env_u32("FSDKR_COMB_EXP_PRIO", 0);
-  CombExpArgs ea{};
+  CombExpArgs ea{};   // default issue priority (1 or 2 measured no faster, profiles/r04/r04p_*)
   ea.consts = consts;
-  ea.prio = prio;
   size_t total = 0;
   for (uint32_t k = 0; k < n; ++k) {
     const CombJob& j = *jobs[k];

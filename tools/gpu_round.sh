@@ -12,6 +12,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of a short bench.py run -> prof/
 #   trace            kernel trace of whole n = 64 collect() calls + timeline of one -> trace_summary.txt
 #   trace4           the same for whole configs[4] collect_many() calls (1024 sessions) -> trace4_summary.txt
+#   trace256         the same for whole n = 256 collect() calls (configs[3])  -> trace256_summary.txt
 #   pmc64 | pmc256   one --pmc pass over whole n = 64 / n = 256 calls (tools/pmc_step.py)
 #                    -> pmc_step_n64.json / pmc_step_n256.json (per-call counter totals)
 #   pmcmx            PMC passes over the metric-2 modexp launch (tools/pmc.sh)
@@ -66,6 +67,11 @@ for step in "$@"; do
               || fail trace4 $? $OUT/trace4.log
             f=$(find $OUT/trace4 -name "*kernel_trace.csv" | head -1)
             python $R/tools/prof_summary.py "$f" --gap 19 --step -1 > $OUT/trace4_summary.txt || exit 1 ;;
+    trace256) (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace256 -o tr \
+                -- python3 $R/tools/prof_collect.py --full --n 256 --t 128 --joins 0 --steps 2 > $OUT/trace256.log 2>&1) \
+                || fail trace256 $? $OUT/trace256.log
+              f=$(find $OUT/trace256 -name "*kernel_trace.csv" | head -1)
+              python $R/tools/prof_summary.py "$f" --gap 10 --step -1 > $OUT/trace256_summary.txt || exit 1 ;;
     pmc64) pmc_step n64 --n 64 --joins 4 --t 32 ;;
     pmc256) pmc_step n256 --n 256 --joins 0 --t 128 ;;
     pmcmx) bash $R/tools/pmc.sh $TAG/pmcmx || exit 1 ;;
