@@ -374,33 +374,51 @@ def sessions_bench(ctx, count, steps, seed):
             "data": "synthetic (seeded GPU prover; keys are distinct products of pairs from a shared prime pool)"}
 
 
-def config3_bench(ctx, steps, seed, n=256, t=128):
+def config3_bench(ctx, steps, seed, n=256, t=128, dist=None, dev=None):
     """BASELINE configs[3] (the north_star target): RefreshMessage::collect at n = 256,
     t = 128, 2048-bit keys, 65 536 PDL + 65 536 Alice proofs + 256 ring-Pedersen +
-    256 correct-key proofs verified in ONE batched pass on ONE GPU (the whole
-    collect() call per step, as the headline), on n distinct refresh messages
-    from the seeded GPU prover (synth.synth_collect)."""
+    256 correct-key proofs verified in ONE batched pass (the whole collect() call
+    per step, as the headline), on n distinct refresh messages from the seeded GPU
+    prover (synth.synth_collect).  With a process group (bench.py --gpus N) every
+    rank runs shard.collect on its slice of the messages (one verdict all-reduce
+    per call) and the step time is the max over ranks."""
     import torch
-    from fsdkr import refresh, synth
+    from fsdkr import refresh, shard, synth
+    world = dist.get_world_size() if dist is not None else 1
     tg = time.perf_counter()
     msgs, joins, lk = synth.synth_collect(ctx, n, 0, t, seed)
     gen_s = time.perf_counter() - tg
     keys = [copy.deepcopy(lk) for _ in range(steps + 1)]
-    refresh.collect(msgs, keys[0], lk.paillier_dk, joins, ctx=ctx)   # warm-up + correctness gate
+
+    def call(key):
+        if dist is not None:
+            shard.collect(dist, msgs, key, lk.paillier_dk, joins, ctx, device=dev)
+        else:
+            refresh.collect(msgs, key, lk.paillier_dk, joins, ctx=ctx)
+    call(keys[0])   # warm-up + correctness gate
     assert keys[0].x_i != lk.x_i and len(keys[0].pk_vec) == n, "collect() did not update the LocalKey"
+    if dist is not None:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(steps):
-        refresh.collect(msgs, keys[s + 1], lk.paillier_dk, joins, ctx=ctx)
+        call(keys[s + 1])
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     el = (time.perf_counter() - t0) / steps
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
     proofs = proofs_of(n, 0, n)
+    where = "on ONE GPU" if world == 1 else f"sharded by refresh message over {world} GPUs (max over ranks)"
     return {"workload": f"RefreshMessage::collect n={n} t={t}: {n} refresh messages, M=256, 2048-bit N "
-                        f"(BASELINE configs[3], the north_star target) on ONE GPU; one step = the whole collect() "
-                        f"call", "n": n, "t": t, "proofs_per_step": proofs, "steps": steps, "ms_per_step": el * 1e3,
-            "value": proofs / el, "unit": "proofs/s", "workload_gen_s": gen_s,
-            "collect_efficiency": efficiency(collect_work(n, 0, n), collect_issued(n, 0, n), el,
-                                             pmc=pmc_per_call("n256")),
+                        f"(BASELINE configs[3], the north_star target) {where}; one step = the whole collect() "
+                        f"call", "n": n, "t": t, "n_gpus": world, "proofs_per_step": proofs, "steps": steps,
+            "ms_per_step": el * 1e3, "value": proofs / el, "unit": "proofs/s", "workload_gen_s": gen_s,
+            "collect_efficiency": efficiency(collect_work(n, 0, n), collect_issued(n, 0, n), el, world,
+                                             pmc=pmc_per_call("n256") if world == 1 else None),
             "data": f"synthetic (seeded GPU prover fs-dkr_amd/fsdkr/synth.py); {n} distinct refresh messages"}
 
 
@@ -538,6 +556,8 @@ def main():
     ms_per_step = elapsed / a.steps * 1e3
     proofs = proofs_of(R, J, n)
     value = proofs * a.steps / elapsed
+    # configs[3] (n = 256): on one GPU, or sharded over every rank of the group
+    c3 = config3_bench(ctx, a.config3_steps, a.seed + 3, dist=dist, dev=dev) if a.config3_steps and n != 256 else None
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -553,7 +573,6 @@ def main():
             cpu = cpu_baseline_python(msgs, joins, lk, 200)
             cpu["cpp_unavailable"] = str(e)
     s4 = sessions_bench(ctx, a.sessions, a.session_steps, a.seed + 4) if a.sessions and world == 1 else None
-    c3 = config3_bench(ctx, a.config3_steps, a.seed + 3) if a.config3_steps and world == 1 and n != 256 else None
     kg = keygen_bench(ctx) if world == 1 else None
     W_collect = collect_work(R, J, n)
     traffic, traffic_src = pmc_traffic(roof["count"])
