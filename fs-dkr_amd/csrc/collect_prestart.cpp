@@ -339,16 +339,37 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
     P += R * ns;
   }
   const uint32_t nn = 2 * nl;
-  // the inputs, at each session's own width, for the match in prepare
-  g.recv_n.clear();
-  g.s2.clear();
-  g.s.clear();
-  for (uint32_t k = 0; k < count; ++k) {
-    const fsdkr_collect_batch* b = bs + k;
-    const GaPre::Sess& x = ss[k];
-    g.recv_n.insert(g.recv_n.end(), b->recv_n, b->recv_n + (size_t)x.n * x.nl);
-    g.s2.insert(g.s2.end(), b->pdl_s2, b->pdl_s2 + (size_t)x.R * x.n * x.nl);
-    g.s.insert(g.s.end(), b->rp_s, b->rp_s + (size_t)x.R * x.n * x.nl);
+  // the inputs, at each session's own width, for the match in prepare (copied in
+  // parallel chunks: 67 MB at n = 256, on the path before GA starts)
+  size_t words_n = 0, words_p = 0;
+  for (const GaPre::Sess& x : ss) {
+    words_n += (size_t)x.n * x.nl;
+    words_p += (size_t)x.R * x.n * x.nl;
+  }
+  g.recv_n.resize(words_n);
+  g.s2.resize(words_p);
+  g.s.resize(words_p);
+  {
+    struct Cp { uint32_t* dst; const uint32_t* src; size_t words; };
+    std::vector<Cp> cps;
+    size_t on = 0, op = 0;
+    constexpr size_t kChunk = 1u << 18;   // 1 MB pieces
+    auto add = [&](uint32_t* dst, const uint32_t* src, size_t words) {
+      for (size_t o = 0; o < words; o += kChunk) cps.push_back(Cp{dst + o, src + o, std::min(kChunk, words - o)});
+    };
+    for (uint32_t k = 0; k < count; ++k) {
+      const fsdkr_collect_batch* b = bs + k;
+      const GaPre::Sess& x = ss[k];
+      const size_t wn = (size_t)x.n * x.nl, wp = (size_t)x.R * x.n * x.nl;
+      add(g.recv_n.data() + on, b->recv_n, wn);
+      add(g.s2.data() + op, b->pdl_s2, wp);
+      add(g.s.data() + op, b->rp_s, wp);
+      on += wn;
+      op += wp;
+    }
+    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
+      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].words * 4);
+    });
   }
   // image: [N^2 | N | s2 | s | descriptors], outputs after it
   auto al = Img::al;
@@ -366,11 +387,23 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
     c->fail("fsdkr_collect_prestart: device allocation of %zu bytes failed", total);
     return FSDKR_E_OOM;
   }
-  std::vector<uint8_t> img(o_out, 0);
-  uint32_t* NN = reinterpret_cast<uint32_t*>(img.data() + o_NN);
-  uint32_t* RN = reinterpret_cast<uint32_t*>(img.data() + o_rn);
-  uint32_t* S2 = reinterpret_cast<uint32_t*>(img.data() + o_s2);
-  uint32_t* S1 = reinterpret_cast<uint32_t*>(img.data() + o_s);
+  // the image in the pinned arena (prepare reuses it later: this H2D completes
+  // before the call returns), one fast H2D
+  uint8_t* img = c->host_arena(o_out);
+  if (!img) {
+    c->fail("fsdkr_collect_prestart: pinned host allocation of %zu bytes failed", o_out);
+    return FSDKR_E_OOM;
+  }
+  bool narrow = false;   // a session narrower than nl: its rows are zero-extended
+  for (const GaPre::Sess& x : ss) narrow = narrow || x.nl != nl;
+  parallel_for(narrow ? o_desc / 4096 + 1 : o_rn / 4096 + 1, 16, [&](size_t c0, size_t c1) {
+    const size_t lo = c0 * 4096, hi = std::min(c1 * 4096, narrow ? o_desc : o_rn);
+    if (lo < hi) memset(img + lo, 0, hi - lo);
+  });
+  uint32_t* NN = reinterpret_cast<uint32_t*>(img + o_NN);
+  uint32_t* RN = reinterpret_cast<uint32_t*>(img + o_rn);
+  uint32_t* S2 = reinterpret_cast<uint32_t*>(img + o_s2);
+  uint32_t* S1 = reinterpret_cast<uint32_t*>(img + o_s);
   std::vector<uint32_t> rbits(n);
   std::vector<uint32_t> sess_of_recv(n);
   for (uint32_t k = 0; k < count; ++k) std::fill(sess_of_recv.begin() + ss[k].rbase, sess_of_recv.begin() + ss[k].rbase + ss[k].n, k);
@@ -389,15 +422,17 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   for (uint32_t k = 0; k < count; ++k) {   // pair rows, zero-extended to nl
     const GaPre::Sess& x = ss[k];
     const size_t cnt = (size_t)x.R * x.n;
-    if (x.nl == nl) {
-      memcpy(S2 + x.pbase * nl, bs[k].pdl_s2, cnt * nl * 4);
-      memcpy(S1 + x.pbase * nl, bs[k].rp_s, cnt * nl * 4);
-    } else {
-      for (size_t q = 0; q < cnt; ++q) {
-        memcpy(S2 + (x.pbase + q) * nl, bs[k].pdl_s2 + q * x.nl, (size_t)x.nl * 4);
-        memcpy(S1 + (x.pbase + q) * nl, bs[k].rp_s + q * x.nl, (size_t)x.nl * 4);
+    parallel_for(cnt, 2048, [&](size_t q0, size_t q1) {
+      if (x.nl == nl) {
+        memcpy(S2 + (x.pbase + q0) * nl, bs[k].pdl_s2 + q0 * nl, (q1 - q0) * nl * 4);
+        memcpy(S1 + (x.pbase + q0) * nl, bs[k].rp_s + q0 * nl, (q1 - q0) * nl * 4);
+      } else {
+        for (size_t q = q0; q < q1; ++q) {
+          memcpy(S2 + (x.pbase + q) * nl, bs[k].pdl_s2 + q * x.nl, (size_t)x.nl * 4);
+          memcpy(S1 + (x.pbase + q) * nl, bs[k].rp_s + q * x.nl, (size_t)x.nl * 4);
+        }
       }
-    }
+    });
   }
   auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
   ModexpJob J1;
@@ -418,12 +453,13 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
     c->fail("fsdkr_collect_prestart: GA descriptors %zu > %zu bytes", desc.size(), desc_bytes);
     return FSDKR_E_ARG;
   }
-  memcpy(img.data() + o_desc, desc.data(), desc.size());
+  memcpy(img + o_desc, desc.data(), desc.size());
+  memset(img + o_desc + desc.size(), 0, o_out - o_desc - desc.size());
   hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
   StreamScope scope(c, gs);
   int rc;
-  if ((rc = c->hip_check(hipMemcpyAsync(dev, img.data(), img.size(), hipMemcpyHostToDevice, gs), "prestart H2D")) ||
-      (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // img is pageable and local
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_out, hipMemcpyHostToDevice, gs), "prestart H2D")) ||
+      (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // the arena is reused by prepare
     return rc;
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,

@@ -229,20 +229,13 @@ class CollectBatch:
         M = m_security
         G = _Gather()
         k = self._k
-        # ---- widths: nl covers every value of the nl / 2nl slots; ek.n and sigma get ckl
-        sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
-        f_ckn = G.field([m.ek.n for m in all_m] or [0])
-        ck_bits = max(1, f_ckn[1])
-        ck_short, f_sig = False, None
-        if not self.header_only:
-            ck_short = any(len(x) < M2 for x in sig)
-            f_sig = G.field([s for row in sig for s in row + [0] * (M2 - len(row))])
-            ck_bits = max(ck_bits, f_sig[1])
-        ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
-        if ckl is None:
-            raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
-        self._ga, self._pending = None, None
+        self._ga, self._pending, self._stage1b = None, None, None
         if self.header_only:
+            f_ckn = G.field([m.ek.n for m in all_m] or [0])
+            ck_bits = max(1, f_ckn[1])
+            ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
+            if ckl is None:
+                raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
             c.nl = 64 if ck_bits <= 2048 else 96
             c.ckl = max(ckl, c.nl)
             c.ck_n = k(G.slot(f_ckn, c.ckl))
@@ -261,35 +254,26 @@ class CollectBatch:
             rng = [m.range_proofs[i] for m in msgs for i in range(n)]
         # receivers (placeholders past the keys the LocalKey holds: odd modulus 3)
         rst = list(sts[:avail]) + [None] * (n - avail)
+        # gathered first: GA's fields and what sets stage 1's width; every other
+        # field is gathered by _rest() (stage1b / complete), after GA has started
         F = {"recv_n": G.field([x.n for x in keys[:avail]] + [3] * (n - avail)),
              "recv_ntilde": G.field([s.N if s else 3 for s in rst]),
              "recv_h1": G.field([s.g if s else 1 for s in rst]),
              "recv_h2": G.field([s.ni if s else 1 for s in rst]),
              "pdl_s2": G.field(pdl, "s2"), "rp_s": G.field(rng, "s")}
-        for a in ("s1", "s3"):
-            F["pdl_" + a] = G.field(pdl, a)
-        for a in ("s1", "s2"):
-            F["rp_" + a] = G.field(rng, a)
-        for a in ("S", "T", "N"):
+        for a in ("T", "N"):
             F["ped_" + a] = G.field([m.ring_pedersen_statement for m in all_m], a)
-        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
-        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
-        if any(len(x) < M for x in A) or any(len(z) < M for z in Z):
-            c.ped_lens = k(np.array([[len(x), len(z)] for x, z in zip(A, Z)], dtype=np.uint32))
-        F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
-        F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
-        c.s1l = _limbs_for(max(F["pdl_s1"][1], F["rp_s1"][1], 1))
-        c.s3l = _limbs_for(max(F["pdl_s3"][1], F["rp_s2"][1], 1))
-        c.zl = _limbs_for(max(F["ped_Z"][1], 1))
+        self._pending = dict(msgs=msgs, joins=joins, all_m=all_m, n=n, M=M, G=G, F=F, pdl=pdl, rng=rng,
+                             t=local_key.t, rest=False)
         # stage 1: the fields fsdkr_collect_prestart reads (GA's bases and moduli, the
         # h1/h2 table bases and the exponents that size the tables), at the width they
         # need; stage 2 (complete) keeps them if the batch width agrees
         ga_bits = max(1, *(F[x][1] for x in ("recv_n", "recv_ntilde", "recv_h1", "recv_h2", "pdl_s2", "rp_s",
                                               "ped_T", "ped_N")))
         nl_ga = 64 if ga_bits <= 2048 else 96 if ga_bits <= 3072 else None
-        self._ga = None
-        self._stage1b = None
         if staged and nl_ga is not None:
+            if not split_stage1 or ck_stage1:
+                self._rest()   # stage 1 then packs more than GA's own fields
             Gs = _Gather()
             # GA's own fields first when split: GA starts after converting 2Rn + n
             # values instead of every stage-1 field (stage1b() packs the rest; n = 64
@@ -300,26 +284,60 @@ class CollectBatch:
             # the correct-key job (sigma^n mod n) reads only ek.n and sigma: stage 1
             # packs them at the width complete() gives them, so the prestart runs
             # it beside GA (csrc/collect_prestart.cpp prestart_ck)
-            ck_pre = ck_stage1 and not ck_short and not split
+            st = self._pending
+            ck_pre = ck_stage1 and not st["ck_short"] and not split_stage1
             if ck_pre:
-                c.ckl = max(ckl, nl_ga)
-                ga["ck_n"] = Gs.slot(f_ckn, c.ckl)
-                ga["ck_sigma"] = Gs.slot(f_sig, c.ckl)
+                c.ckl = max(st["ckl"], nl_ga)
+                ga["ck_n"] = Gs.slot(st["f_ckn"], c.ckl)
+                ga["ck_sigma"] = Gs.slot(st["f_sig"], c.ckl)
             Gs.run()
             for name, arr in ga.items():
                 setattr(c, name, k(arr))
             c.nl = nl_ga
             self._ga = (nl_ga, ga)
-        self._pending = dict(msgs=msgs, joins=joins, all_m=all_m, n=n, M=M, G=G, F=F, ckl=ckl, f_ckn=f_ckn,
-                             f_sig=f_sig, ck_short=ck_short, sig=sig, pdl=pdl, rng=rng, t=local_key.t)
         if not staged:
             self.complete()
+
+    def _rest(self):
+        """The gathers stage 1 leaves for later (correct-key widths, the exponents
+        and ring-Pedersen vectors): their bit lengths set the slot widths s1l, s3l,
+        zl and ckl.  Runs once, from stage1b() or complete()."""
+        st = self._pending
+        if st is None or st["rest"]:
+            return
+        st["rest"] = True
+        c, k, G, F, M = self.c, self._k, st["G"], st["F"], st["M"]
+        all_m, pdl, rng = st["all_m"], st["pdl"], st["rng"]
+        sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
+        f_ckn = G.field([m.ek.n for m in all_m] or [0])
+        ck_short = any(len(x) < M2 for x in sig)
+        f_sig = G.field([s for row in sig for s in row + [0] * (M2 - len(row))])
+        ck_bits = max(1, f_ckn[1], f_sig[1])
+        ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
+        if ckl is None:
+            raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
+        for a in ("s1", "s3"):
+            F["pdl_" + a] = G.field(pdl, a)
+        for a in ("s1", "s2"):
+            F["rp_" + a] = G.field(rng, a)
+        F["ped_S"] = G.field([m.ring_pedersen_statement for m in all_m], "S")
+        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
+        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
+        if any(len(x) < M for x in A) or any(len(z) < M for z in Z):
+            c.ped_lens = k(np.array([[len(x), len(z)] for x, z in zip(A, Z)], dtype=np.uint32))
+        F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
+        F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
+        c.s1l = _limbs_for(max(F["pdl_s1"][1], F["rp_s1"][1], 1))
+        c.s3l = _limbs_for(max(F["pdl_s3"][1], F["rp_s2"][1], 1))
+        c.zl = _limbs_for(max(F["ped_Z"][1], 1))
+        st.update(ckl=ckl, f_ckn=f_ckn, f_sig=f_sig, ck_short=ck_short, sig=sig)
 
     def complete(self):
         """Stage 2 of a staged batch (CollectBatch(..., staged=True)): every other field."""
         st = getattr(self, "_pending", None)
         if st is None:
             return self
+        self._rest()
         self._pending = None
         c, k = self.c, self._k
         msgs, joins, all_m, n, M, G, F = (st[x] for x in ("msgs", "joins", "all_m", "n", "M", "G", "F"))
@@ -386,6 +404,7 @@ class CollectBatch:
         tables start)."""
         if not self._stage1b or self._pending is None or self._ga is None:
             return False
+        self._rest()
         F, c = self._pending["F"], self.c
         nl_ga, ga = self._ga
         Gs = _Gather()
