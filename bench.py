@@ -303,7 +303,7 @@ def pmc_traffic(count):
     return d["hbm_traffic_bytes"] * count / inst, os.path.relpath(files[-1], REPO)
 
 
-def phases(ctx, msgs, lk, joins, key_bits):
+def _phases_once(ctx, msgs, lk, joins, key_bits):
     """One instrumented collect, in refresh.collect's order: where the host time
     of a step goes (stage-1 pack, GA prestart, stage-2 pack overlapping the
     prestarted chains, prepare, pipeline launch, share-recovery launch (its host
@@ -343,6 +343,15 @@ def phases(ctx, msgs, lk, joins, key_bits):
                   "recovery_launch_ms": (tr - t3) * 1e3, "finish_wait_ms": (t4 - tr) * 1e3,
                   "recovery_finish_ms": (t45 - t4) * 1e3, "first_error_ms": (t5 - t45) * 1e3,
                   "device_pipeline_ms": min(runs)}
+
+
+def phases(ctx, msgs, lk, joins, key_bits, reps=3):
+    """_phases_once `reps` times (a fresh LocalKey each): the median of every
+    phase (one instrumented call is one sample of a ~50 ms call)."""
+    res = [_phases_once(ctx, msgs, copy.deepcopy(lk), joins, key_bits) for _ in range(reps)]
+    ph = {k: float(np.median([r[2][k] for r in res])) for k in res[0][2]}
+    ph["samples"] = reps
+    return res[-1][0], res[-1][1], ph
 
 
 def sessions_bench(ctx, count, steps, seed):

@@ -133,8 +133,12 @@ int collect_launch_impl(Ctx* c) {
   }
   {  // Feldman share checks (inputs only; one Horner chain per pair)
     hipStream_t ss = c->side_stream(6);
+    // one Horner chain of t+1 small-scalar steps per pair on one thread: ~2 % of
+    // GA's work at n = 256, but a long serial chain; at the default priority it
+    // was the last job of an 8-way n = 256 shard rank (64.5 of 85 ms,
+    // profiles/r04/r04w_*), so its waves take issue priority
     FeldmanArgs f{PI(pl.o_vss), PI(pl.o_Q), (const FeldmanInfo*)(dev + pl.d_finfo), (uint8_t*)(out_base + pl.x_fel),
-                  P};
+                  P, 3};
     c->mark("ec", true, ss);
     rc = c->hip_check(launch_feldman(f, ss), "feldman");
     c->mark("ec", false, ss);

@@ -82,6 +82,9 @@ __global__ void feldman_kernel(const FeldmanArgs a) {
   using namespace ec;
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= a.count) return;
+  if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
   const FeldmanInfo in = a.info[p];
   if (in.ncoef == 0) {
     a.verdict[p] = 2u;

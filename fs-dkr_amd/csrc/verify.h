@@ -94,6 +94,7 @@ struct FeldmanArgs {
   const FeldmanInfo* info;  // [count]
   uint8_t* verdict;         // [count] bit0 ok, bit1 panic
   uint32_t count;
+  uint32_t prio;            // s_setprio of the Horner threads (one long serial chain each)
 };
 
 // 2-adic half of a check modulo an even modulus N = 2^k * m (m odd):
