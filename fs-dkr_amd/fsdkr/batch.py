@@ -495,7 +495,7 @@ class SessionSet:
     CollectBatch; header-only sessions (threshold / size failures) are not
     prepared.  `live` lists the prepared sessions, in `structs` row order."""
 
-    def __init__(self, sessions, m_security=256, key_bits=2048, staged=False):
+    def __init__(self, sessions, m_security=256, key_bits=2048, staged=False, split_stage1=True):
         """staged: gather only what fsdkr_collect_prestart_multi reads (recv_n, PDL
         s2, range-proof s of the regular sessions; prestart_array) and leave the
         rest to complete(), so the longest chains run while it packs."""
@@ -522,8 +522,9 @@ class SessionSet:
         self._pending = (sessions, reg, M, key_bits)
         # the prestart covers the set only when every prepared session is regular
         # (prepare_multi's session list must equal the prestart's)
+        self._s1b = None   # a split stage 1's rest: (n, nl, M, its gathered fields)
         if staged and reg and len(reg) == len(self.live):
-            self._stage1(sessions, reg, M)
+            self._stage1(sessions, reg, M, split_stage1)
         if not staged:
             self.complete()
 
@@ -543,12 +544,14 @@ class SessionSet:
                                                           dtype=_BATCH_DT)[0]
         return self
 
-    def _stage1(self, sessions, reg, M):
+    def _stage1(self, sessions, reg, M, split=True):
         """The fields fsdkr_collect_prestart_multi reads: the GA chains' (receivers'
         N, PDL s2, range-proof s), the fixed-base tables' bases (receivers' N~,
         h1, h2; ring-Pedersen T and N) and the correct-key job's (ek.n, sigma).  The exponents stay in stage 2: the tables
         are sized by honest bounds (s1 < 2^770, s3 | s2 < 2^770 N~, Z < phi(N)),
-        which prepare checks against the packed exponents."""
+        which prepare checks against the packed exponents.  split: GA's fields
+        only, so GA starts after converting 2Rn + n values per session; stage1b()
+        packs the rest for a second prestart call."""
         ses = [sessions[s] for s in reg]
         R = np.array([len(m) for m, lk, j in ses], dtype=np.int64)
         n = R + np.array([len(j) for m, lk, j in ses], dtype=np.int64)
@@ -565,20 +568,14 @@ class SessionSet:
         am = [m for ms, lk, js in ses for m in ms + js]
         rps = [m.ring_pedersen_statement for m in am]
         f_T, f_N = G.field(rps, "T"), G.field(rps, "N")
-        # the correct-key job's inputs (ek.n, sigma_vec): the prestart runs it beside GA
-        f_ckn = G.field([m.ek.n for m in am])
-        f_sig = G.rows([m.dk_correctness_proof for m in am], "sigma_vec", M2)
         bits = max(1, f_rn[1], f_s2[1], f_s[1], f_nt[1], f_h1[1], f_h2[1], f_T[1], f_N[1])
         nl = 64 if bits <= 2048 else 96 if bits <= 3072 else None
         if nl is None:
             return
-        ckl = next((w for w in _CK_WIDTHS if max(1, f_ckn[1], f_sig[1]) <= 32 * w), None)
         a_rn, a_s2, a_s = G.slot(f_rn, nl), G.slot(f_s2, nl), G.slot(f_s, nl)
-        a_nt, a_h1, a_h2 = G.slot(f_nt, nl), G.slot(f_h1, nl), G.slot(f_h2, nl)
-        a_T, a_N = G.slot(f_T, nl), G.slot(f_N, nl)
-        if ckl is not None:
-            ckl = max(ckl, nl)
-            a_ckn, a_sig = G.slot(f_ckn, ckl), G.slot(f_sig, ckl)
+        rest = (f_nt, f_h1, f_h2, f_T, f_N, am)
+        if not split:
+            self._stage1_rest(G, n, nl, M, *rest)
         G.run()
 
         def starts(counts):
@@ -590,17 +587,56 @@ class SessionSet:
         st["recv_n"] = np.uint64(self._k(a_rn)) + starts(n) * np.uint64(nl * 4)
         st["pdl_s2"] = np.uint64(self._k(a_s2)) + starts(R * n) * np.uint64(nl * 4)
         st["rp_s"] = np.uint64(self._k(a_s)) + starts(R * n) * np.uint64(nl * 4)
-        for name, arr in (("recv_ntilde", a_nt), ("recv_h1", a_h1), ("recv_h2", a_h2)):
-            st[name] = np.uint64(self._k(arr)) + starts(n) * np.uint64(nl * 4)
-        for name, arr in (("ped_T", a_T), ("ped_N", a_N)):
-            st[name] = np.uint64(self._k(arr)) + starts(n) * np.uint64(nl * 4)   # R + J messages per session
         st["m_security"] = M
         st["s1l"], st["s3l"], st["zl"] = _limbs_for(770), nl + _limbs_for(770), nl
+        self._pre, self.n_prestart = st, len(reg)
+        if split:
+            self._s1b = (n, nl, M) + rest
+        else:
+            self._stage1_fill()
+
+    def _stage1_rest(self, G, n, nl, M, f_nt, f_h1, f_h2, f_T, f_N, am):
+        """slots of the tables' bases and the correct-key inputs (converted by G.run)"""
+        f_ckn = G.field([m.ek.n for m in am])
+        f_sig = G.rows([m.dk_correctness_proof for m in am], "sigma_vec", M2)
+        ckl = next((w for w in _CK_WIDTHS if max(1, f_ckn[1], f_sig[1]) <= 32 * w), None)
+        arrs = {"recv_ntilde": G.slot(f_nt, nl), "recv_h1": G.slot(f_h1, nl), "recv_h2": G.slot(f_h2, nl),
+                "ped_T": G.slot(f_T, nl), "ped_N": G.slot(f_N, nl)}
+        if ckl is not None:
+            ckl = max(ckl, nl)
+            arrs["ck_n"], arrs["ck_sigma"] = G.slot(f_ckn, ckl), G.slot(f_sig, ckl)
+        self._s1_arrs = (n, nl, ckl, arrs)
+
+    def _stage1_fill(self):
+        """point the prestart rows at _stage1_rest's converted arrays"""
+        n, nl, ckl, arrs = self._s1_arrs
+        st = self._pre
+
+        def starts(counts):
+            return np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.uint64)
+        for name in ("recv_ntilde", "recv_h1", "recv_h2"):
+            st[name] = np.uint64(self._k(arrs[name])) + starts(n) * np.uint64(nl * 4)
+        for name in ("ped_T", "ped_N"):
+            st[name] = np.uint64(self._k(arrs[name])) + starts(n) * np.uint64(nl * 4)   # R + J messages per session
         if ckl is not None:
             st["ckl"] = ckl
-            st["ck_n"] = np.uint64(self._k(a_ckn)) + starts(n) * np.uint64(ckl * 4)
-            st["ck_sigma"] = np.uint64(self._k(a_sig)) + starts(n * M2) * np.uint64(ckl * 4)
-        self._pre, self.n_prestart = st, len(reg)
+            st["ck_n"] = np.uint64(self._k(arrs["ck_n"])) + starts(n) * np.uint64(ckl * 4)
+            st["ck_sigma"] = np.uint64(self._k(arrs["ck_sigma"])) + starts(n * M2) * np.uint64(ckl * 4)
+
+    def stage1b(self):
+        """The rest of a split stage 1 (the fixed-base tables' bases, the
+        correct-key inputs) for a second fsdkr_collect_prestart_multi call (GA
+        keeps running; the table chains and the correct-key job start).  True when
+        it packed them."""
+        if self._s1b is None or self._pre is None or self._pending is None:
+            return False
+        n, nl, M, *rest = self._s1b
+        self._s1b = None
+        G = _Gather(self._owned)
+        self._stage1_rest(G, n, nl, M, *rest)
+        G.run()
+        self._stage1_fill()
+        return True
 
     def stage_z(self):
         """Stage 1b of a staged set: the ring-Pedersen Z rows of every regular

@@ -282,6 +282,8 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="sp
     sset = SessionSet([(r, lk, j) for r, lk, dk, j in sess], m_security, key_bits, staged=True)
     if sset.n_prestart:   # every session's s2^N, s^N mod N^2 chains start while the rest is packed
         ctx.collect_prestart_set(sset)
+        if sset.stage1b():   # the table bases and correct-key inputs: those jobs start beside GA
+            ctx.collect_prestart_set(sset)
         if sset.stage_z():   # then the ring-Pedersen T^Z exponents behind the T tables
             ctx.collect_prestart_rp_set(sset)
     sset.complete()
@@ -424,14 +426,19 @@ def _speculative_launch(ctx, jobs):
 
 
 def _finish_both(ctx, finish, pend):
-    """finish() the launched verification batch, then the launched share recovery
-    (pend, or None) even when finish() raises: a recovery left in flight would
-    refuse every later fsdkr_collect_recover_launch on the context.  Returns
-    (finish()'s verdicts, the recovery results or None)."""
+    """Finish the launched share recovery (pend, or None), then finish() the
+    launched verification batch, each even when the other raises: neither stays
+    in flight (a recovery left in flight would refuse every later
+    fsdkr_collect_recover_launch on the context).  The recovery goes first: its
+    GPU work ends well before the pipeline's, so its host combination overlaps
+    the pipeline instead of following it (configs[4]: ~25 ms of 1024 sessions).
+    Returns (finish()'s verdicts, the recovery results or None)."""
+    specs = None
     try:
-        verdicts = finish()
+        if pend is not None:
+            specs = _speculative_finish(ctx, pend)
     finally:
-        specs = _speculative_finish(ctx, pend) if pend is not None else None
+        verdicts = finish()
     return verdicts, specs
 
 

@@ -201,6 +201,8 @@ def test_config4_prestart_hit_and_miss(gpu_ctx):
             pre = SessionSet(prestart_of, 256, 3072, staged=True)
             assert pre.n_prestart == 6
             gpu_ctx.collect_prestart_set(pre)
+            if pre.stage1b():
+                gpu_ctx.collect_prestart_set(pre)
         sset = SessionSet(work, 256, 3072)
         gpu_ctx.collect_prepare_set(sset)
         gpu_ctx.collect_launch()
@@ -233,6 +235,8 @@ def test_config4_prestarted_ring_pedersen_hit_and_miss(gpu_ctx):
     def run(target, prestart_of):
         if prestart_of is not None:
             pre = SessionSet(prestart_of, 256, 3072, staged=True)
+            gpu_ctx.collect_prestart_set(pre)
+            assert pre.stage1b()
             gpu_ctx.collect_prestart_set(pre)
             assert pre.stage_z()
             gpu_ctx.collect_prestart_rp_set(pre)

@@ -247,6 +247,7 @@ def test_session_set_stage1_correct_key_rows():
     from fsdkr.batch import M2, SessionSet
     sess = fake_sessions(5, seed=4)
     ss = SessionSet(sess, 256, 3072, staged=True)
+    assert int(ss._pre["ckl"][0]) == 0 and ss.stage1b() and not ss.stage1b()   # split: GA's fields first
     pre = ss._pre
     ckl = int(pre["ckl"][0])
     assert ckl == 96

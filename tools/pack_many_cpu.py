@@ -74,9 +74,14 @@ def main():
         t0 = time.perf_counter()
         sset = SessionSet(sess, 256, 3072, staged=True)
         t1 = time.perf_counter()
+        sset.stage1b()
+        tb = time.perf_counter()
+        sset.stage_z()
+        tz = time.perf_counter()
         sset.complete()
         t2 = time.perf_counter()
-        out = {"sessions": a.sessions, "stage1_ms": (t1 - t0) * 1e3, "stage2_ms": (t2 - t1) * 1e3}
+        out = {"sessions": a.sessions, "stage1_ms": (t1 - t0) * 1e3, "stage1b_ms": (tb - t1) * 1e3,
+               "stage_z_ms": (tz - tb) * 1e3, "stage2_ms": (t2 - tz) * 1e3}
         out.update({k.strip("_") + "_ms": v for k, v in acc.items()})
         print(json.dumps(out), flush=True)
         del sset

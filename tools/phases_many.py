@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase times of refresh.collect_many over BASELINE configs[4] (S independent
 t=1 n=3 sessions, 3072-bit keys), in collect_many's own order: stage-1 gather,
-GA prestart, stage-2 gather, multi-session prepare, launch, share-recovery
+GA prestart, stage 1b (Z) + the T^Z prestart, stage-2 gather, multi-session prepare, launch, share-recovery
 launch, finish wait, recovery finish, per-session first error + key updates;
 then the whole collect_many call and the device pipeline alone.  With
 --gap-ms each instrumented call is preceded by an idle gap, so a rocprofv3
@@ -41,6 +41,11 @@ def main():
         t.append(time.perf_counter())
         ctx.collect_prestart_set(sset)
         t.append(time.perf_counter())
+        if sset.stage1b():   # the table bases and correct-key inputs, a second prestart call
+            ctx.collect_prestart_set(sset)
+        if sset.stage_z():   # stage 1b (the ring-Pedersen Z rows), then the T^Z combs
+            ctx.collect_prestart_rp_set(sset)
+        t.append(time.perf_counter())
         sset.complete()
         t.append(time.perf_counter())
         ctx.collect_prepare_set(sset)
@@ -59,7 +64,7 @@ def main():
             assert e.variant == 0 and not isinstance(sp, Exception)
             _apply_share(lk, dk, sp)
         t.append(time.perf_counter())
-        names = ["stage1_ms", "prestart_ms", "stage2_ms", "prepare_ms", "launch_ms", "recovery_launch_ms",
+        names = ["stage1_ms", "prestart_ms", "stage1b_z_prestart_rp_ms", "stage2_ms", "prepare_ms", "launch_ms", "recovery_launch_ms",
                  "finish_wait_ms", "recovery_finish_ms", "map_apply_ms"]
         out = {"sessions": a.sessions}
         out.update({k: (t[i + 1] - t[i]) * 1e3 for i, k in enumerate(names)})
