@@ -302,9 +302,11 @@ typedef struct fsdkr_error {
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out);
 
 /* Fixed-base batch: out[i] = bases[base_idx[i]] ^ exp[i] mod mods[base_mod_idx[base_idx[i]]]
- * (exact).  The GPU builds one table of base^(2^(w j)) per base and evaluates
- * every exponent with Brickell-Gordon-McCurley-Wilson windowing; results are
- * identical to fsdkr_modexp_batch.  This is the engine behind the bases the
+ * (exact).  The GPU builds one squaring chain of base^(2^(w j)) per base and
+ * evaluates every exponent with Brickell-Gordon-McCurley-Wilson windowing, or,
+ * when many exponents share a base, with a Lim-Lee comb over the chain (tables
+ * of 2^h products per base: b - 1 squarings and v b products per exponent;
+ * FSDKR_FB_COMB=0 forces BGMW); results are identical to fsdkr_modexp_batch.  This is the engine behind the bases the
  * reference exponentiates many times with curv BigInt::mod_pow: h1, h2 of a
  * receiver's DLogStatement (zk_pdl_with_slack.rs:144-157, range_proofs.rs:129-137)
  * and ring-Pedersen T (ring_pedersen_proof.rs:144).  mod_limbs in {64, 96}. */
