@@ -253,8 +253,10 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
 // wave takes the same path.  For a 2048-bit exponent at w = 6: 2048 squarings
 // and ~325 other products instead of 2045 + 441 (fixed 5-bit windows).  Results
 // are bit-identical to base^exp mod N.
+// (at most 256 registers per lane: two waves per SIMD, like modexp_kernel's
+// 4-lane shape; unbounded, the 4-lane schedule state took 256 VGPRs + 27 AGPRs)
 template <int KD, int G, int K32, bool QS>
-__global__ __launch_bounds__(BLOCK) void modexp_slide_kernel(const ModexpArgs a) {
+__global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
@@ -278,8 +280,15 @@ __global__ __launch_bounds__(BLOCK) void modexp_slide_kernel(const ModexpArgs a)
   M.ninv = C[3 * KD];
   const uint32_t w = a.window, tw = 1u << (w - 1);   // odd powers T[0..tw), x^2 at T[tw]
   uint32_t* T = a.table + (size_t)inst * (tw + 1) * KD;
-  const uint32_t* E = reinterpret_cast<const uint32_t*>(a.exp_ptr[inst]);
-  const int exp_limbs = (int)a.exp_len[inst];
+  // the wave's instances share the exponent (the caller's layout): its address
+  // and length are made wave-uniform, so the window schedule below runs on the
+  // scalar unit in SGPRs (per-lane copies held the 4-lane shape at 256 VGPRs +
+  // 29 AGPRs, one wave per SIMD)
+  const uint64_t ea = a.exp_ptr[inst];
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ea >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ea));
+  const int exp_limbs = __builtin_amdgcn_readfirstlane((int)a.exp_len[inst]);
   auto bit = [&](int i) -> uint32_t { return (E[i >> 5] >> (i & 31)) & 1u; };
   int top = 32 * exp_limbs - 1;
   while (top >= 0 && E[top >> 5] == 0) top = (top & ~31) - 1;   // skip zero limbs
