@@ -9,7 +9,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <map>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <vector>
@@ -86,6 +89,105 @@ unsigned host_threads() {
     return hw ? std::min(hw, 16u) : 4u;
   }();
   return n;
+}
+
+namespace {
+thread_local bool tl_pool_worker = false;
+
+struct PoolJob {
+  void (*fn)(void*, size_t);
+  void* arg;
+  size_t chunks;
+  std::atomic<size_t> next{0};
+  size_t done = 0;   // chunks finished (under the pool mutex)
+  int active = 0;    // workers holding the job (under the pool mutex)
+};
+
+// Parked workers: a run publishes its job under the mutex and bumps the
+// generation; every worker takes chunks until none is left, then reports them.
+// The job lives on the caller's stack until every chunk is done and no worker
+// holds it.
+struct HostPool {
+  std::mutex run_m;   // one run at a time
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  PoolJob* cur = nullptr;
+  uint64_t gen = 0;
+
+  explicit HostPool(unsigned workers) {
+    for (unsigned k = 0; k < workers; ++k) std::thread([this] { loop(); }).detach();
+  }
+  static size_t drain(PoolJob& j) {
+    size_t did = 0;
+    for (;;) {
+      const size_t c = j.next.fetch_add(1);
+      if (c >= j.chunks) return did;
+      j.fn(j.arg, c);
+      ++did;
+    }
+  }
+  void loop() {
+    tl_pool_worker = true;
+    uint64_t seen = 0;
+    for (;;) {
+      PoolJob* j;
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return gen != seen && cur != nullptr; });
+        seen = gen;
+        j = cur;
+        ++j->active;
+      }
+      const size_t did = drain(*j);
+      {
+        std::lock_guard<std::mutex> l(m);
+        j->done += did;
+        --j->active;
+      }
+      done_cv.notify_all();
+    }
+  }
+  void run(PoolJob& j) {
+    {
+      std::lock_guard<std::mutex> l(m);
+      cur = &j;
+      ++gen;
+    }
+    cv.notify_all();
+    const size_t did = drain(j);
+    std::unique_lock<std::mutex> l(m);
+    j.done += did;
+    done_cv.wait(l, [&] { return j.done == j.chunks && j.active == 0; });
+    cur = nullptr;
+  }
+};
+
+HostPool& host_pool() {
+  static HostPool* p = new HostPool(host_threads() > 1 ? host_threads() - 1 : 0);   // never destroyed: workers parked
+  return *p;
+}
+}  // namespace
+
+void host_pool_run(size_t chunks, void (*fn)(void*, size_t), void* arg) {
+  if (chunks == 0) return;
+  if (chunks == 1) {
+    fn(arg, 0);
+    return;
+  }
+  HostPool& p = host_pool();
+  std::unique_lock<std::mutex> busy(p.run_m, std::defer_lock);
+  if (tl_pool_worker || !busy.try_lock()) {   // nested or concurrent: fresh threads
+    std::vector<std::thread> th;
+    for (size_t c = 1; c < chunks; ++c) th.emplace_back([=] { fn(arg, c); });
+    fn(arg, 0);
+    for (auto& t : th) t.join();
+    return;
+  }
+  PoolJob j;
+  j.fn = fn;
+  j.arg = arg;
+  j.chunks = chunks;
+  p.run(j);
 }
 
 size_t Ctx::tbeg(const char* name, hipStream_t st) {

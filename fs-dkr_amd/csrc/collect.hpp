@@ -149,11 +149,14 @@ inline void parallel_for(size_t n, size_t grain, F&& f) {
     f((size_t)0, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(chunks - 1);
-  for (size_t c = 1; c < chunks; ++c) th.emplace_back([&, c] { f(n * c / chunks, n * (c + 1) / chunks); });
-  f((size_t)0, n / chunks);
-  for (auto& t : th) t.join();
+  struct Part {
+    F* f;
+    size_t n, chunks;
+  } part{&f, n, chunks};
+  host_pool_run(chunks, [](void* a, size_t c) {
+    const Part& x = *static_cast<const Part*>(a);
+    (*x.f)(x.n * c / x.chunks, x.n * (c + 1) / x.chunks);
+  }, &part);
 }
 
 // FSDKR_PREP_PROFILE=1: host pre-pass phase times on stderr (diagnostics)

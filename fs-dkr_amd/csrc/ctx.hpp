@@ -108,6 +108,13 @@ struct CtScope {
 // OMP_NUM_THREADS, else min(hardware threads, 16)).
 unsigned host_threads();
 
+// fn(arg, c) for every c in [0, chunks), on a process-wide pool of
+// host_threads() - 1 parked worker threads and the calling thread; returns when
+// every chunk is done.  A call from a pool worker, or while another thread's
+// call runs, uses fresh threads instead (the collect() pre-pass issues a dozen
+// of these per call: spawning 15 threads each time cost ~0.2-0.5 ms apiece).
+void host_pool_run(size_t chunks, void (*fn)(void*, size_t), void* arg);
+
 // A batch of modexp instances of one modulus width (k32 limbs) and one
 // exponent-length class (exp_bits = max bits; sets the window count).
 struct ModexpJob {

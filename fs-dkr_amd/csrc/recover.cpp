@@ -33,10 +33,14 @@ void parallel_for_host(size_t n, size_t grain, F&& f) {
     f((size_t)0, n);
     return;
   }
-  std::vector<std::thread> th;
-  for (size_t k = 1; k < chunks; ++k) th.emplace_back([&, k] { f(n * k / chunks, n * (k + 1) / chunks); });
-  f((size_t)0, n / chunks);
-  for (auto& t : th) t.join();
+  struct Part {
+    F* f;
+    size_t n, chunks;
+  } part{&f, n, chunks};
+  host_pool_run(chunks, [](void* a, size_t c) {
+    const Part& x = *static_cast<const Part*>(a);
+    (*x.f)(x.n * c / x.chunks, x.n * (c + 1) / x.chunks);
+  }, &part);
 }
 }  // namespace
 
