@@ -308,10 +308,14 @@ class CollectBatch:
         st["rest"] = True
         c, k, G, F, M = self.c, self._k, st["G"], st["F"], st["M"]
         all_m, pdl, rng = st["all_m"], st["pdl"], st["rng"]
-        sig = [list(m.dk_correctness_proof.sigma_vec[:M2]) for m in all_m]
         f_ckn = G.field([m.ek.n for m in all_m] or [0])
-        ck_short = any(len(x) < M2 for x in sig)
-        f_sig = G.field([s for row in sig for s in row + [0] * (M2 - len(row))])
+        dkp = [m.dk_correctness_proof for m in all_m]
+        ck_short = any(len(d.sigma_vec) < M2 for d in dkp)
+        sig = [list(d.sigma_vec[:M2]) for d in dkp] if ck_short else None
+        if ck_short:   # short vectors: zero-padded rows (the verdict reports them)
+            f_sig = G.field([s for row in sig for s in row + [0] * (M2 - len(row))])
+        else:          # the common case: the first M2 of every vector, flattened in C
+            f_sig = G.rows(dkp, "sigma_vec", M2)
         ck_bits = max(1, f_ckn[1], f_sig[1])
         ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
         if ckl is None:
@@ -321,12 +325,16 @@ class CollectBatch:
         for a in ("s1", "s2"):
             F["rp_" + a] = G.field(rng, a)
         F["ped_S"] = G.field([m.ring_pedersen_statement for m in all_m], "S")
-        A = [list(m.ring_pedersen_proof.A[:M]) for m in all_m]
-        Z = [list(m.ring_pedersen_proof.Z[:M]) for m in all_m]
-        if any(len(x) < M for x in A) or any(len(z) < M for z in Z):
-            c.ped_lens = k(np.array([[len(x), len(z)] for x, z in zip(A, Z)], dtype=np.uint32))
-        F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
-        F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
+        rpp = [m.ring_pedersen_proof for m in all_m]
+        if any(len(r.A) < M or len(r.Z) < M for r in rpp):   # short vectors: zero-padded rows
+            c.ped_lens = k(np.array([[min(len(r.A), M), min(len(r.Z), M)] for r in rpp], dtype=np.uint32))
+            A = [list(r.A[:M]) for r in rpp]
+            Z = [list(r.Z[:M]) for r in rpp]
+            F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
+            F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
+        else:   # the first M of every vector, flattened in C
+            F["ped_A"] = G.rows(rpp, "A", M)
+            F["ped_Z"] = G.rows(rpp, "Z", M)
         c.s1l = _limbs_for(max(F["pdl_s1"][1], F["rp_s1"][1], 1))
         c.s3l = _limbs_for(max(F["pdl_s3"][1], F["rp_s2"][1], 1))
         c.zl = _limbs_for(max(F["ped_Z"][1], 1))
