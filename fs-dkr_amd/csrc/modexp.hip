@@ -559,13 +559,18 @@ hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint3
   return mod_setup(k32, mods, n_mod, consts, st);
 }
 
+// The constants depend on KD only (exact values), so the setup runs in a light
+// shape: few VGPRs and little LDS, so a setup at the head of a job's chain is
+// dispatched beside long-running waves instead of waiting for a whole free slot
+// (the 2-lane 2048-bit setup took 222 VGPRs and 36 KB per block and waited up to
+// 29 ms behind an 8-way n = 256 rank's GA, profiles/r04/r04ad_*).
 hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
   switch (k32) {
     case 32: return launch_setup<36, 2, 32>(mods, n_mod, consts, st);
-    case 64: return launch_setup<72, 2, 64>(mods, n_mod, consts, st);
+    case 64: return launch_setup<72, 8, 64>(mods, n_mod, consts, st);
     case 96: return launch_setup<108, 4, 96>(mods, n_mod, consts, st);
-    case 128: return launch_setup<144, 4, 128>(mods, n_mod, consts, st);
-    case 192: return launch_setup<216, 4, 192>(mods, n_mod, consts, st);
+    case 128: return launch_setup<144, 16, 128>(mods, n_mod, consts, st);
+    case 192: return launch_setup<216, 8, 192>(mods, n_mod, consts, st);
     default: return hipErrorInvalidValue;
   }
 }
