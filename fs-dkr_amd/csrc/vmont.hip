@@ -173,10 +173,12 @@ static hipError_t eq_launch(const EqCheckArgs& a, hipStream_t st) {
 hipError_t launch_eq_check(uint32_t k32, const EqCheckArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
   switch (k32) {
-    case 64: return eq_launch<72, 2, 64>(a, st);
+    // 8-lane shapes: a few products per instance; the 2/4-lane shapes spilled
+    // (256 VGPRs + 256 AGPRs + scratch) at the tail of every pipeline
+    case 64: return eq_launch<72, 8, 64>(a, st);
     case 96: return eq_launch<108, 4, 96>(a, st);
-    case 128: return eq_launch<144, 4, 128>(a, st);
-    case 192: return eq_launch<216, 4, 192>(a, st);
+    case 128: return eq_launch<144, 8, 128>(a, st);
+    case 192: return eq_launch<216, 8, 192>(a, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -188,10 +190,10 @@ static hipError_t p3_launch(const Prod3Args& a, hipStream_t st) {
 hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
   switch (k32) {
-    case 64: return p3_launch<72, 2, 64>(a, st);
+    case 64: return p3_launch<72, 8, 64>(a, st);
     case 96: return p3_launch<108, 4, 96>(a, st);
-    case 128: return p3_launch<144, 4, 128>(a, st);
-    case 192: return p3_launch<216, 4, 192>(a, st);
+    case 128: return p3_launch<144, 8, 128>(a, st);
+    case 192: return p3_launch<216, 8, 192>(a, st);
     default: return hipErrorInvalidValue;
   }
 }
