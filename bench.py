@@ -327,11 +327,13 @@ def _phases_once(ctx, msgs, lk, joins, key_bits):
     tr = time.perf_counter()
     v = ctx.collect_finish(b)
     t4 = time.perf_counter()
+    span = ctx.collect_last_span_ms()
     _speculative_finish(ctx, pend)
     t45 = time.perf_counter()
     b.first_error(v)
     t5 = time.perf_counter()
-    # the device pipeline alone on the prepared batch (no host work)
+    # the device pipeline alone on the prepared batch (no host work, and no
+    # prestart: GA runs inside it from a cold start)
     ctx.collect_prepare(b)
     runs = []
     for _ in range(3):
@@ -342,7 +344,7 @@ def _phases_once(ctx, msgs, lk, joins, key_bits):
                   "pack_stage2_ms": (t1 - tp) * 1e3, "prepare_ms": (t2 - t1) * 1e3, "launch_ms": (t3 - t2) * 1e3,
                   "recovery_launch_ms": (tr - t3) * 1e3, "finish_wait_ms": (t4 - tr) * 1e3,
                   "recovery_finish_ms": (t45 - t4) * 1e3, "first_error_ms": (t5 - t45) * 1e3,
-                  "device_pipeline_ms": min(runs)}
+                  "device_pipeline_ms": min(runs), "call_device_span_ms": span}
 
 
 def phases(ctx, msgs, lk, joins, key_bits, reps=3):

@@ -501,7 +501,22 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
   fsdkr::free_collect_plan(c);
   fsdkr::free_ga_pre(c);
   fsdkr::free_recover(c);
+  if (c->span_beg) (void)hipEventDestroy(c->span_beg);
+  if (c->span_end) (void)hipEventDestroy(c->span_end);
   delete c;
+}
+
+int Ctx::span_begin(hipStream_t st) {
+  if (!span_beg && hipEventCreate(&span_beg) != hipSuccess) return hip_check(hipErrorOutOfMemory, "span event");
+  if (!span_end && hipEventCreate(&span_end) != hipSuccess) return hip_check(hipErrorOutOfMemory, "span event");
+  span_armed = true;
+  span_ms = -1.0f;
+  return hip_check(hipEventRecord(span_beg, st), "span event record");
+}
+
+double fsdkr_collect_last_span_ms(const fsdkr_ctx* ctx) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  return c ? (double)c->span_ms : -1.0;
 }
 
 const char* fsdkr_last_error(const fsdkr_ctx* ctx) {

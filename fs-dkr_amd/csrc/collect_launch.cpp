@@ -27,6 +27,7 @@ int collect_launch_impl(Ctx* c) {
   auto PI = [&](size_t o) { return (const uint32_t*)(dev + o); };
   int rc;
   hipStream_t st = c->stream;
+  if (!c->span_armed && (rc = c->span_begin(st))) return rc;   // no prestart: the span starts here
   // the alice pre-verdicts become the initial range verdicts
   if ((rc = c->hip_check(hipMemcpyAsync(out_base + pl.x_rng, dev + pl.d_alpre, P, hipMemcpyDeviceToDevice, st), "D2D")))
     return rc;
@@ -241,6 +242,7 @@ int collect_launch_impl(Ctx* c) {
     c->mark("alice_hash", false);
     if (rc) return rc;
   }
+  if (c->span_armed && (rc = c->hip_check(hipEventRecord(c->span_end, st), "span event record"))) return rc;
   pl.launched = true;
   return FSDKR_OK;
 }
@@ -288,6 +290,10 @@ int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
       (rc = D2H(pdlv.data(), pl.x_pdlv, P)) || (rc = D2H(rng.data(), pl.x_rng, P)))
     return rc;
   if ((rc = c->sync())) return rc;
+  if (c->span_armed) {
+    c->span_armed = false;
+    if (hipEventElapsedTime(&c->span_ms, c->span_beg, c->span_end) != hipSuccess) c->span_ms = -1.0f;
+  }
   // PDL unit test of c: c^eA witnesses it unless eA == 0 / the Alice proof was rejected early
   std::vector<uint32_t> unit_c_pdl(unn.begin(), unn.begin() + P);
   for (size_t k = 0; k < pl.cpdl_extra.size(); ++k) unit_c_pdl[pl.cpdl_extra[k]] = unn[P + k];

@@ -461,6 +461,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_out, hipMemcpyHostToDevice, gs), "prestart H2D")) ||
       (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // the arena is reused by prepare
     return rc;
+  if ((rc = c->span_begin(gs))) return rc;   // the call's first device work
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
                          group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))

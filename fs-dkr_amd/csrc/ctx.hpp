@@ -73,6 +73,13 @@ struct Ctx {
   uint32_t ga_cus = 0;
   // CU mask words of a balanced set of `count` CUs (in = true) or of its complement
   std::vector<uint32_t> cu_mask(uint32_t count, bool in) const;
+  // device span of the last collect() call: a timing event at the first device
+  // work of the call (prestart H2D done, else the pipeline launch) and one after
+  // the pipeline's last kernel; finish turns them into span_ms
+  hipEvent_t span_beg = nullptr, span_end = nullptr;
+  bool span_armed = false;
+  float span_ms = -1.0f;
+  int span_begin(hipStream_t st);
   // synchronise the stream and fold pending events into `times`
   int sync();
 };

@@ -382,7 +382,12 @@ struct Mont29 {
     for (int cyc = 0; cyc < G; ++cyc) {
       // values unchanged; only the optimiser's view of them is reset (see opaque)
       opaque<L>(b);
-      opaque<L>(n);
+      // not n in the short-lane squarings (b2 held): there the per-cycle
+      // barrier made the register allocator rotate the modulus digits through
+      // copies every cycle (16 lanes: 183 -> 171 VALU per 9-row squaring cycle
+      // of the sliding-window kernel, 8 lanes: 649 -> 625 per 18 rows, and
+      // 4 fewer VGPRs); their zext is not hoisted there either
+      if constexpr (!(SQ && USE_B2)) opaque<L>(n);
       if constexpr (SQ && USE_B2) opaque<L>(b2);
       cycle<SQ, QS>(acc, b, b2, n, a_lds + cyc * L, cur, cyc + 1 < G ? (uint32_t)L : 0u,
                     std::make_integer_sequence<int, L>{});

@@ -141,6 +141,8 @@ def lib():
     L.fsdkr_collect_launch.restype = ctypes.c_int
     L.fsdkr_collect_prestart.argtypes = [vp, ctypes.POINTER(CollectBatchC)]
     L.fsdkr_collect_prestart.restype = ctypes.c_int
+    L.fsdkr_collect_last_span_ms.argtypes = [vp]
+    L.fsdkr_collect_last_span_ms.restype = ctypes.c_double
     L.fsdkr_collect_finish.argtypes = [vp, ctypes.POINTER(VerdictsC)]
     L.fsdkr_collect_finish.restype = ctypes.c_int
     L.fsdkr_collect_prepare_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
@@ -367,6 +369,11 @@ class Context:
         """Start the s^N mod N^2 chains of a batch whose GA fields are packed
         (CollectBatch(..., staged=True)); the next prepare of it reuses them."""
         self.check(self._lib.fsdkr_collect_prestart(self._h, ctypes.byref(batch.c)))
+
+    def collect_last_span_ms(self):
+        """Device span of the last finished collect() call (HIP events: first
+        device work -> the pipeline's last kernel), -1 before any."""
+        return float(self._lib.fsdkr_collect_last_span_ms(self._h))
 
     def collect_launch(self):
         """Enqueue the kernel pipeline of the prepared batch (returns at once)."""

@@ -237,6 +237,13 @@ int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
  * starts only the parts that are new. */
 int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
 
+/* Device span of the last finished collect() call (single or multi-session), in
+ * ms from HIP timing events: from the call's first device work (the end of the
+ * prestart's upload, or the pipeline launch when nothing was prestarted) to the
+ * end of the pipeline's last kernel.  -1 before the first finish.  Diagnostic
+ * only; the reference has no counterpart. */
+double fsdkr_collect_last_span_ms(const fsdkr_ctx* ctx);
+
 /* ---- Many independent collect() calls in ONE device pass -------------------
  * `count` sessions (e.g. BASELINE configs[4]: 1024 custody wallets, t=1 n=3,
  * 3072-bit keys), each the batch its own RefreshMessage::collect
