@@ -183,6 +183,18 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
         for (int j = 0; j < L; ++j) acc[j] = T[(size_t)d0 * KD + g * L + j];
       }
     }
+    if (st >= n_build && st < n_steps - 1 && sub < w) {
+      // the window's squarings in a loop of their own (no step logic or
+      // register shuffles of the general step between them), then this
+      // iteration continues as the window multiply
+      for (; sub < w; ++sub, ++st) {
+        __builtin_amdgcn_wave_barrier();
+        lds_put<KD, G>(stream, acc, g);
+        __builtin_amdgcn_wave_barrier();
+        if constexpr (QS) M.sqr_s(acc, acc, stream);
+        else M.sqr(acc, acc, stream);
+      }
+    }
     if (st == 0) {
       src = C + 2 * KD;
     } else if (st < n_build) {
