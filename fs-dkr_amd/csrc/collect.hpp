@@ -461,7 +461,8 @@ inline bool group_by_exponent(ModexpJob& J, uint32_t per_wave, uint32_t pad_row)
   G.exp_ptr.reserve(cnt + cnt / 8);
   auto put = [&](uint32_t k, uint32_t row) {
     G.add(J.base_ptr[k], J.base_len[k], J.exp_ptr[k], J.exp_len[k], J.ebits[k], J.mod_idx[k]);
-    G.out_idx.push_back(row);
+    if (G.out_idx.size() == G.size()) G.out_idx.back() = row;   // add() extended a non-empty out_idx
+    else G.out_idx.push_back(row);
   };
   for (size_t s = 0; s < cnt;) {
     size_t e = s;

@@ -143,6 +143,9 @@ struct ModexpJob {
     mod_idx.push_back(m);
     ebits.push_back(eb);
     if (eb > exp_bits) exp_bits = eb;
+    // a job that carries output rows (group_by_exponent, append) keeps one per
+    // instance: the added instance writes the next row
+    if (!out_idx.empty()) out_idx.push_back((uint32_t)(size() - 1));
   }
   // append another job's instances (same modulus width): one merged launch
   void append(const ModexpJob& o) {

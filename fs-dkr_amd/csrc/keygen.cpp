@@ -227,7 +227,9 @@ extern "C" int fsdkr_sample_primes(fsdkr_ctx* ctx, uint32_t bits, uint32_t count
     // the walk stays below 2^bits (a `bits`-bit prime): start + 2k < 2^bits
     uint32_t wspan = span;
     const hbn::Limbs room = hbn::sub(hbn::shl(hbn::Limbs{1}, bits), w.start);   // > 0: start < 2^bits
-    if (hbn::bitlen(room) <= 32) wspan = std::min<uint32_t>(span, (room.empty() ? 0u : room[0] + 1u) / 2u);
+    // (in 64 bits: room = 0xFFFFFFFF is odd and reachable, room + 1 must not wrap)
+    if (hbn::bitlen(room) <= 32)
+      wspan = (uint32_t)std::min<uint64_t>(span, (room.empty() ? 0ull : (uint64_t)room[0] + 1ull) / 2ull);
     w.offs = sieve(w.start, wspan);
     return FSDKR_OK;
   };

@@ -235,6 +235,13 @@ __global__ __launch_bounds__(BLOCK) void modexp_kernel(const ModexpArgs a) {
     }
   }
   if constexpr (QS) {   // exit: acc * 1 / R modulo N itself (acc = x R mod N' is x R mod N)
+    // one window (an exponent below 2^w, e.g. 0 or 1): the loop above ends with
+    // the table (st < n_steps - 1 = n_build), so the ladder start T[d0] is loaded here
+    if (n_steps - 1 == n_build) {
+      const uint32_t d0 = digit(0);
+#pragma unroll
+      for (int j = 0; j < L; ++j) acc[j] = T[(size_t)d0 * KD + g * L + j];
+    }
 #pragma unroll
     for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
     M.ninv = C0[3 * KD];

@@ -403,11 +403,9 @@ def _speculative_launch(ctx, jobs):
         decrypt = job[4] if len(job) > 4 else True
         try:
             plan = _recovery_plan(msgs, lk, n_new)
-            if not decrypt:
-                todo.append(k)
-                cj.append(dict(nl=64, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=[0] *
-                               (plan["t_vss"] + 1), p=1, q=1, points=plan["pts"][lo:hi], flags=RECOVER_NO_DECRYPT))
-                continue
+            # the key's width and shape are checked on EVERY rank of a sharded call
+            # (before the decrypt / no-decrypt split), so a key the decrypting rank
+            # refuses makes every rank raise the same panic (fsdkr/shard.py)
             nl = _dk_limbs(lk.paillier_dk)
             if nl is None:
                 raise FsDkrPanic("share recovery: decryption key wider than 6144 bits")
@@ -415,7 +413,12 @@ def _speculative_launch(ctx, jobs):
             # mulm mod NN), so a ciphertext c + k N^2 recovers like c: reduce here,
             # the C ABI takes ciphertexts below 2^(64 nl) (fsdkr.h)
             nn_ = (lk.paillier_dk.p * lk.paillier_dk.q) ** 2
-            cts = [c % nn_ if c >= nn_ else c for c in plan["cts"]]
+            cts = [c % nn_ if nn_ and c >= nn_ else c for c in plan["cts"]]   # p or q = 0: the GPU reports it
+            if not decrypt:
+                todo.append(k)
+                cj.append(dict(nl=64, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=[0] *
+                               (plan["t_vss"] + 1), p=1, q=1, points=plan["pts"][lo:hi], flags=RECOVER_NO_DECRYPT))
+                continue
         except (FsDkrPanic, IndexError, AttributeError, TypeError) as e:
             out[k] = e if isinstance(e, FsDkrPanic) else FsDkrPanic(f"share recovery: {e!r}")
             continue

@@ -58,13 +58,18 @@ def _bytes_pt(b):
 
 def encode_recovery(spec, n, rows, decrypt):
     """This rank's part of the share recovery as bytes of the exchange region:
-    its pk_vec rows, and (the decrypting rank) status, share and y.  A panic the
-    plan raised is not encoded: every rank raises the same one from the same inputs."""
+    its pk_vec rows, and (the decrypting rank) status, share and y.  Status: 1 ok,
+    2 ok but li_vec out of bounds, 3 Paillier::decrypt panic, 4 another panic of
+    the decrypting rank (the plan's and the key checks run on every rank from the
+    same inputs, refresh._speculative_launch, so every rank normally raises it
+    itself; 4 makes the ranks agree whatever happens), 0 never written."""
     from .refresh import _DecryptPanic
     out = np.zeros(recovery_len(n), np.uint8)
     if spec is None or isinstance(spec, Exception):
         if decrypt and isinstance(spec, _DecryptPanic):   # Paillier::decrypt on a degenerate key
             out[0] = 3
+        elif decrypt:   # any other panic (or no result) of the decrypting rank: every rank raises
+            out[0] = 4
         return out
     share, y, pk, t_ok = spec
     lo, hi = rows
@@ -78,13 +83,19 @@ def encode_recovery(spec, n, rows, decrypt):
 
 
 def decode_recovery(region, local_spec, n):
-    """The merged recovery (the tuple refresh._conclude takes, or the panic)."""
+    """The merged recovery (the tuple refresh._conclude takes, or the panic).
+    A status other than 1 / 2 / 3 from the decrypting rank is a panic on every
+    rank: a share 0 applied by some ranks while the decrypting rank panics would
+    leave the ranks' LocalKeys diverged."""
     from .refresh import _DecryptPanic
     if isinstance(local_spec, Exception) and not isinstance(local_spec, _DecryptPanic):
         return local_spec
     st = int(region[0])
     if st == 3:
         return _DecryptPanic("share recovery: Paillier::decrypt (degenerate decryption key)")
+    if st not in (1, 2):   # 0: the decrypting rank wrote nothing; 4: it hit a panic this rank did not
+        from .refresh import FsDkrPanic
+        return FsDkrPanic(f"share recovery: no result from the decrypting rank (status {st})")
     share = int.from_bytes(bytes(region[1:33]), "little")
     y = _bytes_pt(region[33:97])
     pk = [_bytes_pt(region[97 + 64 * i:97 + 64 * (i + 1)]) for i in range(n)]

@@ -80,6 +80,30 @@ def test_modexp_every_group_size(gpu_ctx, limbs, group):
     assert not bad, f"G={group}: {len(bad)} mismatches, first at {bad[0]}"
 
 
+@pytest.mark.parametrize("limbs,group", [(64, 8), (128, 8), (128, 16), (128, 32), (192, 8)])
+@pytest.mark.parametrize("kind", ["zero", "zero_one"])
+def test_modexp_one_window_quotient_scaled(gpu_ctx, limbs, group, kind):
+    """The quotient-scaled group shapes (modexp_kernel QS, 8-32 lanes) on launches
+    whose exponents all fit one window (all 0, or all 0/1: w = 1, nwin = 1): the
+    ladder start T[d0] is loaded after the table build (it used to return the last
+    table row, base^(2^w - 1), instead of base^e)."""
+    rnd = random.Random(77 * limbs + group + len(kind))
+    bits = 32 * limbs
+    mods = [_odd(rnd, bits) for _ in range(3)] + [(1 << bits) - 1]
+    count = 96
+    idx = [rnd.randrange(len(mods)) for _ in range(count)]
+    bases = [rnd.getrandbits(bits) for _ in range(count)]
+    exps = [0] * count if kind == "zero" else [rnd.getrandbits(1) for _ in range(count)]
+    gpu_ctx.set_modexp_group(group)
+    try:
+        got = gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs)
+    finally:
+        gpu_ctx.set_modexp_group(0)
+    want = [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
+    bad = [k for k in range(count) if got[k] != want[k]]
+    assert not bad, f"G={group}: {len(bad)} mismatches, first at {bad[0]}"
+
+
 @pytest.mark.parametrize("limbs", [32, 64, 96, 128])
 def test_modexp_regular_access_equals_plain(gpu_ctx, limbs):
     """fsdkr_modexp_batch_ct (secret exponents: table scans, uniform window count)

@@ -56,6 +56,16 @@ def _summary(k):
     return (k.x_i, k.y, list(k.pk_vec), [e.n for e in k.paillier_key_vec])
 
 
+class _WideDk:
+    """a decryption key wider than the recovery's 6144-bit limit"""
+    p = (1 << 3100) + 15
+    q = (1 << 3100) + 27
+
+
+class _NoDk:
+    """a decryption key without its primes (AttributeError in the recovery plan)"""
+
+
 def _worker(rank, world, port, name, tamper, q):
     sys.path[:0] = [REPO, os.path.join(REPO, "fs-dkr_amd"), HERE]
     import torch.distributed as dist
@@ -63,6 +73,8 @@ def _worker(rank, world, port, name, tamper, q):
     from oracle_device import OracleDevice
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     msgs, joins, key, dk, kb = _scenario(name, tamper)
+    if tamper in ("dk_wide", "dk_noattr"):   # the local key's decryption key, not the new one
+        key.paillier_dk = _WideDk() if tamper == "dk_wide" else _NoDk()
     k = key.clone()
     dev = OracleDevice(msgs, joins, k, world, rank)
     out = _outcome(lambda: shard.collect(dist, msgs, k, dk, joins, dev, key_bits=kb))
@@ -96,3 +108,26 @@ def test_sharded_collect_equals_single_process(name, tamper):
         assert summ == _summary(ko), rank
     if tamper is None:
         assert want is None
+
+
+@pytest.mark.parametrize("tamper", ["dk_wide", "dk_noattr"])
+def test_sharded_recovery_panic_agrees_on_every_rank(tamper):
+    """A decryption key the share recovery refuses (wider than 6144 bits, or
+    without its primes) is checked on every rank, not only on the decrypting one:
+    every rank raises the same panic and leaves the same LocalKey (the
+    non-decrypting ranks used to apply share 0 while rank 0 panicked)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    name = "transcript_t2_n5_kb1024.json.gz"
+    ps = [ctx.Process(target=_worker, args=(r, world, port, name, tamper, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    outs = {out[0] if out else None for _, out, _ in res}
+    assert outs == {"panic"}, res
+    assert res[0][2] == res[1][2]
