@@ -309,13 +309,11 @@ def _phases_once(ctx, msgs, lk, joins, key_bits):
     prestarted chains, prepare, pipeline launch, share-recovery launch (its host
     pre-pass overlaps the pipeline), finish wait, recovery finish, first error)."""
     from fsdkr.batch import CollectBatch
-    from fsdkr.refresh import _speculative_finish, _speculative_launch
+    from fsdkr.refresh import _speculative_finish, _speculative_launch, prestart
     t0 = time.perf_counter()
     b = CollectBatch(msgs, lk, joins, 256, key_bits, staged=True)
     ts = time.perf_counter()
-    ctx.collect_prestart(b)
-    if b.stage1b():
-        ctx.collect_prestart(b)
+    prestart(ctx, b)
     tp = time.perf_counter()
     b.complete()
     t1 = time.perf_counter()

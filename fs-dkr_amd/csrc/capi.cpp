@@ -71,6 +71,21 @@ uint8_t* Ctx::host_arena(size_t bytes) {
   return pinned;
 }
 
+uint8_t* Ctx::host_buf(const char* name, size_t bytes) {
+  DevBuf& b = hbufs[name];
+  if (b.bytes >= bytes && b.ptr) return (uint8_t*)b.ptr;
+  if (b.ptr) (void)hipHostFree(b.ptr);
+  b.ptr = nullptr;
+  b.bytes = 0;
+  const size_t want = bytes + bytes / 4 + (1u << 20);
+  if (hipHostMalloc(&b.ptr, want, hipHostMallocDefault) != hipSuccess) {
+    b.ptr = nullptr;
+    return nullptr;
+  }
+  b.bytes = want;
+  return (uint8_t*)b.ptr;
+}
+
 static hipStream_t make_stream(const Ctx* c, int masked);
 
 hipStream_t Ctx::aux_stream() {
@@ -497,6 +512,8 @@ void fsdkr_ctx_destroy(fsdkr_ctx* ctx) {
     if (sd) (void)hipStreamDestroy(sd);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->pinned) (void)hipHostFree(c->pinned);
+  for (auto& kv : c->hbufs)
+    if (kv.second.ptr) (void)hipHostFree(kv.second.ptr);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   fsdkr::free_collect_plan(c);
   fsdkr::free_ga_pre(c);
@@ -512,6 +529,11 @@ int Ctx::span_begin(hipStream_t st) {
   span_armed = true;
   span_ms = -1.0f;
   return hip_check(hipEventRecord(span_beg, st), "span event record");
+}
+
+uint32_t fsdkr_collect_reuse_mask(const fsdkr_ctx* ctx) {
+  const Ctx* c = reinterpret_cast<const Ctx*>(ctx);
+  return c ? c->reuse_mask : 0u;
 }
 
 double fsdkr_collect_last_span_ms(const fsdkr_ctx* ctx) {

@@ -140,6 +140,21 @@ struct HostSha {
   }
 };
 
+// PDL challenge e = H(G, Q, c, z, u1, u2, u3) of pair lp of batch b as 8 little-endian
+// limbs (zk_pdl_with_slack.rs:114-122; every value as curv's to_bytes)
+inline bool pdl_challenge(HostSha& sha, const fsdkr_collect_batch* b, size_t lp, uint32_t* e8) {
+  const uint32_t w = b->nl;
+  sha.buf.clear();
+  sha.buf.insert(sha.buf.end(), G_COMPRESSED, G_COMPRESSED + 33);
+  put_point(sha.buf, b->commit + lp * 16);
+  put_bigint(sha.buf, b->enc + lp * 2 * w, 2 * w);
+  put_bigint(sha.buf, b->pdl_z + lp * w, w);
+  put_point(sha.buf, b->pdl_u1 + lp * 16);
+  put_bigint(sha.buf, b->pdl_u2 + lp * 2 * w, 2 * w);
+  put_bigint(sha.buf, b->pdl_u3 + lp * w, w);
+  return sha.digest(e8);
+}
+
 // f(begin, end) over [0, n) on up to host_threads() threads (inline when small)
 template <class F>
 inline void parallel_for(size_t n, size_t grain, F&& f) {
@@ -157,6 +172,17 @@ inline void parallel_for(size_t n, size_t grain, F&& f) {
     const Part& x = *static_cast<const Part*>(a);
     (*x.f)(x.n * c / x.chunks, x.n * (c + 1) / x.chunks);
   }, &part);
+}
+
+// a[0, words) == b[0, words), compared in parallel chunks
+inline bool words_equal(const uint32_t* a, const uint32_t* b, size_t words) {
+  if (words < (1u << 16)) return memcmp(a, b, words * 4) == 0;
+  std::atomic<bool> eq{true};
+  parallel_for((words + 65535) / 65536, 1, [&](size_t c0, size_t c1) {
+    const size_t lo = c0 * 65536, hi = std::min(words, c1 * 65536);
+    if (eq.load(std::memory_order_relaxed) && memcmp(a + lo, b + lo, (hi - lo) * 4) != 0) eq = false;
+  });
+  return eq;
 }
 
 // FSDKR_PREP_PROFILE=1: host pre-pass phase times on stderr (diagnostics)
@@ -299,6 +325,12 @@ struct CollectPlan {
   // equalities read them once tz_done has fired
   bool tz_hit = false;
   hipEvent_t tz_done = nullptr;
+  // the challenge jobs (J2, J5, their inverses, pdl_u1, Feldman) computed by the
+  // prestart (ch_hit): the pipeline waits for ch_ev before its equalities
+  bool ch_hit = false;
+  hipEvent_t ch_ev[3] = {};
+  // device words finish reads back (the plan's output region, or the prestart's)
+  const void *r_unn = nullptr, *r_uzA = nullptr, *r_uzp = nullptr, *r_pdlv = nullptr, *r_fel = nullptr;
   FbJob fb;
   size_t d_FB = 0;
   uint32_t* fb_table = nullptr;
@@ -334,6 +366,7 @@ struct GaPre {
   uint32_t Mt = 0, fb_w = 0, bits_h1 = 0, bits_h2 = 0, bits_z = 0, fb_entries = 0;
   uint32_t* fb_table = nullptr;
   hipEvent_t fb_done = nullptr;     // every table built
+  hipEvent_t fb_setup = nullptr;    // the table chains' moduli constants ready (fb_cons)
   // Lim-Lee comb tables of the base classes (FbJob::plan_comb), built on the
   // chains' stream after them: prepare's and prestart_rp's combs take them
   std::vector<CombPre> comb_pre;
@@ -357,6 +390,25 @@ struct GaPre {
   const uint32_t* tz_z = nullptr;        // the device copy of the Z rows [Mt*M][tz_zl]
   uint32_t tz_zl = 0;
   hipEvent_t tz_done = nullptr;
+  // device rows the later prestart jobs read: N_i^2 (GA's image, n x nn) and N~_i (the
+  // table chains' moduli, n x nl)
+  const uint32_t* nn_rows = nullptr;
+  const uint32_t* nt_rows = nullptr;
+  // the challenge jobs (prestart_chal, once stage 1c packed their fields): PDL challenges
+  // (host), J2 = c^e_pdl | c^e_A mod N_i^2, J5 = z^e_pdl | zA^e_A mod N~_i, the inverses
+  // and unit flags, pdl_u1, Feldman.  ch_host keeps the rows they read (prepare's match).
+  bool ch_valid = false;
+  uint32_t ch_P = 0, ch_V = 0, ch_el = 0, ch_s1l = 0, ch_n_inv_nn = 0;
+  const uint8_t* ch_host = nullptr;
+  struct ChRows {   // offsets of the compared fields in ch_host (rows at the session widths)
+    size_t enc, pz, pu1, pu2, pu3, Q, az, ae, ps1, as1, vss, vlen, rn, rt;
+  } ch_off{};
+  std::vector<uint32_t> ch_epdl;          // [P][8]
+  std::vector<uint32_t> ch_cpdl_extra;    // pairs whose c unit test is an extra nn inverse
+  uint32_t *ch_J2 = nullptr, *ch_J5 = nullptr, *ch_invc = nullptr, *ch_invz = nullptr;
+  uint32_t *ch_unn = nullptr, *ch_uzA = nullptr, *ch_uzp = nullptr;
+  uint8_t *ch_pdlv = nullptr, *ch_fel = nullptr;
+  hipEvent_t ch_ev[3] = {};
 };
 
 // width-independent 64-bit digest of `rows` rows of `w` words (trailing zero
@@ -487,6 +539,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
 int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
+bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_prepare.cpp
 int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_launch.cpp

@@ -132,7 +132,7 @@ int collect_launch_impl(Ctx* c) {
     }
     if ((rc = join_later(ss))) return rc;
   }
-  {  // Feldman share checks (inputs only; one Horner chain per pair)
+  if (!pl.ch_hit) {  // Feldman share checks (inputs only; one Horner chain per pair; else prestarted)
     hipStream_t ss = c->side_stream(6);
     // one Horner chain of t+1 small-scalar steps per pair on one thread: ~2 % of
     // GA's work at n = 256, but a long serial chain; at the default priority it
@@ -172,18 +172,20 @@ int collect_launch_impl(Ctx* c) {
   }
   hipEvent_t ready;
   if ((rc = fork(st, &ready))) return rc;
-  {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses
+  {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses (prestarted on a chal hit)
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
     if ((rc = launch_group(2, ss, 0, j2_group, cons_nn))) return rc;
-    InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
-                  PX(pl.x_unn), nullptr, pl.n_inv_nn};
-    c->mark("inverse", true, ss);
-    rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
-    c->mark("inverse", false, ss);
+    if (!pl.ch_hit) {
+      InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
+                    PX(pl.x_unn), nullptr, pl.n_inv_nn};
+      c->mark("inverse", true, ss);
+      rc = c->hip_check(launch_inverse(nn, a, ss), "inverse nn");
+      c->mark("inverse", false, ss);
+    }
     if (rc || (rc = join_later(ss))) return rc;
   }
-  {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
+  if (!pl.ch_hit) {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
     hipStream_t ss = c->side_stream(5);
     (void)hipStreamWaitEvent(ss, ready, 0);
     PdlU1Args u{PI(pl.o_ps1), PI(pl.o_epdl), PI(pl.o_Q), PI(pl.o_pu1), pl.s1l, (uint8_t*)(out_base + pl.x_pdlv), P};
@@ -195,7 +197,7 @@ int collect_launch_impl(Ctx* c) {
   }
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
-  {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses
+  if (!pl.ch_hit) {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses (else prestarted)
     hipStream_t js = st;
     if ((rc = launch_group(3, js, prio[3], j5_group, cons_nl))) return rc;
     InverseArgs b1{(const uint64_t*)(dev + pl.d_iynl), (const uint64_t*)(dev + pl.d_imnl), PX(pl.x_invz),
@@ -214,6 +216,8 @@ int collect_launch_impl(Ctx* c) {
   }
   if (pl.ga_hit) (void)hipStreamWaitEvent(st, pl.ga_done, 0);   // the prestarted s^N rows
   if (pl.tz_hit) (void)hipStreamWaitEvent(st, pl.tz_done, 0);   // the prestarted ring-Pedersen T^Z rows
+  if (pl.ch_hit)   // the prestarted challenge jobs (J2, J5 -> inverses; pdl_u1 -> Feldman)
+    for (hipEvent_t ev : pl.ch_ev) (void)hipStreamWaitEvent(st, ev, 0);
   // equality checks and exact products
   {
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqnn), PI(pl.d_eqnnm), cons_nn, PX(pl.x_pbits), DI(pl.o_one),
@@ -278,16 +282,17 @@ int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
       eqck(pl.n_eq_ck), p2(pl.n_p2);
   std::vector<uint8_t> fel(P), pdlv(P), rng(P);
   int rc;
-  auto D2H = [&](void* dst, size_t off, size_t bytes) {
+  auto D2Hp = [&](void* dst, const void* src, size_t bytes) {
     if (!bytes) return (int)FSDKR_OK;
-    return c->hip_check(hipMemcpyAsync(dst, out_base + off, bytes, hipMemcpyDeviceToHost, st), "D2H verdicts");
+    return c->hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st), "D2H verdicts");
   };
+  auto D2H = [&](void* dst, size_t off, size_t bytes) { return D2Hp(dst, out_base + off, bytes); };
   if ((rc = D2H(ppanic.data(), pl.x_ppanic, Mt * 4)) ||
-      (rc = D2H(unn.data(), pl.x_unn, unn.size() * 4)) || (rc = D2H(uzA.data(), pl.x_uzA, P * 4)) ||
-      (rc = D2H(uzp.data(), pl.x_uzp, P * 4)) || (rc = D2H(eq2.data(), pl.x_eq2, P * 4)) ||
+      (rc = D2Hp(unn.data(), pl.r_unn, unn.size() * 4)) || (rc = D2Hp(uzA.data(), pl.r_uzA, P * 4)) ||
+      (rc = D2Hp(uzp.data(), pl.r_uzp, P * 4)) || (rc = D2H(eq2.data(), pl.x_eq2, P * 4)) ||
       (rc = D2H(eq3.data(), pl.x_eq3, eq3.size() * 4)) || (rc = D2H(eqck.data(), pl.x_eqck, eqck.size() * 4)) ||
-      (rc = D2H(p2.data(), pl.x_p2, p2.size() * 4)) || (rc = D2H(fel.data(), pl.x_fel, P)) ||
-      (rc = D2H(pdlv.data(), pl.x_pdlv, P)) || (rc = D2H(rng.data(), pl.x_rng, P)))
+      (rc = D2H(p2.data(), pl.x_p2, p2.size() * 4)) || (rc = D2Hp(fel.data(), pl.r_fel, P)) ||
+      (rc = D2Hp(pdlv.data(), pl.r_pdlv, P)) || (rc = D2H(rng.data(), pl.x_rng, P)))
     return rc;
   if ((rc = c->sync())) return rc;
   if (c->span_armed) {

@@ -12,6 +12,7 @@ namespace fsdkr {
 // ------------------------------------------------------------------------------
 int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
   free_collect_plan(c);   // a failed prepare leaves no plan behind
+  c->reuse_mask = 0;
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prepare: no batch");
     return FSDKR_E_ARG;
@@ -104,6 +105,13 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     pl.pre_cons_wide = gpre->wide;
     gpre->valid = false;   // consumed (the buffer lives until the next prestart)
   }
+  // prestarted challenge jobs of this batch (stage 1c): J2, J5, their inverses,
+  // pdl_u1 and Feldman are not launched again, the PDL challenges not hashed again
+  pl.ch_hit = chal_pre_matches(c, bs, count) && gpre->ch_P == P;
+  if (pl.ch_hit) {
+    for (int k = 0; k < 3; ++k) pl.ch_ev[k] = gpre->ch_ev[k];
+    gpre->ch_valid = false;   // consumed
+  }
   clk.lap("shapes");
 
   // ---------------- host pre-pass (O(n) + O(P) scans, no big exponentiations; threaded)
@@ -130,7 +138,9 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   // PDL challenges e = H(G, Q, c, z, u1, u2, u3) (zk_pdl_with_slack.rs:114-122) on the
   // host threads of this scan: J2 (c^e), J5 (z^e) and pdl_u1 can start with the pipeline
   std::vector<uint32_t>& EPDL = pl.e_pdl;
-  EPDL.assign((size_t)P * 8, 0u);
+  if (pl.ch_hit) EPDL = gpre->ch_epdl;
+  else EPDL.assign((size_t)P * 8, 0u);
+  const bool hash = !pl.ch_hit;
   std::atomic<bool> sha_fail{false};
   parallel_for(P, 256, [&](size_t b0, size_t b1) {
     Maxes mx;
@@ -139,16 +149,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       const Sess& x = pl.ss[sess_of_pair[p]];
       const fsdkr_collect_batch* b = x.b;
       const size_t lp = p - x.pbase;
-      const uint32_t w = b->nl;
-      sha.buf.clear();
-      sha.buf.insert(sha.buf.end(), G_COMPRESSED, G_COMPRESSED + 33);
-      put_point(sha.buf, b->commit + lp * 16);
-      put_bigint(sha.buf, b->enc + lp * 2 * w, 2 * w);
-      put_bigint(sha.buf, b->pdl_z + lp * w, w);
-      put_point(sha.buf, b->pdl_u1 + lp * 16);
-      put_bigint(sha.buf, b->pdl_u2 + lp * 2 * w, 2 * w);
-      put_bigint(sha.buf, b->pdl_u3 + lp * w, w);
-      if (!sha.digest(EPDL.data() + p * 8)) sha_fail = true;
+      if (hash && !pdl_challenge(sha, b, lp, EPDL.data() + p * 8)) sha_fail = true;
       const uint32_t* Np = b->recv_n + (size_t)(lp % x.n) * b->nl;
       const uint32_t* s1 = b->pdl_s1 + lp * b->s1l;
       // s1 < N -> (N+1)^s1 mod N^2 = 1 + s1*N  (binomial, bit-identical)
@@ -593,20 +594,24 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
         J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
       const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
-      if (which == 0) J2.add(cp, nn, DI(o_epdl + (size_t)p * 32), 8, 256, r);
-      else J2.add(cp, nn, DI(o_ae + (size_t)p * el * 4), el, mx.ae, r);
+      if (pl.ch_hit) {   // (prestarted)
+      } else if (which == 0) {
+        J2.add(cp, nn, DI(o_epdl + (size_t)p * 32), 8, 256, r);
+      } else {
+        J2.add(cp, nn, DI(o_ae + (size_t)p * el * 4), el, mx.ae, r);
+      }
       // fixed bases (FB): h1^s1 -> J3 slot | h2^s3 (s2 for Alice) -> J4 slot;  J5: z^e
       const size_t slot = (size_t)which * P + p;
       if (which == 0) {
         FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
         fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
-        J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
+        if (!pl.ch_hit) J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
         FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
         fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
                             DX(x_J4 + slot * nl * 4)});
-        J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
+        if (!pl.ch_hit) J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
       }
     }
   for (uint32_t p = 0; p < P; ++p)
@@ -746,16 +751,17 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   cpdl_extra.clear();
   inv_y_nn.reserve(2 * (size_t)P);
   inv_m_nn.reserve(2 * (size_t)P);
-  for (uint32_t p = 0; p < P; ++p) {
+  for (uint32_t p = 0; p < P && !pl.ch_hit; ++p) {
     inv_y_nn.push_back(DX(x_J2 + ((size_t)P + p) * nn * 4));
     inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
   }
-  for (uint32_t p = 0; p < P; ++p)
+  for (uint32_t p = 0; p < P && !pl.ch_hit; ++p)
     if (ae_bits[p] == 0 || !alice_pre[p]) {  // c^eA does not witness c's unit-ness
       inv_y_nn.push_back(DX(x_J2 + (size_t)p * nn * 4));
       inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
       cpdl_extra.push_back(p);
     }
+  if (pl.ch_hit) cpdl_extra = gpre->ch_cpdl_extra;
   for (uint32_t p = 0; p < P; ++p) {  // zA^eA (value) then z^e_pdl (unit test)
     const uint64_t mt = DI(o_rt + (size_t)recv_of_pair[p] * nl * 4);
     inv_y_nl[p] = DX(x_J5 + ((size_t)P + p) * nl * 4);
@@ -765,6 +771,13 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   }
   const size_t d_iynn = put(inv_y_nn.data(), inv_y_nn.size() * 8), d_imnn = put(inv_m_nn.data(), inv_m_nn.size() * 8);
   const size_t d_iynl = put(inv_y_nl.data(), inv_y_nl.size() * 8), d_imnl = put(inv_m_nl.data(), inv_m_nl.size() * 8);
+  // the rows of J2 / J5 and the inverses: the prestart's (ch_hit) or this plan's outputs
+  auto J2_row = [&](size_t k) {
+    return pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_J2 + k * nn) : DX(x_J2 + k * nn * 4);
+  };
+  auto J5_row = [&](size_t k) {
+    return pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_J5 + k * nl) : DX(x_J5 + k * nl * 4);
+  };
   // eq_check descriptors
   clk.lap("desc fb/binom/inv");
   std::vector<EqOperand> eq_nn(P), eq_nl, eq_ck;
@@ -774,7 +787,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     e.a = pdl_small[p] ? DX(x_Bpdl + (size_t)p * nn * 4) : DX(x_J9 + (size_t)j9_index[p] * nn * 4);
     e.b = pl.ga_hit ? J1_at(p) : DX(x_J1 + (size_t)p * nn * 4);
     e.c = DI(o_pu2 + (size_t)p * nn * 4);
-    e.d = DX(x_J2 + (size_t)p * nn * 4);
+    e.d = J2_row(p);
     e.a_len = e.b_len = e.c_len = e.d_len = nn;
     e.sel = 0xFFFFFFFFu;
     e.flags = 1;
@@ -787,7 +800,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     e.a = DX(x_J3 + (size_t)p * nl * 4);
     e.b = DX(x_J4 + (size_t)p * nl * 4);
     e.c = DI(o_pu3 + (size_t)p * nl * 4);
-    e.d = DX(x_J5 + (size_t)p * nl * 4);
+    e.d = J5_row(p);
     e.a_len = e.b_len = e.c_len = e.d_len = nl;
     e.sel = 0xFFFFFFFFu;
     e.flags = 1;
@@ -846,10 +859,11 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   std::vector<Prod3Operand> p3_nn(P), p3_nl(P);
   for (uint32_t p = 0; p < P; ++p) {
     p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), pl.ga_hit ? J1_at((size_t)P + p) : DX(x_J1 + ((size_t)P + p) * nn * 4),
-                DX(x_invc + (size_t)p * nn * 4),
+                pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invc + (size_t)p * nn) : DX(x_invc + (size_t)p * nn * 4),
                 nn, nn, nn, 0};
     p3_nl[p] = {DX(x_J3 + ((size_t)P + p) * nl * 4), DX(x_J4 + ((size_t)P + p) * nl * 4),
-                DX(x_invz + (size_t)p * nl * 4), nl, nl, nl, 0};
+                pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invz + (size_t)p * nl) : DX(x_invz + (size_t)p * nl * 4),
+                nl, nl, nl, 0};
   }
   const size_t d_p3nn = put(p3_nn.data(), p3_nn.size() * sizeof(Prod3Operand)),
                d_p3nl = put(p3_nl.data(), p3_nl.size() * sizeof(Prod3Operand)),
@@ -967,11 +981,18 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_eqck = d_eqck;
   pl.d_eqckm = d_eqckm; pl.d_p3nn = d_p3nn; pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc;
   pl.d_alpre = d_alpre;
-  pl.n_inv_nn = (uint32_t)inv_y_nn.size();
+  pl.n_inv_nn = pl.ch_hit ? gpre->ch_n_inv_nn : (uint32_t)inv_y_nn.size();
+  pl.r_unn = pl.ch_hit ? (const void*)gpre->ch_unn : out_base + x_unn;
+  pl.r_uzA = pl.ch_hit ? (const void*)gpre->ch_uzA : out_base + x_uzA;
+  pl.r_uzp = pl.ch_hit ? (const void*)gpre->ch_uzp : out_base + x_uzp;
+  pl.r_pdlv = pl.ch_hit ? (const void*)gpre->ch_pdlv : out_base + x_pdlv;
+  pl.r_fel = pl.ch_hit ? (const void*)gpre->ch_fel : out_base + x_fel;
   pl.n_eq_nn = (uint32_t)eq_nn.size();
   pl.n_eq_nl = (uint32_t)eq_nl.size();
   pl.n_eq_ck = (uint32_t)eq_ck.size();
   for (Sess& x : pl.ss) x.b = nullptr;   // the caller's buffers are not used after prepare
+  c->reuse_mask = (pl.ga_hit ? 1u : 0u) | (pl.fb_hit ? 2u : 0u) | (pl.ck_hit ? 4u : 0u) | (pl.tz_hit ? 8u : 0u) |
+                  (pl.ch_hit ? 16u : 0u);
   c->plan = plan.release();
   return FSDKR_OK;
 }

@@ -170,10 +170,14 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
   uint32_t* cons = nullptr;
   if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl")))
     return rc;
+  if (!g.fb_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_setup, hipEventDisableTiming), "event")))
+    return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.fb_setup, ts), "event record"))) return rc;   // N~_i constants ready
   if (!g.fb_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_done, hipEventDisableTiming), "event")))
     return rc;
   g.fb_table = reinterpret_cast<uint32_t*>(dev + o_tab);
   g.fb_cons = cons;
+  g.nt_rows = reinterpret_cast<const uint32_t*>(dev + o_mod);
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
   FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
@@ -296,6 +300,336 @@ static int prestart_ck(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, Ga
 }
 
 
+// The challenge jobs of a batch whose stage 1c packed their fields: everything the
+// PDL / Alice / Feldman checks compute without an exponent table.
+//  - PDL challenges e = H(G, Q, c, z, u1, u2, u3) (zk_pdl_with_slack.rs:114-122) on the
+//    host threads;
+//  - J2 = c^e_pdl | c^e_A mod N_i^2 -> inverse_coop of every c^e_A (Alice's u needs the
+//    value, range_proofs.rs:140-148) and of c^e_pdl where e_A does not witness c's
+//    unit-ness (the PDL panic, zk_pdl_with_slack.rs:180);
+//  - J5 = z^e_pdl | zA^e_A mod N~_i -> the inverses of zA^e_A (Alice's w, :129-137) and
+//    the unit test of z^e_pdl;
+//  - pdl_u1 (G s1 + Q (q - e) on secp256k1), then Feldman (refresh_message.rs:147-191);
+// on their own streams beside GA, ~10 ms before prepare would start them.  The image
+// (and the rows that only the challenges read) stays in a pinned host buffer:
+// prepare compares the batch with it and takes these results on a match (ch_hit).
+static int prestart_chal(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, GaPre& g) {
+  if (g.sess.size() != count || !g.fb_valid || !g.fb_cons || !g.fb_setup || !g.nn_rows || !g.nt_rows || !g.cons)
+    return FSDKR_OK;
+  const uint32_t nl = g.nl, nn = 2 * nl;
+  uint32_t el = 0, s1l = 0, P = 0, V = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (b->nl != nl || !b->enc || !b->pdl_z || !b->pdl_u1 || !b->pdl_u2 || !b->pdl_u3 || !b->commit || !b->rp_z ||
+        !b->rp_e || !b->pdl_s1 || !b->rp_s1 || !b->vss || !b->el || !b->s1l || b->range_lens || b->recv_avail ||
+        (k && (b->el != el || b->s1l != s1l)))
+      return FSDKR_OK;   // prepare computes them (one width per field here)
+    el = b->el;
+    s1l = b->s1l;
+    const GaPre::Sess& x = g.sess[k];
+    if (x.nl != nl || x.pbase != P) return FSDKR_OK;
+    P += x.R * x.n;
+    for (uint32_t m = 0; m < x.R; ++m) V += ncoef_of(b, m);
+  }
+  if (!P) return FSDKR_OK;
+  std::vector<uint32_t> sess_of_pair(P);
+  for (uint32_t k = 0; k < count; ++k)
+    std::fill(sess_of_pair.begin() + g.sess[k].pbase, sess_of_pair.begin() + g.sess[k].pbase + g.sess[k].R * g.sess[k].n, k);
+  auto recv_of = [&](uint32_t p) {
+    const GaPre::Sess& x = g.sess[sess_of_pair[p]];
+    return (uint32_t)(x.rbase + (p - x.pbase) % x.n);
+  };
+  // ---- host: PDL challenges, Alice pre-checks (as prepare's pair scan)
+  g.ch_epdl.assign((size_t)P * 8, 0u);
+  std::vector<uint8_t> alice_pre(P);
+  std::vector<uint32_t> ae_bits(P);
+  std::vector<uint32_t> ae_max(host_threads() + 1, 1);
+  std::atomic<uint32_t> slot{0};
+  std::atomic<bool> sha_fail{false};
+  const hbn::Limbs& q3 = q_cubed();
+  parallel_for(P, 128, [&](size_t b0, size_t b1) {
+    HostSha sha;
+    uint32_t mx = 1;
+    for (size_t p = b0; p < b1; ++p) {
+      const GaPre::Sess& x = g.sess[sess_of_pair[p]];
+      const fsdkr_collect_batch* b = bs + sess_of_pair[p];
+      const size_t lp = p - x.pbase;
+      if (!pdl_challenge(sha, b, lp, g.ch_epdl.data() + p * 8)) sha_fail = true;
+      ae_bits[p] = hbn::bitlen(b->rp_e + lp * el, el);
+      const bool s1_ok = hbn::cmp_raw(b->rp_s1 + lp * s1l, s1l, q3.data(), q3.size()) <= 0;
+      alice_pre[p] = (s1_ok && ae_bits[p] <= 256) ? 1 : 0;
+      if (alice_pre[p]) mx = std::max(mx, ae_bits[p]);
+    }
+    ae_max[slot++ % ae_max.size()] = mx;
+  });
+  if (sha_fail) {
+    c->fail("fsdkr_collect_prestart: SHA-256 (OpenSSL EVP) failed");
+    return FSDKR_E_ARG;
+  }
+  uint32_t mx_ae = 1;
+  for (uint32_t v : ae_max) mx_ae = std::max(mx_ae, v);
+  // ---- layout: [device image | rows only the host reads] in one pinned buffer
+  auto al = Img::al;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = al(o + bytes);
+    return at;
+  };
+  GaPre::ChRows& R = g.ch_off;
+  R.enc = take((size_t)P * nn * 4);
+  R.pz = take((size_t)P * nl * 4);
+  R.az = take((size_t)P * nl * 4);
+  R.ae = take((size_t)P * el * 4);
+  const size_t o_ep = take((size_t)P * 32);
+  R.ps1 = take((size_t)P * s1l * 4);
+  R.Q = take((size_t)P * 64);
+  R.pu1 = take((size_t)P * 64);
+  R.vss = take((size_t)V * 64);
+  const size_t o_fi = take((size_t)P * sizeof(FeldmanInfo));
+  // descriptors: J2, J5 (2P each), inverse operand addresses (nn: <= 2P, nl: 2P)
+  ModexpJob J2, J5;
+  J2.k32 = nn;
+  J5.k32 = nl;
+  const size_t o_dJ2 = take((size_t)2 * P * 32), o_dJ5 = take((size_t)2 * P * 32);
+  const size_t o_iynn = take((size_t)2 * P * 8), o_imnn = take((size_t)2 * P * 8);
+  const size_t o_iynl = take((size_t)2 * P * 8), o_imnl = take((size_t)2 * P * 8);
+  const size_t dev_in = o;
+  // host-only rows of the match: u2, u3 (hashed), Alice s1 (pre-check), the receivers
+  R.pu2 = take((size_t)P * nn * 4);
+  R.pu3 = take((size_t)P * nl * 4);
+  R.as1 = take((size_t)P * s1l * 4);
+  R.vlen = take((size_t)count * 4 + (size_t)P * 4);
+  R.rn = take((size_t)g.n * nl * 4);
+  R.rt = take((size_t)g.n * nl * 4);
+  const size_t host_bytes = o;
+  // device outputs after the image
+  size_t od = dev_in;
+  auto out = [&](size_t bytes) {
+    const size_t at = od;
+    od = al(od + bytes);
+    return at;
+  };
+  const size_t x_J2 = out((size_t)2 * P * nn * 4), x_J5 = out((size_t)2 * P * nl * 4);
+  const size_t x_invc = out((size_t)2 * P * nn * 4), x_invz = out((size_t)P * nl * 4);
+  const size_t x_unn = out((size_t)2 * P * 4), x_uzA = out((size_t)P * 4), x_uzp = out((size_t)P * 4);
+  const size_t x_pdlv = out(P), x_fel = out(P);
+  uint8_t* dev = (uint8_t*)c->buf("collect_ch_pre", od);
+  uint8_t* img = c->host_buf("collect_ch_img", host_bytes);
+  if (!dev || !img) {
+    c->fail("fsdkr_collect_prestart: allocation of %zu device / %zu pinned bytes failed", od, host_bytes);
+    return FSDKR_E_OOM;
+  }
+  auto DI = [&](size_t off) { return (uint64_t)(uintptr_t)(dev + off); };
+  // ---- rows (per session, contiguous at the shared widths)
+  {
+    struct Cp {
+      uint8_t* dst;
+      const void* src;
+      size_t bytes;
+    };
+    std::vector<Cp> cps;
+    auto add = [&](size_t dst, const void* src, size_t bytes) {
+      constexpr size_t kChunk = 1u << 20;
+      for (size_t q = 0; q < bytes; q += kChunk)
+        cps.push_back(Cp{img + dst + q, (const uint8_t*)src + q, std::min(kChunk, bytes - q)});
+    };
+    size_t voff = 0;
+    for (uint32_t k = 0; k < count; ++k) {
+      const fsdkr_collect_batch* b = bs + k;
+      const GaPre::Sess& x = g.sess[k];
+      const size_t pb = x.pbase, cnt = (size_t)x.R * x.n;
+      uint32_t vk = 0;
+      for (uint32_t m = 0; m < x.R; ++m) vk += ncoef_of(b, m);
+      add(R.enc + pb * nn * 4, b->enc, cnt * nn * 4);
+      add(R.pz + pb * nl * 4, b->pdl_z, cnt * nl * 4);
+      add(R.az + pb * nl * 4, b->rp_z, cnt * nl * 4);
+      add(R.ae + pb * el * 4, b->rp_e, cnt * el * 4);
+      add(R.ps1 + pb * s1l * 4, b->pdl_s1, cnt * s1l * 4);
+      add(R.Q + pb * 64, b->commit, cnt * 64);
+      add(R.pu1 + pb * 64, b->pdl_u1, cnt * 64);
+      add(R.vss + voff * 64, b->vss, (size_t)vk * 64);
+      add(R.pu2 + pb * nn * 4, b->pdl_u2, cnt * nn * 4);
+      add(R.pu3 + pb * nl * 4, b->pdl_u3, cnt * nl * 4);
+      add(R.as1 + pb * s1l * 4, b->rp_s1, cnt * s1l * 4);
+      add(R.rn + x.rbase * nl * 4, b->recv_n, (size_t)x.n * nl * 4);
+      add(R.rt + x.rbase * nl * 4, b->recv_ntilde, (size_t)x.n * nl * 4);
+      voff += vk;
+    }
+    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
+      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].bytes);
+    });
+  }
+  // commitment counts (the match): [count] zeros for the regular shape, then per message
+  uint32_t* vlen = reinterpret_cast<uint32_t*>(img + R.vlen);
+  memset(vlen, 0, (size_t)count * 4 + (size_t)P * 4);
+  {
+    size_t q = count;
+    for (uint32_t k = 0; k < count; ++k) {
+      vlen[k] = bs[k].vss_len ? 1u : 0u;
+      for (uint32_t m = 0; m < bs[k].n_refresh; ++m) vlen[q++] = ncoef_of(bs + k, m);
+    }
+  }
+  memcpy(img + o_ep, g.ch_epdl.data(), (size_t)P * 32);
+  auto* finfo = reinterpret_cast<FeldmanInfo*>(img + o_fi);
+  for (uint32_t k = 0, voff = 0; k < count; ++k) {
+    const GaPre::Sess& x = g.sess[k];
+    for (uint32_t m = 0; m < x.R; ++m) {
+      const uint32_t nc = ncoef_of(bs + k, m);
+      for (uint32_t i = 0; i < x.n; ++i) finfo[x.pbase + (size_t)m * x.n + i] = {voff, nc, i + 1, 0};
+      voff += nc;
+    }
+  }
+  // J2 / J5 in prepare's instance order; inverse operands as prepare builds them
+  g.ch_cpdl_extra.clear();
+  auto* iynn = reinterpret_cast<uint64_t*>(img + o_iynn);
+  auto* imnn = reinterpret_cast<uint64_t*>(img + o_imnn);
+  auto* iynl = reinterpret_cast<uint64_t*>(img + o_iynl);
+  auto* imnl = reinterpret_cast<uint64_t*>(img + o_imnl);
+  for (int which = 0; which < 2; ++which)
+    for (uint32_t p = 0; p < P; ++p) {
+      const uint32_t r = recv_of(p);
+      const uint64_t cp = DI(R.enc + (size_t)p * nn * 4);
+      if (which == 0) {
+        J2.add(cp, nn, DI(o_ep + (size_t)p * 32), 8, 256, r);
+        J5.add(DI(R.pz + (size_t)p * nl * 4), nl, DI(o_ep + (size_t)p * 32), 8, 256, r);
+      } else {
+        J2.add(cp, nn, DI(R.ae + (size_t)p * el * 4), el, mx_ae, r);
+        J5.add(DI(R.az + (size_t)p * nl * 4), nl, DI(R.ae + (size_t)p * el * 4), alice_pre[p] ? el : 0, mx_ae, r);
+      }
+    }
+  uint32_t n_inv_nn = 0;
+  for (uint32_t p = 0; p < P; ++p) {   // Alice c^eA: the value and c's unit test
+    iynn[n_inv_nn] = DI(x_J2 + ((size_t)P + p) * nn * 4);
+    imnn[n_inv_nn++] = (uint64_t)(uintptr_t)(g.nn_rows + (size_t)recv_of(p) * nn);
+  }
+  for (uint32_t p = 0; p < P; ++p)
+    if (ae_bits[p] == 0 || !alice_pre[p]) {   // c^eA does not witness c's unit-ness: test c^e_pdl
+      iynn[n_inv_nn] = DI(x_J2 + (size_t)p * nn * 4);
+      imnn[n_inv_nn++] = (uint64_t)(uintptr_t)(g.nn_rows + (size_t)recv_of(p) * nn);
+      g.ch_cpdl_extra.push_back(p);
+    }
+  for (uint32_t p = 0; p < P; ++p) {   // zA^eA (value) then z^e_pdl (unit test)
+    const uint64_t mt = (uint64_t)(uintptr_t)(g.nt_rows + (size_t)recv_of(p) * nl);
+    iynl[p] = DI(x_J5 + ((size_t)P + p) * nl * 4);
+    imnl[p] = mt;
+    iynl[P + p] = DI(x_J5 + (size_t)p * nl * 4);
+    imnl[P + p] = mt;
+  }
+  {
+    std::vector<uint8_t> d2, d5;
+    J2.pack(d2);
+    J5.pack(d5);
+    memcpy(img + o_dJ2, d2.data(), d2.size());
+    memcpy(img + o_dJ5, d5.data(), d5.size());
+  }
+  // ---- upload on the J2 stream, then the three chains
+  hipStream_t s2 = c->side_stream(2), s5 = c->side_stream(5), s6 = c->side_stream(6);
+  int rc;
+  // an earlier prestart's chains that nobody consumed may still read the image on
+  // the other two streams: the upload waits for them
+  for (int k = 1; k < 3; ++k)
+    if (g.ch_ev[k]) (void)hipStreamWaitEvent(s2, g.ch_ev[k], 0);
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img, dev_in, hipMemcpyHostToDevice, s2), "prestart chal H2D")))
+    return rc;
+  for (hipEvent_t& e : g.ch_ev)
+    if (!e && (rc = c->hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event"))) return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.ch_ev[0], s2), "event record"))) return rc;
+  (void)hipStreamWaitEvent(s5, g.ch_ev[0], 0);
+  (void)hipStreamWaitEvent(s6, g.ch_ev[0], 0);
+  // J2's constants: GA's N_i^2 rows (the KD = 144 class; a 32-lane GA set up KD = 160)
+  const uint32_t* cons_nn = g.cons;
+  if (g.wide) {
+    uint32_t* cw = nullptr;
+    StreamScope scope(c, s2);
+    if ((rc = setup_moduli(c, nn, g.nn_rows, g.n, &cw, "collect_ch_nn"))) return rc;
+    cons_nn = cw;
+  }
+  (void)hipStreamWaitEvent(s2, g.ga_setup, 0);
+  (void)hipStreamWaitEvent(s5, g.fb_setup, 0);   // N~_i constants (the table prestart's setup)
+  // the lanes launch() gives them: J2 at 16 lanes (one instance per wave for <= 1024
+  // chains), J5 at 8 lanes (collect_launch.cpp)
+  const uint32_t j2_group = nn == 128 ? (J2.size() <= 1024 ? kWaveGroup : J2.size() <= 16384 ? 16 : 8) : 8;
+  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J2.size(), J2.exp_bits, dev + o_dJ2, cons_nn,
+                               reinterpret_cast<uint32_t*>(dev + x_J2), s2, "mxt_J2pre", 0, j2_group)) ||
+      (rc = launch_modexp_desc(c, nl, (uint32_t)J5.size(), J5.exp_bits, dev + o_dJ5, g.fb_cons,
+                               reinterpret_cast<uint32_t*>(dev + x_J5), s5, "mxt_J5pre", 1, 8)))
+    return rc;
+  auto U64 = [&](size_t off) { return reinterpret_cast<const uint64_t*>(dev + off); };
+  auto U32 = [&](size_t off) { return reinterpret_cast<uint32_t*>(dev + off); };
+  InverseArgs inn{U64(o_iynn), U64(o_imnn), U32(x_invc), U32(x_unn), nullptr, n_inv_nn};
+  InverseArgs inl1{U64(o_iynl), U64(o_imnl), U32(x_invz), U32(x_uzA), nullptr, P};
+  InverseArgs inl2{U64(o_iynl) + P, U64(o_imnl) + P, nullptr, U32(x_uzp), nullptr, P};
+  if ((rc = c->hip_check(launch_inverse(nn, inn, s2), "prestart inverse nn")) ||
+      (rc = c->hip_check(launch_inverse(nl, inl1, s5), "prestart inverse nl")) ||
+      (rc = c->hip_check(launch_inverse(nl, inl2, s5), "prestart inverse nl 2")))
+    return rc;
+  PdlU1Args u{U32(R.ps1), U32(o_ep), U32(R.Q), U32(R.pu1), s1l, dev + x_pdlv, P};
+  FeldmanArgs f{U32(R.vss), U32(R.Q), reinterpret_cast<const FeldmanInfo*>(dev + o_fi), dev + x_fel, P, 3};
+  if ((rc = c->hip_check(launch_pdl_u1(u, s6), "prestart pdl_u1")) ||
+      (rc = c->hip_check(launch_feldman(f, s6), "prestart feldman")))
+    return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.ch_ev[0], s2), "event record")) ||
+      (rc = c->hip_check(hipEventRecord(g.ch_ev[1], s5), "event record")) ||
+      (rc = c->hip_check(hipEventRecord(g.ch_ev[2], s6), "event record")))
+    return rc;
+  g.ch_host = img;
+  g.ch_P = P;
+  g.ch_V = V;
+  g.ch_el = el;
+  g.ch_s1l = s1l;
+  g.ch_n_inv_nn = n_inv_nn;
+  g.ch_J2 = U32(x_J2);
+  g.ch_J5 = U32(x_J5);
+  g.ch_invc = U32(x_invc);
+  g.ch_invz = U32(x_invz);
+  g.ch_unn = U32(x_unn);
+  g.ch_uzA = U32(x_uzA);
+  g.ch_uzp = U32(x_uzp);
+  g.ch_pdlv = dev + x_pdlv;
+  g.ch_fel = dev + x_fel;
+  g.ch_valid = true;
+  return FSDKR_OK;
+}
+
+// do the prestarted challenge jobs belong to these sessions (every row they read equal)?
+bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
+  const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
+  if (!g || !g->ch_valid || !g->ch_host || g->sess.size() != count) return false;
+  const uint32_t nl = g->nl, nn = 2 * nl, el = g->ch_el, s1l = g->ch_s1l;
+  const GaPre::ChRows& R = g->ch_off;
+  auto at = [&](size_t off) { return reinterpret_cast<const uint32_t*>(g->ch_host + off); };
+  const uint32_t* vlen = at(R.vlen);
+  size_t voff = 0, q = count;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const GaPre::Sess& x = g->sess[k];
+    const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
+    if (b->nl != nl || b->el != el || b->s1l != s1l || x.n != ns || x.R != b->n_refresh || b->range_lens ||
+        b->recv_avail || !b->enc || !b->pdl_z || !b->pdl_u1 || !b->pdl_u2 || !b->pdl_u3 || !b->commit || !b->rp_z ||
+        !b->rp_e || !b->pdl_s1 || !b->rp_s1 || !b->vss || vlen[k] != (b->vss_len ? 1u : 0u))
+      return false;
+    uint32_t vk = 0;
+    for (uint32_t m = 0; m < x.R; ++m, ++q) {
+      if (vlen[q] != ncoef_of(b, m)) return false;
+      vk += vlen[q];
+    }
+    const size_t pb = x.pbase, cnt = (size_t)x.R * x.n;
+    if (!words_equal(at(R.enc) + pb * nn, b->enc, cnt * nn) || !words_equal(at(R.pz) + pb * nl, b->pdl_z, cnt * nl) ||
+        !words_equal(at(R.az) + pb * nl, b->rp_z, cnt * nl) || !words_equal(at(R.ae) + pb * el, b->rp_e, cnt * el) ||
+        !words_equal(at(R.ps1) + pb * s1l, b->pdl_s1, cnt * s1l) || !words_equal(at(R.Q) + pb * 16, b->commit, cnt * 16) ||
+        !words_equal(at(R.pu1) + pb * 16, b->pdl_u1, cnt * 16) || !words_equal(at(R.vss) + voff * 16, b->vss, (size_t)vk * 16) ||
+        !words_equal(at(R.pu2) + pb * nn, b->pdl_u2, cnt * nn) || !words_equal(at(R.pu3) + pb * nl, b->pdl_u3, cnt * nl) ||
+        !words_equal(at(R.as1) + pb * s1l, b->rp_s1, cnt * s1l) ||
+        !words_equal(at(R.rn) + x.rbase * nl, b->recv_n, (size_t)x.n * nl) ||
+        !words_equal(at(R.rt) + x.rbase * nl, b->recv_ntilde, (size_t)x.n * nl))
+      return false;
+    voff += vk;
+  }
+  return true;
+}
+
+
 // GA prestart of `count` sessions (one: fsdkr_collect_prestart; many:
 // fsdkr_collect_prestart_multi), in prepare's global order: session s's
 // receivers and pairs after session s-1's, every row at the widest nl.
@@ -307,6 +641,8 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   g.comb_pre.clear();
   g.ck_valid = false;
   g.tz_valid = false;
+  g.ch_valid = false;
+  g.nn_rows = g.nt_rows = nullptr;
   *n_out = *P_out = 0;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
   if (running && running->launched) {
@@ -316,7 +652,8 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // a prepared plan that consumed the previous prestart reads its s^N rows and
   // fixed-base tables in place: this prestart overwrites (or reallocates) those
   // buffers, so the plan is dropped (a later launch reports "no prepared batch")
-  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit)) free_collect_plan(c);
+  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit || running->ch_hit))
+    free_collect_plan(c);
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prestart: no batch");
     return FSDKR_E_ARG;
@@ -468,6 +805,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
     return rc;
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
   g.cons = cons;
+  g.nn_rows = reinterpret_cast<const uint32_t*>(dev + o_NN);
   g.wide = group == kWideGroup;
   if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
     return rc;
@@ -509,7 +847,8 @@ int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count)
   }
   GaPre& g = *gp;
   if (!g.fb_valid && (rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
-  return g.ck_valid ? FSDKR_OK : prestart_ck(c, bs, count, g);
+  if (!g.ck_valid && (rc = prestart_ck(c, bs, count, g))) return rc;
+  return g.ch_valid ? FSDKR_OK : prestart_chal(c, bs, count, g);
 }
 
 uint64_t rows_digest(const uint32_t* p, size_t rows, uint32_t w, uint64_t row0) {

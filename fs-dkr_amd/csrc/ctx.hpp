@@ -43,6 +43,9 @@ struct Ctx {
   uint8_t* pinned = nullptr;
   size_t pinned_bytes = 0;
   uint8_t* host_arena(size_t bytes);
+  // named grow-only pinned host buffers (a prestart's image, kept for prepare's match)
+  std::map<std::string, DevBuf> hbufs;
+  uint8_t* host_buf(const char* name, size_t bytes);
   // stream of the share-recovery entry points (decrypt, MSM): separate from the
   // collect pipeline so they overlap a launched batch (fsdkr_collect_launch)
   hipStream_t aux = nullptr;
@@ -79,6 +82,7 @@ struct Ctx {
   hipEvent_t span_beg = nullptr, span_end = nullptr;
   bool span_armed = false;
   float span_ms = -1.0f;
+  uint32_t reuse_mask = 0;   // prestarted parts the last prepare reused (fsdkr_collect_reuse_mask)
   int span_begin(hipStream_t st);
   // synchronise the stream and fold pending events into `times`
   int sync();

@@ -143,6 +143,8 @@ def lib():
     L.fsdkr_collect_prestart.restype = ctypes.c_int
     L.fsdkr_collect_last_span_ms.argtypes = [vp]
     L.fsdkr_collect_last_span_ms.restype = ctypes.c_double
+    L.fsdkr_collect_reuse_mask.argtypes = [vp]
+    L.fsdkr_collect_reuse_mask.restype = ctypes.c_uint32
     L.fsdkr_collect_finish.argtypes = [vp, ctypes.POINTER(VerdictsC)]
     L.fsdkr_collect_finish.restype = ctypes.c_int
     L.fsdkr_collect_prepare_multi.argtypes = [vp, ctypes.POINTER(CollectBatchC), ctypes.c_uint32]
@@ -374,6 +376,13 @@ class Context:
         """Device span of the last finished collect() call (HIP events: first
         device work -> the pipeline's last kernel), -1 before any."""
         return float(self._lib.fsdkr_collect_last_span_ms(self._h))
+
+    REUSE = {"ga": 1, "tables": 2, "ck": 4, "tz": 8, "chal": 16}
+
+    def collect_reuse(self):
+        """Names of the prestarted parts the last prepare reused (fsdkr_collect_reuse_mask)."""
+        m = int(self._lib.fsdkr_collect_reuse_mask(self._h))
+        return {k for k, bit in self.REUSE.items() if m & bit}
 
     def collect_launch(self):
         """Enqueue the kernel pipeline of the prepared batch (returns at once)."""

@@ -229,7 +229,7 @@ class CollectBatch:
         M = m_security
         G = _Gather()
         k = self._k
-        self._ga, self._pending, self._stage1b = None, None, None
+        self._ga, self._pending, self._stage1b, self._stage1c = None, None, None, False
         if self.header_only:
             f_ckn = G.field([m.ek.n for m in all_m] or [0])
             ck_bits = max(1, f_ckn[1])
@@ -280,6 +280,7 @@ class CollectBatch:
             # whole call 0.5-1.2 ms shorter, profiles/r04/r04g_*, r04h_*)
             names = ("recv_n", "pdl_s2", "rp_s") + (() if split_stage1 else _STAGE1B)
             self._stage1b = _STAGE1B if split_stage1 else None
+            self._stage1c = split_stage1
             ga = {name: Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c)) for name in names}
             # the correct-key job (sigma^n mod n) reads only ek.n and sigma: stage 1
             # packs them at the width complete() gives them, so the prestart runs
@@ -350,17 +351,7 @@ class CollectBatch:
         c, k = self.c, self._k
         msgs, joins, all_m, n, M, G, F = (st[x] for x in ("msgs", "joins", "all_m", "n", "M", "G", "F"))
         J = len(joins)
-        pdl, rng = st["pdl"], st["rng"]
-        F["enc"] = G.field([m.points_encrypted_vec[i] for m in msgs for i in range(n)])
-        for a in ("z", "u2", "u3"):
-            F["pdl_" + a] = G.field(pdl, a)
-        for a in ("z", "e"):
-            F["rp_" + a] = G.field(rng, a)
-        if J:
-            for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
-                F["dlog_" + name] = G.field([j.dlog_statement for j in joins], attr)
-            for name, which, attr in (("x1", 1, "x"), ("x2", 2, "x"), ("y1", 1, "y"), ("y2", 2, "y")):
-                F["dlog_" + name] = G.field([getattr(j, f"composite_dlog_proof_base_h{which}") for j in joins], attr)
+        self._late(st)
 
         def bits(*names):
             return max([1] + [F[x][1] for x in names if x in F])
@@ -383,6 +374,11 @@ class CollectBatch:
         keep = set()
         if self._ga is not None:
             keep = {x for x in self._ga[1] if self._ga[0] == nl or x in _STAGE1_WIDTH}
+            if "rp_e" in keep and self._ga[1]["rp_e"].shape[1] != c.el:
+                keep.discard("rp_e")
+            for y in ("dlog_y1", "dlog_y2"):
+                if y in keep and self._ga[1][y].shape[1] != c.yl:
+                    keep.discard(y)
         for name, f in F.items():
             if name not in keep:
                 setattr(c, name, k(G.slot(f, width.get(name, nl))))
@@ -395,15 +391,79 @@ class CollectBatch:
         if st["ck_short"]:
             c.ck_lens = k(np.array([len(x) for x in st["sig"]], dtype=np.uint32))
         G.run()
-        c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
-        c.pdl_u1 = k(pack_points(pdl, "u1"))
-        t = st["t"]
-        com = [list(m.coefficients_committed_vec.commitments) for m in msgs]
-        if any(len(x) != t + 1 for x in com):   # Horner over each message's own vector
-            c.vss_len = k(np.array([len(x) for x in com], dtype=np.uint32))
-        c.vss = k(pack_points([p for x in com for p in x] or [None]))
+        if "commit" not in ga_arrs:   # (stage1c packed the points already)
+            self._points(st)
         self.nl = nl
         return self
+
+    def _late(self, st):
+        """The gathers of the challenge jobs' fields (PDL transcript, Alice c / z / e,
+        DLog proofs): from stage1c() or complete(), once."""
+        if st.get("late"):
+            return
+        st["late"] = True
+        F, G, pdl, rng, n = st["F"], st["G"], st["pdl"], st["rng"], st["n"]
+        F["enc"] = G.field([m.points_encrypted_vec[i] for m in st["msgs"] for i in range(n)])
+        for a in ("z", "u2", "u3"):
+            F["pdl_" + a] = G.field(pdl, a)
+        for a in ("z", "e"):
+            F["rp_" + a] = G.field(rng, a)
+        if st["joins"]:
+            for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
+                F["dlog_" + name] = G.field([j.dlog_statement for j in st["joins"]], attr)
+            for name, which, attr in (("x1", 1, "x"), ("x2", 2, "x"), ("y1", 1, "y"), ("y2", 2, "y")):
+                F["dlog_" + name] = G.field([getattr(j, f"composite_dlog_proof_base_h{which}") for j in st["joins"]],
+                                            attr)
+
+    def _points(self, st):
+        """secp256k1 points: the shares' commitments Q, PDL u1 and the VSS commitments"""
+        c, k, n, msgs = self.c, self._k, st["n"], st["msgs"]
+        c.commit = k(pack_points([m.points_committed_vec[i] for m in msgs for i in range(n)]))
+        c.pdl_u1 = k(pack_points(st["pdl"], "u1"))
+        com = [list(m.coefficients_committed_vec.commitments) for m in msgs]
+        if any(len(x) != st["t"] + 1 for x in com):   # Horner over each message's own vector
+            c.vss_len = k(np.array([len(x) for x in com], dtype=np.uint32))
+        c.vss = k(pack_points([p for x in com for p in x] or [None]))
+
+    def stage1c(self):
+        """After stage1b(): the fields of the jobs that read no exponent table -- the
+        PDL transcript (c, z, u1, u2, u3, Q), Alice c / z / e, the Feldman
+        commitments, ek.n with sigma_vec and the joins' DLog proofs -- at the width
+        complete() gives them, for a third fsdkr_collect_prestart call: the PDL
+        challenges are hashed on the host and c^e, z^e (their inverses and unit
+        flags), pdl_u1, Feldman, the correct-key and DLog exponentiations start
+        beside GA instead of after prepare.  True when it packed them (False: a
+        field is wider than stage 1's width, or stage 1 was not split)."""
+        if not self._stage1c or self._pending is None or self._ga is None or self._stage1b is not None:
+            return False
+        self._stage1c = False
+        st = self._pending
+        self._rest()
+        self._late(st)
+        F, c = st["F"], self.c
+        nl_ga, ga = self._ga
+        one = max(F[x][1] for x in ("pdl_z", "pdl_u3", "rp_z"))
+        two = max(F[x][1] for x in ("enc", "pdl_u2"))
+        dl = max([1] + [F[x][1] for x in ("dlog_N", "dlog_g", "dlog_ni", "dlog_x1", "dlog_x2") if x in F])
+        if max(one, dl) > 32 * nl_ga or two > 64 * nl_ga or st["ck_short"]:
+            return False   # complete() picks the batch width; the prestart is skipped
+        c.el = _limbs_for(max(F["rp_e"][1], 1))
+        if "dlog_y1" in F:
+            c.yl = _limbs_for(max(F["dlog_y1"][1], F["dlog_y2"][1], 1))
+        width = {"enc": 2 * nl_ga, "pdl_u2": 2 * nl_ga, "rp_e": c.el, "dlog_y1": c.yl, "dlog_y2": c.yl}
+        names = [x for x in _STAGE1C if x in F]
+        Gs = _Gather()
+        for name in names:
+            ga[name] = Gs.slot(F[name], width.get(name, nl_ga))
+        c.ckl = max(st["ckl"], nl_ga)
+        ga["ck_n"] = Gs.slot(st["f_ckn"], c.ckl)
+        ga["ck_sigma"] = Gs.slot(st["f_sig"], c.ckl)
+        Gs.run()
+        for name in names + ["ck_n", "ck_sigma"]:
+            setattr(c, name, self._k(ga[name]))
+        self._points(st)
+        ga["commit"] = None   # marker: complete() keeps the packed points
+        return True
 
     def stage1b(self):
         """The rest of stage 1 (the fixed-base tables' bases and the exponents
@@ -447,6 +507,10 @@ class CollectBatch:
 # stage-1 fields after GA's own (recv_n, pdl_s2, rp_s): the fixed-base tables'
 # bases and the exponents that size them
 _STAGE1B = ("recv_ntilde", "recv_h1", "recv_h2", "ped_T", "ped_N", "pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
+
+# stage 1c (after 1b): the challenge jobs' limb fields (+ the points, ek.n and sigma_vec)
+_STAGE1C = ("enc", "pdl_z", "pdl_u2", "pdl_u3", "rp_z", "rp_e", "dlog_N", "dlog_g", "dlog_ni", "dlog_x1", "dlog_x2",
+            "dlog_y1", "dlog_y2")
 
 # stage-1 fields whose slot width does not depend on nl
 _STAGE1_WIDTH = {"pdl_s1": lambda c: c.s1l, "rp_s1": lambda c: c.s1l, "pdl_s3": lambda c: c.s3l,

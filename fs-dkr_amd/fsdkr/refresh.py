@@ -228,6 +228,22 @@ def _check_mode(recovery):
         raise ValueError(f"recovery must be one of {RECOVERY_MODES}")
 
 
+def prestart(ctx, batch):
+    """The staged starts of a CollectBatch(..., staged=True) before complete():
+    stage 1 (GA's fields) -> fsdkr_collect_prestart starts GA; stage 1b (the
+    tables' bases and exponents) -> the table chains and comb tables start beside
+    it; stage 1c (the PDL transcripts, Alice c / z / e, Feldman, correct-key and
+    DLog inputs) -> the challenge jobs start.  Each call finds GA running and
+    starts what the newly packed fields allow."""
+    if not batch.ga_ready or not hasattr(ctx, "collect_prestart"):
+        return
+    ctx.collect_prestart(batch)
+    if batch.stage1b():
+        ctx.collect_prestart(batch)
+        if batch.stage1c():
+            ctx.collect_prestart(batch)
+
+
 def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_security=256, key_bits=2048,
             recovery="speculative"):
     """RefreshMessage::collect (refresh_message.rs:321-467).  `recovery`:
@@ -241,10 +257,7 @@ def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_secu
     # stage 1 packs what the pipeline's longest job reads and starts it on the GPU;
     # the rest of the batch is packed while those chains run
     batch = CollectBatch(msgs, local_key, joins, m_security, key_bits, staged=True)
-    if batch.ga_ready:
-        ctx.collect_prestart(batch)
-        if batch.stage1b():   # the tables' fields after GA's: GA keeps running, the tables start
-            ctx.collect_prestart(batch)
+    prestart(ctx, batch)
     spec, verdicts, pend = None, None, None
     batch.complete()
     if not batch.header_only:
@@ -342,10 +355,7 @@ def collect_all(refresh_messages, parties, join_messages, ctx=None, m_security=2
     for members in groups.values():
         lk0 = parties[members[0]][0]
         batch = CollectBatch(msgs, lk0, joins, m_security, key_bits, staged=True)
-        if batch.ga_ready:
-            ctx.collect_prestart(batch)
-            if batch.stage1b():
-                ctx.collect_prestart(batch)
+        prestart(ctx, batch)
         jobs = [(msgs, parties[p][0], len(msgs) + len(joins)) for p in members]
         specs = [None] * len(members)
         verdicts, pend = None, None

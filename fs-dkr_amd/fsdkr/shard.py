@@ -171,10 +171,8 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
     b = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], m_security, key_bits, n_recv=n, staged=True)
     if b.header_only:   # an empty refresh slice (joins only) or a size failure the header batch reports
         return None, None
-    if b.ga_ready and hasattr(ctx, "collect_prestart"):   # the long chains start while stage 2 packs
-        ctx.collect_prestart(b)
-        if b.stage1b():
-            ctx.collect_prestart(b)
+    from .refresh import prestart
+    prestart(ctx, b)   # the long chains start while stage 2 packs
     b.complete()
     ctx.collect_prepare(b)
     ctx.collect_launch()

@@ -234,8 +234,19 @@ int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
  * recv_h2, ped_T, ped_N and the exponent widths) and the correct-key job (ck_n,
  * ck_sigma) start too when present.  Called again with the same GA fields while
  * those chains run (a caller that packed them first), it leaves GA running and
- * starts only the parts that are new. */
+ * starts only the parts that are new.  Once the tables are started, a call that
+ * finds the challenge jobs' fields (enc, commit, pdl_z, pdl_u1, pdl_u2, pdl_u3,
+ * rp_z, rp_e, el, vss with the table call's pdl_s1 / rp_s1) starts them: the PDL
+ * challenges (hashed on the host), c^e mod N^2 and z^e mod N~ of the PDL and
+ * Alice proofs with their inverses, pdl_u1 and the Feldman checks.  prepare
+ * reuses each started part only if every row that part read is equal. */
 int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
+
+/* Which prestarted parts the last fsdkr_collect_prepare[_multi] reused (bit
+ * mask): 1 GA chains, 2 fixed-base tables, 4 correct-key job, 8 ring-Pedersen
+ * T^Z exponents, 16 challenge jobs.  0 before any prepare.  Diagnostic (tests
+ * check that a changed batch is recomputed); the reference has no counterpart. */
+uint32_t fsdkr_collect_reuse_mask(const fsdkr_ctx* ctx);
 
 /* Device span of the last finished collect() call (single or multi-session), in
  * ms from HIP timing events: from the call's first device work (the end of the

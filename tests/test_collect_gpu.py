@@ -351,3 +351,67 @@ def test_collect_recover_launch_finish(gpu_ctx, dkr5):
     with pytest.raises(FsdkrError):
         gpu_ctx.collect_recover_finish(h)        # nothing launched any more
     assert gpu_ctx.collect_recover(jobs) == want  # the context is usable again
+
+
+def _vt(v):
+    return tuple(bytes(getattr(v, f)) for f in ("feldman", "pdl", "range", "ped", "ck", "dlog"))
+
+
+def _change(msgs, field):
+    """one field of pair (message 1, receiver 2) changed: a field the prestarted
+    challenge jobs read (or hash)"""
+    bad = copy.deepcopy(msgs)
+    m = bad[1]
+    if field in ("u1", "u2", "u3", "z", "s1"):
+        p = m.pdl_proof_vec[2]
+        val = ec.add(p.u1, ec.G) if field == "u1" else getattr(p, field) + 1
+        m.pdl_proof_vec[2] = dataclasses.replace(p, **{field: val})
+    elif field in ("alice_z", "alice_e"):
+        a = m.range_proofs[2]
+        f = field.split("_")[1]
+        m.range_proofs[2] = dataclasses.replace(a, **{f: getattr(a, f) ^ 1})
+    elif field == "c":
+        m.points_encrypted_vec = list(m.points_encrypted_vec)
+        m.points_encrypted_vec[2] += 1
+    elif field == "Q":
+        m.points_committed_vec = list(m.points_committed_vec)
+        m.points_committed_vec[2] = ec.add(m.points_committed_vec[2], ec.G)
+    elif field == "vss":
+        com = m.coefficients_committed_vec
+        pts = list(com.commitments)
+        pts[0] = ec.add(pts[0], ec.G)
+        m.coefficients_committed_vec = type(com)(**{**com.__dict__, "commitments": pts})
+    return bad
+
+
+@pytest.mark.parametrize("field", ["u1", "u2", "u3", "z", "s1", "alice_z", "alice_e", "c", "Q", "vss"])
+def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field):
+    """Stage 1c (CollectBatch.stage1c): the third fsdkr_collect_prestart starts the
+    challenge jobs -- PDL challenges hashed on the host, c^e mod N^2 and z^e mod
+    N~ with their inverses, pdl_u1, Feldman -- from the packed fields.  A prepare
+    of the same batch reuses them (fsdkr_collect_reuse_mask) and its verdicts equal
+    an un-prestarted run's.  A prepare of a batch with one field changed after the
+    prestart must recompute them: its verdicts equal that batch's own
+    un-prestarted run, which rejects the changed pair."""
+    from fsdkr.batch import CollectBatch
+    from fsdkr.refresh import prestart
+    keys, msgs, dks, _ = _dkr(1, 3, "prestart-chal")
+    lk = keys[0]
+    a = CollectBatch(msgs, lk, [], 256, KB, staged=True)
+    prestart(gpu_ctx, a)
+    a.complete()
+    gpu_ctx.collect_prepare(a)
+    assert {"ga", "chal"} <= gpu_ctx.collect_reuse()
+    v = gpu_ctx.collect_run(a)
+    ref = gpu_ctx.verify_collect(CollectBatch(msgs, lk, [], 256, KB))
+    assert _vt(v) == _vt(ref)
+    assert (v.pdl & 7 == 7).all() and (v.range & 1).all() and (v.feldman & 1).all()
+    bad = _change(msgs, field)
+    prestart(gpu_ctx, CollectBatch(msgs, lk, [], 256, KB, staged=True))
+    b = CollectBatch(bad, lk, [], 256, KB)
+    gpu_ctx.collect_prepare(b)
+    assert "chal" not in gpu_ctx.collect_reuse()
+    vb = gpu_ctx.collect_run(b)
+    want = gpu_ctx.verify_collect(CollectBatch(bad, lk, [], 256, KB))
+    assert _vt(vb) == _vt(want)
+    assert _vt(want) != _vt(ref)
