@@ -25,6 +25,7 @@ void free_ga_pre(Ctx* c) {
   if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
   if (g && g->fb_setup) (void)hipEventDestroy(g->fb_setup);
+  if (g && g->fx_done) (void)hipEventDestroy(g->fx_done);
   if (g && g->ck_done) (void)hipEventDestroy(g->ck_done);
   if (g && g->tz_done) (void)hipEventDestroy(g->tz_done);
   if (g && g->comb_done) (void)hipEventDestroy(g->comb_done);

@@ -329,6 +329,9 @@ struct CollectPlan {
   // prestart (ch_hit): the pipeline waits for ch_ev before its equalities
   bool ch_hit = false;
   hipEvent_t ch_ev[3] = {};
+  // the fixed-base exponents computed by the prestart (fx_hit): J3 / J4 / RP rows there
+  bool fx_hit = false;
+  hipEvent_t fx_done = nullptr;
   // device words finish reads back (the plan's output region, or the prestart's)
   const void *r_unn = nullptr, *r_uzA = nullptr, *r_uzp = nullptr, *r_pdlv = nullptr, *r_fel = nullptr;
   FbJob fb;
@@ -363,6 +366,7 @@ struct GaPre {
   // for exponents of up to bits_h1 / bits_h2 bits with window w
   bool fb_valid = false;
   std::vector<uint32_t> ntilde, h1, h2, T, pedmod;   // bases, and the T_m moduli rows
+  std::vector<uint64_t> fb_bptr;                      // device rows of the bases [h1_i | T_m | h2_i]
   uint32_t Mt = 0, fb_w = 0, bits_h1 = 0, bits_h2 = 0, bits_z = 0, fb_entries = 0;
   uint32_t* fb_table = nullptr;
   hipEvent_t fb_done = nullptr;     // every table built
@@ -409,6 +413,15 @@ struct GaPre {
   uint32_t *ch_unn = nullptr, *ch_uzA = nullptr, *ch_uzp = nullptr;
   uint8_t *ch_pdlv = nullptr, *ch_fel = nullptr;
   hipEvent_t ch_ev[3] = {};
+  // the fixed-base exponents (prestart_fbx, when stage 1b packed the exponents): h1^s1 |
+  // h1^s1A -> J3 slots, h2^s3 | h2^s2A -> J4 slots, T_m^Z_k -> RP rows, as combs over the
+  // prestarted tables; fx_host keeps the exponent rows for prepare's match
+  bool fx_valid = false;
+  uint32_t fx_s1l = 0, fx_s3l = 0, fx_zl = 0;
+  const uint8_t* fx_host = nullptr;
+  size_t fx_ps1 = 0, fx_as1 = 0, fx_ps3 = 0, fx_as2 = 0, fx_z = 0;   // offsets in fx_host
+  uint32_t *fx_J3 = nullptr, *fx_J4 = nullptr, *fx_RP = nullptr;
+  hipEvent_t fx_done = nullptr;
 };
 
 // width-independent 64-bit digest of `rows` rows of `w` words (trailing zero
@@ -540,6 +553,7 @@ int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count)
 int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
+bool fbx_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_prepare.cpp
 int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_launch.cpp

@@ -216,6 +216,7 @@ int collect_launch_impl(Ctx* c) {
   }
   if (pl.ga_hit) (void)hipStreamWaitEvent(st, pl.ga_done, 0);   // the prestarted s^N rows
   if (pl.tz_hit) (void)hipStreamWaitEvent(st, pl.tz_done, 0);   // the prestarted ring-Pedersen T^Z rows
+  if (pl.fx_hit) (void)hipStreamWaitEvent(st, pl.fx_done, 0);   // the prestarted fixed-base exponents
   if (pl.ch_hit)   // the prestarted challenge jobs (J2, J5 -> inverses; pdl_u1 -> Feldman)
     for (hipEvent_t ev : pl.ch_ev) (void)hipStreamWaitEvent(st, ev, 0);
   // equality checks and exact products

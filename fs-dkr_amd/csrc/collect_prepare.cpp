@@ -561,6 +561,39 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };        // input address
   auto DX = [&](size_t o) { return (uint64_t)(uintptr_t)(out_base + o); };   // output address
 
+  // the h1_i / h2_i tables of a prestart: sized for the prestart's exponent bounds
+  // (taller tables only add unused entries), used if the layout then agrees
+  const GaPre* gp = reinterpret_cast<const GaPre*>(c->ga_pre);
+  // the prestart's rows are global (session s after s-1) at width nl, zero-extended
+  auto same_rows = [&](const std::vector<uint32_t>& pre, size_t base, const uint32_t* src, size_t rows,
+                       uint32_t ws) {
+    if (pre.size() < (base + rows) * nl) return false;
+    for (size_t r = 0; r < rows; ++r) {
+      const uint32_t* a = pre.data() + (base + r) * nl;
+      if (memcmp(a, src + r * ws, (size_t)ws * 4) != 0) return false;
+      for (uint32_t k = ws; k < nl; ++k)
+        if (a[k]) return false;
+    }
+    return true;
+  };
+  bool fb_cand = gp && gp->fb_valid && gp->nl == nl && gp->n == n && gp->Mt == Mt &&
+                 memcmp(gp->pedmod.data(), PEDN.data(), (size_t)Mt * nl * 4) == 0 &&
+                 std::max(mx.s1, mx.as1) <= gp->bits_h1 && std::max(mx.s3, mx.as2) <= gp->bits_h2 &&
+                 z_max <= gp->bits_z;
+  for (const Sess& x : pl.ss) {
+    if (!fb_cand) break;
+    fb_cand = same_rows(gp->ntilde, x.rbase, x.b->recv_ntilde, x.n, x.b->nl) &&
+              same_rows(gp->h1, x.rbase, x.b->recv_h1, x.n, x.b->nl) &&
+              same_rows(gp->h2, x.rbase, x.b->recv_h2, x.n, x.b->nl) &&
+              same_rows(gp->T, x.mbase, x.b->ped_T, x.Mt, x.b->nl);
+  }
+  // the fixed-base exponents of a prestart (stage 1b's exponent rows, the same tables):
+  // h1 / h2 / T^Z instances are not launched again
+  pl.fx_hit = fb_cand && fbx_pre_matches(c, bs, count);
+  if (pl.fx_hit) {
+    pl.fx_done = gp->fx_done;
+    reinterpret_cast<GaPre*>(c->ga_pre)->fx_valid = false;   // consumed
+  }
   // ---------------- modexp jobs (descriptors addressed into the image)
   ModexpJob J1, J2, J5, J7, J8, J9, GC;
   J1.k32 = J2.k32 = J9.k32 = nn;
@@ -603,14 +636,18 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       // fixed bases (FB): h1^s1 -> J3 slot | h2^s3 (s2 for Alice) -> J4 slot;  J5: z^e
       const size_t slot = (size_t)which * P + p;
       if (which == 0) {
-        FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
-        fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
+        if (!pl.fx_hit) {
+          FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
+          fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
+        }
         if (!pl.ch_hit) J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
-        FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
-        fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
-                            DX(x_J4 + slot * nl * 4)});
+        if (!pl.fx_hit) {
+          FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
+          fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
+                              DX(x_J4 + slot * nl * 4)});
+        }
         if (!pl.ch_hit) J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
       }
     }
@@ -621,7 +658,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       J9.add(DI(o_NP1 + (size_t)r * nn * 4), nn, DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, r);
     }
   clk.lap("desc pairs");
-  if (!tz_hit) {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
+  if (!tz_hit && !pl.fx_hit) {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
     const size_t o = FB.grow((size_t)Mt * M);
     for (uint32_t m = 0; m < Mt; ++m) FB.b_bits[fb_T[m]] = std::max(FB.b_bits[fb_T[m]], std::max(z_max, 1u));
     parallel_for(Mt, 16, [&](size_t m0, size_t m1) {
@@ -684,32 +721,6 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   GD.append(J8);
   const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD),
                d_GC = pack_job(GC);
-  // the h1_i / h2_i tables of a prestart: sized for the prestart's exponent bounds
-  // (taller tables only add unused entries), used if the layout then agrees
-  const GaPre* gp = reinterpret_cast<const GaPre*>(c->ga_pre);
-  // the prestart's rows are global (session s after s-1) at width nl, zero-extended
-  auto same_rows = [&](const std::vector<uint32_t>& pre, size_t base, const uint32_t* src, size_t rows,
-                       uint32_t ws) {
-    if (pre.size() < (base + rows) * nl) return false;
-    for (size_t r = 0; r < rows; ++r) {
-      const uint32_t* a = pre.data() + (base + r) * nl;
-      if (memcmp(a, src + r * ws, (size_t)ws * 4) != 0) return false;
-      for (uint32_t k = ws; k < nl; ++k)
-        if (a[k]) return false;
-    }
-    return true;
-  };
-  bool fb_cand = gp && gp->fb_valid && gp->nl == nl && gp->n == n && gp->Mt == Mt &&
-                 memcmp(gp->pedmod.data(), PEDN.data(), (size_t)Mt * nl * 4) == 0 &&
-                 std::max(mx.s1, mx.as1) <= gp->bits_h1 && std::max(mx.s3, mx.as2) <= gp->bits_h2 &&
-                 z_max <= gp->bits_z;
-  for (const Sess& x : pl.ss) {
-    if (!fb_cand) break;
-    fb_cand = same_rows(gp->ntilde, x.rbase, x.b->recv_ntilde, x.n, x.b->nl) &&
-              same_rows(gp->h1, x.rbase, x.b->recv_h1, x.n, x.b->nl) &&
-              same_rows(gp->h2, x.rbase, x.b->recv_h2, x.n, x.b->nl) &&
-              same_rows(gp->T, x.mbase, x.b->ped_T, x.Mt, x.b->nl);
-  }
   if (fb_cand) {
     for (uint32_t r = 0; r < n; ++r) {
       FB.b_bits[fb_h1[r]] = gp->bits_h1;
@@ -771,6 +782,14 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   }
   const size_t d_iynn = put(inv_y_nn.data(), inv_y_nn.size() * 8), d_imnn = put(inv_m_nn.data(), inv_m_nn.size() * 8);
   const size_t d_iynl = put(inv_y_nl.data(), inv_y_nl.size() * 8), d_imnl = put(inv_m_nl.data(), inv_m_nl.size() * 8);
+  // the fixed-base rows (J3, J4, RP): the prestart's (fx_hit) or this plan's outputs
+  const GaPre* gfx = reinterpret_cast<const GaPre*>(c->ga_pre);
+  auto J3_row = [&](size_t k) {
+    return pl.fx_hit ? (uint64_t)(uintptr_t)(gfx->fx_J3 + k * nl) : DX(x_J3 + k * nl * 4);
+  };
+  auto J4_row = [&](size_t k) {
+    return pl.fx_hit ? (uint64_t)(uintptr_t)(gfx->fx_J4 + k * nl) : DX(x_J4 + k * nl * 4);
+  };
   // the rows of J2 / J5 and the inverses: the prestart's (ch_hit) or this plan's outputs
   auto J2_row = [&](size_t k) {
     return pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_J2 + k * nn) : DX(x_J2 + k * nn * 4);
@@ -797,8 +816,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   eq_nl_mod.reserve(n_eqnl);
   for (uint32_t p = 0; p < P; ++p) {  // PDL u3: h1^s1 * h2^s3 == u3 * z^e  (mod N~), u3 < N~
     EqOperand e;
-    e.a = DX(x_J3 + (size_t)p * nl * 4);
-    e.b = DX(x_J4 + (size_t)p * nl * 4);
+    e.a = J3_row(p);
+    e.b = J4_row(p);
     e.c = DI(o_pu3 + (size_t)p * nl * 4);
     e.d = J5_row(p);
     e.a_len = e.b_len = e.c_len = e.d_len = nl;
@@ -810,7 +829,9 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N; the odd part here)
       EqOperand e;
-      e.a = tz_out ? (uint64_t)(uintptr_t)(tz_out + ((size_t)m * M + k) * nl) : DX(x_RP + ((size_t)m * M + k) * nl * 4);
+      e.a = pl.fx_hit   ? (uint64_t)(uintptr_t)(gfx->fx_RP + ((size_t)m * M + k) * nl)
+            : tz_out ? (uint64_t)(uintptr_t)(tz_out + ((size_t)m * M + k) * nl)
+                     : DX(x_RP + ((size_t)m * M + k) * nl * 4);
       e.b = DI(o_one);
       e.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
       e.d = DI(o_pS + (size_t)m * nl * 4);
@@ -861,7 +882,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), pl.ga_hit ? J1_at((size_t)P + p) : DX(x_J1 + ((size_t)P + p) * nn * 4),
                 pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invc + (size_t)p * nn) : DX(x_invc + (size_t)p * nn * 4),
                 nn, nn, nn, 0};
-    p3_nl[p] = {DX(x_J3 + ((size_t)P + p) * nl * 4), DX(x_J4 + ((size_t)P + p) * nl * 4),
+    p3_nl[p] = {J3_row((size_t)P + p), J4_row((size_t)P + p),
                 pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invz + (size_t)p * nl) : DX(x_invz + (size_t)p * nl * 4),
                 nl, nl, nl, 0};
   }
@@ -992,7 +1013,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   pl.n_eq_ck = (uint32_t)eq_ck.size();
   for (Sess& x : pl.ss) x.b = nullptr;   // the caller's buffers are not used after prepare
   c->reuse_mask = (pl.ga_hit ? 1u : 0u) | (pl.fb_hit ? 2u : 0u) | (pl.ck_hit ? 4u : 0u) | (pl.tz_hit ? 8u : 0u) |
-                  (pl.ch_hit ? 16u : 0u);
+                  (pl.ch_hit ? 16u : 0u) | (pl.fx_hit ? 32u : 0u);
   c->plan = plan.release();
   return FSDKR_OK;
 }

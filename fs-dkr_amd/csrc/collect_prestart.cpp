@@ -154,6 +154,7 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
     bp[n + Mt + r] = (uint64_t)(uintptr_t)(dev + o_h2 + (size_t)r * nl * 4);
   }
   for (uint32_t m = 0; m < Mt; ++m) bp[n + m] = (uint64_t)(uintptr_t)(dev + o_T + (size_t)m * nl * 4);
+  g.fb_bptr.assign(bp, bp + nb);
   std::vector<uint32_t> blen(nb, nl);
   memcpy(img.data() + o_bl, blen.data(), (size_t)nb * 4);
   memcpy(img.data() + o_bm, L.mod.data(), (size_t)nb * 4);
@@ -297,6 +298,189 @@ static int prestart_ck(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, Ga
   g.ck_Mt = Mt;
   g.ck_valid = true;
   return FSDKR_OK;
+}
+
+
+// The fixed-base exponents of a batch whose stage 1b packed the exponents (PDL s1, s3;
+// Alice s1, s2; ring-Pedersen Z): h1_i^s1 | h1_i^s1A (zk_pdl_with_slack.rs:144-157,
+// range_proofs.rs:129-137: the J3 slots), h2_i^s3 | h2_i^s2A (J4), T_m^Z_k
+// (ring_pedersen_proof.rs:144: RP rows), in prepare's instance order, as combs over the
+// prestarted tables (or BGMW over the chains), on the pipeline's fixed-base stream: the
+// schedules run at once, the exponents as soon as the tables exist.  Alice instances
+// run with their full exponents (prepare gives a rejected proof exponent 0; the
+// results then differ, but that proof's verdict is false either way: its w is never
+// compared).  prepare takes the rows when the exponent rows and the tables match (fx_hit).
+static int prestart_fbx(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, GaPre& g) {
+  if (!g.fb_valid || g.sess.size() != count || g.fb_bptr.size() != 2 * (size_t)g.n + g.Mt || !g.fb_table) return FSDKR_OK;
+  const uint32_t nl = g.nl, n = g.n, Mt = g.Mt, M = bs[0].m_security;
+  uint32_t s1l = 0, s3l = 0, zl = 0, P = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    if (b->nl != nl || !b->pdl_s1 || !b->rp_s1 || !b->pdl_s3 || !b->rp_s2 || !b->ped_Z || !b->s1l || !b->s3l ||
+        !b->zl || b->ped_lens || b->range_lens || b->m_security != M || (k && (b->s1l != s1l || b->s3l != s3l || b->zl != zl)))
+      return FSDKR_OK;
+    s1l = b->s1l;
+    s3l = b->s3l;
+    zl = b->zl;
+    if (g.sess[k].pbase != P) return FSDKR_OK;
+    P += g.sess[k].R * g.sess[k].n;
+  }
+  const size_t rows_z = (size_t)Mt * M;
+  // host image: the exponent rows (uploaded, kept for the match)
+  auto al = Img::al;
+  const size_t o_ps1 = 0, o_as1 = al((size_t)P * s1l * 4), o_ps3 = o_as1 + al((size_t)P * s1l * 4),
+               o_as2 = o_ps3 + al((size_t)P * s3l * 4), o_z = o_as2 + al((size_t)P * s3l * 4),
+               o_rows_end = o_z + al(rows_z * zl * 4);
+  // outputs: J3 [2P], J4 [2P], RP [Mt M] rows at nl
+  const size_t o_J3 = o_rows_end, o_J4 = o_J3 + al((size_t)2 * P * nl * 4), o_RP = o_J4 + al((size_t)2 * P * nl * 4),
+               o_desc = o_RP + al(rows_z * nl * 4);
+  uint8_t* dev0 = (uint8_t*)c->buf("collect_fx_pre", o_desc);   // rows + outputs (descriptors: their own buffer)
+  uint8_t* img = c->host_buf("collect_fx_img", o_rows_end);
+  if (!dev0 || !img) {
+    c->fail("fsdkr_collect_prestart: fixed-base exponent allocation failed");
+    return FSDKR_E_OOM;
+  }
+  auto DI = [&](size_t off) { return (uint64_t)(uintptr_t)(dev0 + off); };
+  {
+    struct Cp {
+      uint8_t* dst;
+      const void* src;
+      size_t bytes;
+    };
+    std::vector<Cp> cps;
+    auto add = [&](size_t dst, const void* src, size_t bytes) {
+      constexpr size_t kChunk = 1u << 20;
+      for (size_t q = 0; q < bytes; q += kChunk)
+        cps.push_back(Cp{img + dst + q, (const uint8_t*)src + q, std::min(kChunk, bytes - q)});
+    };
+    size_t zrow = 0;
+    for (uint32_t k = 0; k < count; ++k) {
+      const fsdkr_collect_batch* b = bs + k;
+      const size_t pb = g.sess[k].pbase, cnt = (size_t)g.sess[k].R * g.sess[k].n;
+      const size_t zr = (size_t)(b->n_refresh + b->n_join) * M;
+      add(o_ps1 + pb * s1l * 4, b->pdl_s1, cnt * s1l * 4);
+      add(o_as1 + pb * s1l * 4, b->rp_s1, cnt * s1l * 4);
+      add(o_ps3 + pb * s3l * 4, b->pdl_s3, cnt * s3l * 4);
+      add(o_as2 + pb * s3l * 4, b->rp_s2, cnt * s3l * 4);
+      add(o_z + zrow * zl * 4, b->ped_Z, zr * zl * 4);
+      zrow += zr;
+    }
+    if (zrow != rows_z) return FSDKR_OK;
+    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
+      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].bytes);
+    });
+  }
+  // the job, as prepare builds it: bases [h1_i | T_m | h2_i], instances [h1 | T | h2]
+  std::vector<uint32_t> sess_of_pair(P);
+  for (uint32_t k = 0; k < count; ++k)
+    std::fill(sess_of_pair.begin() + g.sess[k].pbase, sess_of_pair.begin() + g.sess[k].pbase + g.sess[k].R * g.sess[k].n, k);
+  FbJob FX;
+  FX.k32 = nl;
+  for (uint32_t r = 0; r < n; ++r) FX.add_base(g.fb_bptr[r], nl, r);
+  for (uint32_t m = 0; m < Mt; ++m) FX.add_base(g.fb_bptr[n + m], nl, n + m);
+  for (uint32_t r = 0; r < n; ++r) FX.add_base(g.fb_bptr[n + Mt + r], nl, r);
+  for (int which = 0; which < 2; ++which)
+    for (uint32_t p = 0; p < P; ++p) {
+      const GaPre::Sess& x = g.sess[sess_of_pair[p]];
+      const uint32_t r = (uint32_t)(x.rbase + (p - x.pbase) % x.n);
+      FX.add(r, DI((which == 0 ? o_ps1 : o_as1) + (size_t)p * s1l * 4), s1l, 1,
+             DI(o_J3 + ((size_t)which * P + p) * nl * 4));
+    }
+  {
+    const size_t o = FX.grow(rows_z);
+    for (uint32_t m = 0; m < Mt; ++m)
+      for (uint32_t k = 0; k < M; ++k) {
+        const size_t i = o + (size_t)m * M + k, z = (size_t)m * M + k;
+        FX.e_ptr[i] = DI(o_z + z * zl * 4);
+        FX.e_len[i] = zl;
+        FX.e_base[i] = n + m;
+        FX.e_mod[i] = n + m;
+        FX.o_ptr[i] = DI(o_RP + z * nl * 4);
+      }
+  }
+  for (int which = 0; which < 2; ++which)
+    for (uint32_t p = 0; p < P; ++p) {
+      const GaPre::Sess& x = g.sess[sess_of_pair[p]];
+      const uint32_t r = (uint32_t)(x.rbase + (p - x.pbase) % x.n);
+      FX.add(n + Mt + r, DI((which == 0 ? o_ps3 : o_as2) + (size_t)p * s3l * 4), s3l, 1,
+             DI(o_J4 + ((size_t)which * P + p) * nl * 4));
+    }
+  // the prestart's table layout (sized by its exponent bounds)
+  for (uint32_t r = 0; r < n; ++r) {
+    FX.b_bits[r] = g.bits_h1;
+    FX.b_bits[n + Mt + r] = g.bits_h2;
+  }
+  for (uint32_t m = 0; m < Mt; ++m) FX.b_bits[n + m] = g.bits_z;
+  FX.finalize();
+  const FbLayout L = fb_layout(n, Mt, FX.w, g.bits_h1, g.bits_h2, g.bits_z);
+  bool same = FX.w == g.fb_w && L.entries == g.fb_entries;
+  for (uint32_t k = 0; k < FX.bases() && same; ++k)
+    same = FX.b_h[k] == L.h[k] && FX.b_toff[k] == L.toff[k] && FX.b_mod[k] == L.mod[k];
+  if (!same) return FSDKR_OK;
+  FX.plan_comb(comb_mem_cap(c), &g.comb_pre);
+  std::vector<uint8_t> desc;
+  FX.pack(desc);
+  const size_t o_sched = al(desc.size()), o_nst = o_sched + al(FX.sched_bytes()),
+               o_comb = o_nst + al(FX.nsteps_bytes()), dtotal = o_comb + al(FX.comb_scratch + 256);
+  uint8_t* dd = (uint8_t*)c->buf("collect_fx_desc", dtotal);
+  if (!dd) {
+    c->fail("fsdkr_collect_prestart: fixed-base exponent allocation failed");
+    return FSDKR_E_OOM;
+  }
+  hipStream_t fs = c->side_stream(1);   // launch()'s fixed-base stream
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(dev0, img, o_rows_end, hipMemcpyHostToDevice, fs), "prestart fbx H2D")) ||
+      (rc = c->hip_check(hipMemcpyAsync(dd, desc.data(), desc.size(), hipMemcpyHostToDevice, fs), "prestart fbx desc")) ||
+      (rc = c->hip_check(hipStreamSynchronize(fs), "prestart fbx desc sync")))   // desc is pageable and local
+    return rc;
+  FbDev fd{dd, g.fb_table, reinterpret_cast<uint16_t*>(dd + o_sched), reinterpret_cast<uint32_t*>(dd + o_nst),
+           FX.cgroups.empty() ? nullptr : dd + o_comb};
+  FbPre pre{g.fb_table, g.fb_entries, g.fb_done, g.comb_done};
+  if ((rc = fb_launch(c, FX, fd, g.fb_cons, fs, "fb prestart", nullptr, &pre))) return rc;
+  if (!g.fx_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fx_done, hipEventDisableTiming), "event")))
+    return rc;
+  if ((rc = c->hip_check(hipEventRecord(g.fx_done, fs), "event record"))) return rc;
+  g.fx_host = img;
+  g.fx_s1l = s1l;
+  g.fx_s3l = s3l;
+  g.fx_zl = zl;
+  g.fx_ps1 = o_ps1;
+  g.fx_as1 = o_as1;
+  g.fx_ps3 = o_ps3;
+  g.fx_as2 = o_as2;
+  g.fx_z = o_z;
+  g.fx_J3 = reinterpret_cast<uint32_t*>(dev0 + o_J3);
+  g.fx_J4 = reinterpret_cast<uint32_t*>(dev0 + o_J4);
+  g.fx_RP = reinterpret_cast<uint32_t*>(dev0 + o_RP);
+  g.fx_valid = true;
+  return FSDKR_OK;
+}
+
+// do the prestarted fixed-base exponents read these sessions' exponent rows?
+// (the bases, moduli and tables are prepare's fb_cand check)
+bool fbx_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
+  const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
+  if (!g || !g->fx_valid || !g->fx_host || g->sess.size() != count) return false;
+  const uint32_t s1l = g->fx_s1l, s3l = g->fx_s3l, zl = g->fx_zl;
+  auto at = [&](size_t off) { return reinterpret_cast<const uint32_t*>(g->fx_host + off); };
+  size_t zrow = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const fsdkr_collect_batch* b = bs + k;
+    const GaPre::Sess& x = g->sess[k];
+    const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
+    if (b->s1l != s1l || b->s3l != s3l || b->zl != zl || b->ped_lens || b->range_lens || x.n != ns ||
+        x.R != b->n_refresh || !b->pdl_s1 || !b->rp_s1 || !b->pdl_s3 || !b->rp_s2 || !b->ped_Z)
+      return false;
+    const size_t pb = x.pbase, cnt = (size_t)x.R * x.n, zr = (size_t)(b->n_refresh + b->n_join) * b->m_security;
+    if (!words_equal(at(g->fx_ps1) + pb * s1l, b->pdl_s1, cnt * s1l) ||
+        !words_equal(at(g->fx_as1) + pb * s1l, b->rp_s1, cnt * s1l) ||
+        !words_equal(at(g->fx_ps3) + pb * s3l, b->pdl_s3, cnt * s3l) ||
+        !words_equal(at(g->fx_as2) + pb * s3l, b->rp_s2, cnt * s3l) ||
+        !words_equal(at(g->fx_z) + zrow * zl, b->ped_Z, zr * zl))
+      return false;
+    zrow += zr;
+  }
+  return true;
 }
 
 
@@ -547,6 +731,14 @@ static int prestart_chal(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, 
   }
   (void)hipStreamWaitEvent(s2, g.ga_setup, 0);
   (void)hipStreamWaitEvent(s5, g.fb_setup, 0);   // N~_i constants (the table prestart's setup)
+  // FSDKR_CHAL_DEFER=1 (A/B): the two wide launches (J2, J5: ~2 900 waves) wait for the
+  // comb tables, whose short level launches otherwise find every wave slot taken
+  static const bool defer = getenv("FSDKR_CHAL_DEFER") && atoi(getenv("FSDKR_CHAL_DEFER")) == 1;
+  if (defer) {
+    hipEvent_t after = g.comb_done ? g.comb_done : g.fb_done;
+    (void)hipStreamWaitEvent(s2, after, 0);
+    (void)hipStreamWaitEvent(s5, after, 0);
+  }
   // the lanes launch() gives them: J2 at 16 lanes (one instance per wave for <= 1024
   // chains), J5 at 8 lanes (collect_launch.cpp)
   const uint32_t j2_group = nn == 128 ? (J2.size() <= 1024 ? kWaveGroup : J2.size() <= 16384 ? 16 : 8) : 8;
@@ -636,12 +828,18 @@ bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t coun
 int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t* n_out, uint32_t* P_out) {
   if (!c->ga_pre) c->ga_pre = new GaPre();
   GaPre& g = *reinterpret_cast<GaPre*>(c->ga_pre);
+  // an earlier prestart's work that no prepare consumed (a changed batch) may still
+  // run and read the buffers this one overwrites: wait for it (a consumed prestart
+  // finished before the pipeline that waited on it)
+  for (hipEvent_t e : {g.done, g.fb_done, g.comb_done, g.ck_done, g.tz_done, g.ch_ev[0], g.ch_ev[1], g.ch_ev[2], g.fx_done})
+    if (e) (void)hipEventSynchronize(e);
   g.valid = false;
   g.fb_valid = false;
   g.comb_pre.clear();
   g.ck_valid = false;
   g.tz_valid = false;
   g.ch_valid = false;
+  g.fx_valid = false;
   g.nn_rows = g.nt_rows = nullptr;
   *n_out = *P_out = 0;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
@@ -652,7 +850,8 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // a prepared plan that consumed the previous prestart reads its s^N rows and
   // fixed-base tables in place: this prestart overwrites (or reallocates) those
   // buffers, so the plan is dropped (a later launch reports "no prepared batch")
-  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit || running->ch_hit))
+  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit || running->ch_hit ||
+                  running->fx_hit))
     free_collect_plan(c);
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prestart: no batch");
@@ -847,6 +1046,8 @@ int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count)
   }
   GaPre& g = *gp;
   if (!g.fb_valid && (rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
+  static const bool fbx_off = getenv("FSDKR_FBX") && atoi(getenv("FSDKR_FBX")) == 0;   // (A/B)
+  if (!g.fx_valid && !fbx_off && (rc = prestart_fbx(c, bs, count, g))) return rc;
   if (!g.ck_valid && (rc = prestart_ck(c, bs, count, g))) return rc;
   return g.ch_valid ? FSDKR_OK : prestart_chal(c, bs, count, g);
 }

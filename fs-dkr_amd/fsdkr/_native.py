@@ -377,7 +377,7 @@ class Context:
         device work -> the pipeline's last kernel), -1 before any."""
         return float(self._lib.fsdkr_collect_last_span_ms(self._h))
 
-    REUSE = {"ga": 1, "tables": 2, "ck": 4, "tz": 8, "chal": 16}
+    REUSE = {"ga": 1, "tables": 2, "ck": 4, "tz": 8, "chal": 16, "fx": 32}
 
     def collect_reuse(self):
         """Names of the prestarted parts the last prepare reused (fsdkr_collect_reuse_mask)."""

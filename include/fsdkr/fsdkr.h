@@ -232,7 +232,8 @@ int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
  * while a launched batch is not finished.  Does not validate: a batch it cannot
  * start is left to prepare.  The fixed-base tables (recv_ntilde, recv_h1,
  * recv_h2, ped_T, ped_N and the exponent widths) and the correct-key job (ck_n,
- * ck_sigma) start too when present.  Called again with the same GA fields while
+ * ck_sigma) start too when present, and with the exponents themselves (pdl_s1,
+ * pdl_s3, rp_s1, rp_s2, ped_Z) every fixed-base exponentiation behind the tables.  Called again with the same GA fields while
  * those chains run (a caller that packed them first), it leaves GA running and
  * starts only the parts that are new.  Once the tables are started, a call that
  * finds the challenge jobs' fields (enc, commit, pdl_z, pdl_u1, pdl_u2, pdl_u3,
@@ -244,7 +245,7 @@ int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
 
 /* Which prestarted parts the last fsdkr_collect_prepare[_multi] reused (bit
  * mask): 1 GA chains, 2 fixed-base tables, 4 correct-key job, 8 ring-Pedersen
- * T^Z exponents, 16 challenge jobs.  0 before any prepare.  Diagnostic (tests
+ * T^Z exponents (multi-session), 16 challenge jobs, 32 fixed-base exponents.  0 before any prepare.  Diagnostic (tests
  * check that a changed batch is recomputed); the reference has no counterpart. */
 uint32_t fsdkr_collect_reuse_mask(const fsdkr_ctx* ctx);
 

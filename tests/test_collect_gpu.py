@@ -362,7 +362,7 @@ def _change(msgs, field):
     challenge jobs read (or hash)"""
     bad = copy.deepcopy(msgs)
     m = bad[1]
-    if field in ("u1", "u2", "u3", "z", "s1"):
+    if field in ("u1", "u2", "u3", "z", "s1", "s3"):
         p = m.pdl_proof_vec[2]
         val = ec.add(p.u1, ec.G) if field == "u1" else getattr(p, field) + 1
         m.pdl_proof_vec[2] = dataclasses.replace(p, **{field: val})
@@ -376,6 +376,9 @@ def _change(msgs, field):
     elif field == "Q":
         m.points_committed_vec = list(m.points_committed_vec)
         m.points_committed_vec[2] = ec.add(m.points_committed_vec[2], ec.G)
+    elif field == "rp_Z":
+        pf = m.ring_pedersen_proof
+        m.ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(z + (j == 5) for j, z in enumerate(pf.Z)))
     elif field == "vss":
         com = m.coefficients_committed_vec
         pts = list(com.commitments)
@@ -384,15 +387,19 @@ def _change(msgs, field):
     return bad
 
 
-@pytest.mark.parametrize("field", ["u1", "u2", "u3", "z", "s1", "alice_z", "alice_e", "c", "Q", "vss"])
+_FX_FIELDS = ("s1", "s3", "rp_Z")   # read by the prestarted fixed-base exponents (stage 1b)
+
+
+@pytest.mark.parametrize("field", ["u1", "u2", "u3", "z", "s1", "s3", "alice_z", "alice_e", "c", "Q", "vss", "rp_Z"])
 def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field):
-    """Stage 1c (CollectBatch.stage1c): the third fsdkr_collect_prestart starts the
+    """Stages 1b / 1c: the second fsdkr_collect_prestart also starts every
+    fixed-base exponent (h1^s1, h2^s3, T^Z behind the tables), the third the
     challenge jobs -- PDL challenges hashed on the host, c^e mod N^2 and z^e mod
     N~ with their inverses, pdl_u1, Feldman -- from the packed fields.  A prepare
     of the same batch reuses them (fsdkr_collect_reuse_mask) and its verdicts equal
     an un-prestarted run's.  A prepare of a batch with one field changed after the
-    prestart must recompute them: its verdicts equal that batch's own
-    un-prestarted run, which rejects the changed pair."""
+    prestart must recompute the parts that read it: its verdicts equal that
+    batch's own un-prestarted run, which rejects the changed proof."""
     from fsdkr.batch import CollectBatch
     from fsdkr.refresh import prestart
     keys, msgs, dks, _ = _dkr(1, 3, "prestart-chal")
@@ -401,7 +408,7 @@ def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field):
     prestart(gpu_ctx, a)
     a.complete()
     gpu_ctx.collect_prepare(a)
-    assert {"ga", "chal"} <= gpu_ctx.collect_reuse()
+    assert {"ga", "chal", "fx"} <= gpu_ctx.collect_reuse()
     v = gpu_ctx.collect_run(a)
     ref = gpu_ctx.verify_collect(CollectBatch(msgs, lk, [], 256, KB))
     assert _vt(v) == _vt(ref)
@@ -410,7 +417,11 @@ def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field):
     prestart(gpu_ctx, CollectBatch(msgs, lk, [], 256, KB, staged=True))
     b = CollectBatch(bad, lk, [], 256, KB)
     gpu_ctx.collect_prepare(b)
-    assert "chal" not in gpu_ctx.collect_reuse()
+    reused = gpu_ctx.collect_reuse()
+    if field in _FX_FIELDS:
+        assert "fx" not in reused
+    if field not in ("s3", "rp_Z"):   # (the challenge jobs read neither)
+        assert "chal" not in reused
     vb = gpu_ctx.collect_run(b)
     want = gpu_ctx.verify_collect(CollectBatch(bad, lk, [], 256, KB))
     assert _vt(vb) == _vt(want)
