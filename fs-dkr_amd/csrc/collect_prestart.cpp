@@ -733,7 +733,7 @@ static int prestart_chal(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, 
   (void)hipStreamWaitEvent(s5, g.fb_setup, 0);   // N~_i constants (the table prestart's setup)
   // FSDKR_CHAL_DEFER=1 (A/B): the two wide launches (J2, J5: ~2 900 waves) wait for the
   // comb tables, whose short level launches otherwise find every wave slot taken
-  static const bool defer = getenv("FSDKR_CHAL_DEFER") && atoi(getenv("FSDKR_CHAL_DEFER")) == 1;
+  const bool defer = getenv("FSDKR_CHAL_DEFER") && atoi(getenv("FSDKR_CHAL_DEFER")) == 1;
   if (defer) {
     hipEvent_t after = g.comb_done ? g.comb_done : g.fb_done;
     (void)hipStreamWaitEvent(s2, after, 0);
@@ -1046,8 +1046,10 @@ int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count)
   }
   GaPre& g = *gp;
   if (!g.fb_valid && (rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
-  static const bool fbx_off = getenv("FSDKR_FBX") && atoi(getenv("FSDKR_FBX")) == 0;   // (A/B)
-  if (!g.fx_valid && !fbx_off && (rc = prestart_fbx(c, bs, count, g))) return rc;
+  // FSDKR_FBX=1: also start the fixed-base exponents behind the tables (off by default:
+  // no gain at n = 64, interleaved A/B profiles/r05/r05c_ab_*; read per call)
+  const char* fbx_env = getenv("FSDKR_FBX");
+  if (!g.fx_valid && fbx_env && atoi(fbx_env) == 1 && (rc = prestart_fbx(c, bs, count, g))) return rc;
   if (!g.ck_valid && (rc = prestart_ck(c, bs, count, g))) return rc;
   return g.ch_valid ? FSDKR_OK : prestart_chal(c, bs, count, g);
 }

@@ -435,7 +435,7 @@ class CollectBatch:
         beside GA instead of after prepare.  True when it packed them (False: a
         field is wider than stage 1's width, or stage 1 was not split)."""
         if not self._stage1c or self._pending is None or self._ga is None or self._stage1b is not None or \
-                os.environ.get("FSDKR_STAGE1C") == "0":   # (A/B: the round-4 order)
+                os.environ.get("FSDKR_STAGE1C") != "1":   # opt-in: no gain at n = 64 (profiles/r05/r05c_ab_*)
             return False
         self._stage1c = False
         st = self._pending

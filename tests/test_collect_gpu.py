@@ -391,7 +391,7 @@ _FX_FIELDS = ("s1", "s3", "rp_Z")   # read by the prestarted fixed-base exponent
 
 
 @pytest.mark.parametrize("field", ["u1", "u2", "u3", "z", "s1", "s3", "alice_z", "alice_e", "c", "Q", "vss", "rp_Z"])
-def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field):
+def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field, monkeypatch):
     """Stages 1b / 1c: the second fsdkr_collect_prestart also starts every
     fixed-base exponent (h1^s1, h2^s3, T^Z behind the tables), the third the
     challenge jobs -- PDL challenges hashed on the host, c^e mod N^2 and z^e mod
@@ -402,6 +402,8 @@ def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field):
     batch's own un-prestarted run, which rejects the changed proof."""
     from fsdkr.batch import CollectBatch
     from fsdkr.refresh import prestart
+    monkeypatch.setenv("FSDKR_STAGE1C", "1")   # both stages are opt-in (profiles/r05/r05c_ab_*)
+    monkeypatch.setenv("FSDKR_FBX", "1")
     keys, msgs, dks, _ = _dkr(1, 3, "prestart-chal")
     lk = keys[0]
     a = CollectBatch(msgs, lk, [], 256, KB, staged=True)

@@ -139,13 +139,14 @@ def _dump(b, M):
 @pytest.mark.parametrize("big_ped", [False, True])
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("stage1c", [False, True])
-def test_staged_batch_equals_one_shot(big_ped, split, stage1c):
+def test_staged_batch_equals_one_shot(big_ped, split, stage1c, monkeypatch):
     """CollectBatch(staged=True) + complete() packs exactly what the one-shot
     constructor packs, also when stage 1's width is superseded (a 3000-bit PDL z,
     a stage-2 field, moves the batch to 3072-bit slots), when stage 1 is split
     (GA's fields, then stage1b()), and with stage1c() (the challenge jobs' fields:
     refused when a field is wider than stage 1's width)."""
     from fsdkr.batch import CollectBatch
+    monkeypatch.setenv("FSDKR_STAGE1C", "1")   # (opt-in stage)
     M = 8
     msgs, joins, lk = _fake_collect(M=M, big_ped=big_ped)
     one = CollectBatch(msgs, lk, joins, M, 2048)
