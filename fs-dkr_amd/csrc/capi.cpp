@@ -317,7 +317,7 @@ uint32_t choose_slide_window(uint32_t ebits) {
 
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st, const char* table_tag,
-                       uint32_t prio, uint32_t group, uint32_t desc_flags) {
+                       uint32_t prio, uint32_t group, uint32_t desc_flags, const SplitArgs* split) {
   if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
   // sliding windows: the 4096-bit group shapes, public exponents, wave-uniform (caller)
@@ -367,6 +367,30 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.ct = c->ct ? 1u : 0u;
   a.slide = slide ? 1u : 0u;
   a.out_idx = (desc_flags & kDescOutIdx) ? reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 4 * n4) : nullptr;
+  if (split && split->lo_bit) {   // head / tail of split chains: the slide shapes at the caller's lanes
+    if (!slide || grp != group || !(grp == 8 || grp == 16)) {
+      c->fail("split chains need the 8 / 16-lane sliding-window shapes (group %u)", grp);
+      return FSDKR_E_ARG;
+    }
+    const std::string base(table_tag);
+    a.lo_bit = split->lo_bit;
+    a.tail = split->tail ? 1u : 0u;
+    a.state = (uint32_t*)c->buf((base + "_state").c_str(), (size_t)count * KD * 4);
+    if (!a.state) {
+      c->fail("device allocation failed (split chain state)");
+      return FSDKR_E_OOM;
+    }
+    if (split->tail && split->d_desc2) {
+      a.base2_ptr = reinterpret_cast<const uint64_t*>(split->d_desc2);
+      a.exp2_ptr = reinterpret_cast<const uint64_t*>(split->d_desc2 + n8);
+      a.exp2_len = reinterpret_cast<const uint32_t*>(split->d_desc2 + 2 * n8);
+      a.table2 = (uint32_t*)c->buf((base + "_t2").c_str(), (size_t)count * 16 * KD * 4);
+      if (!a.table2) {
+        c->fail("device allocation failed (joint table)");
+        return FSDKR_E_OOM;
+      }
+    }
+  }
   const size_t tm = c->tbeg("modexp", st);
   int rc = c->hip_check(modexp(k32, a, st), "modexp launch");
   c->tend(tm, st);

@@ -193,10 +193,19 @@ void free_recover(Ctx* c);
 void free_ga_pre(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
                       uint32_t group = 0);
+// A split sliding-window launch (ModexpArgs lo_bit / tail, modexp.hip): the head
+// runs the exponent bits >= lo_bit, the tail (same descriptors, group and
+// table_tag) the rest, jointly with base2^exp2 when d_desc2 (per instance:
+// base2_ptr u64 | exp2_ptr u64 | exp2_len u32) is set.
+struct SplitArgs {
+  uint32_t lo_bit = 0;
+  bool tail = false;
+  const uint8_t* d_desc2 = nullptr;
+};
 int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, const uint8_t* d_desc,
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st = nullptr,
                        const char* table_tag = "mxtable", uint32_t prio = 0, uint32_t group = 0,
-                       uint32_t desc_flags = 0);
+                       uint32_t desc_flags = 0, const SplitArgs* split = nullptr);
 // group: kWideGroup prepares the KD = 160 constants of the 32-lane 4096-bit shape
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
                  uint32_t group = 0);

@@ -39,6 +39,19 @@ struct ModexpArgs {
                              // 2^(window-1) + 1 entries); the caller guarantees that the
                              // instances of every wave share their exponent (modexp_slide_kernel)
   const uint32_t* out_idx;   // [count] output row of each instance (nullptr: row = instance)
+  // Split sliding-window chains (slide shapes, QS): a HEAD launch (lo_bit > 0, tail
+  // = 0) runs the exponent bits >= lo_bit, always builds the odd-power table and
+  // writes its accumulator (the chain's Montgomery form) to state; the TAIL launch
+  // (tail = 1, same descriptors, table and w) resumes from state and runs the bits
+  // < lo_bit, jointly with base2^exp2 per instance (4-bit fixed windows over a
+  // 16-entry table in table2) when base2_ptr is set: out = base^exp * base2^exp2.
+  uint32_t lo_bit = 0;
+  uint32_t tail = 0;
+  uint32_t* state = nullptr;        // [count][KD]
+  const uint64_t* base2_ptr = nullptr;   // [count] K32 limbs, reduced
+  const uint64_t* exp2_ptr = nullptr;    // [count]
+  const uint32_t* exp2_len = nullptr;    // [count] limbs, exp2 < 2^lo_bit
+  uint32_t* table2 = nullptr;       // [count][16][KD]
 };
 
 int shape_digits(uint32_t k32);   // KD for a K32-limb modulus class (0 if unsupported)

@@ -312,9 +312,11 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs
   int top = 32 * exp_limbs - 1;
   while (top >= 0 && E[top >> 5] == 0) top = (top & ~31) - 1;   // skip zero limbs
   while (top >= 0 && !bit(top)) --top;
+  // a head launch (lo > 0) runs the bits >= lo only (the tail kernel the rest)
+  const int lo = (int)a.lo_bit;
   // the window that ends the run of bits at i (bit i set): lowest set bit jl >= i - w + 1
   auto window = [&](int i, int* jl) -> uint32_t {
-    int j = max(i - (int)w + 1, 0);
+    int j = max(i - (int)w + 1, lo);
     while (!bit(j)) ++j;
     uint32_t d = 0;
     for (int k = i; k >= j; --k) d = (d << 1) | bit(k);
@@ -345,7 +347,7 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs
       // of the general step between them (16 lanes: ~210 -> 90 VALU
       // instructions per squaring outside its cycle loop)
       if (pend_sq == 0 && pend_mul < 0)
-        while (i >= 0 && !bit(i)) {
+        while (i >= lo && !bit(i)) {
           ++pend_sq;
           --i;
         }
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs
     } else if (pend_mul >= 0) {
       src = T + (size_t)pend_mul * KD;
       pend_mul = -1;
-    } else if (i < 0) {
+    } else if (i < lo) {
       break;
     } else if (!bit(i)) {
       sq = true;
@@ -410,11 +412,20 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs
       if (++jt == tw) phase = 3;
     }
     if (phase == 3 && i == top) {   // the first window: its odd power, no squarings of 1
-      int jl;
-      const uint32_t d = window(i, &jl);
-      load(T + (size_t)(d >> 1) * KD);
-      i = jl - 1;
+      if (top >= lo) {
+        int jl;
+        const uint32_t d = window(i, &jl);
+        load(T + (size_t)(d >> 1) * KD);
+        i = jl - 1;
+      } else {   // a head whose bits are all below lo: 1 (the table is built for the tail)
+        load(C + KD);
+      }
     }
+  }
+  if (lo) {   // head: hand the accumulator (Montgomery form mod the chain's modulus) to the tail
+#pragma unroll
+    for (int j = 0; j < L; ++j) a.state[(size_t)inst * KD + g * L + j] = acc[j];
+    return;
   }
   // exit: acc * 1 / R, modulo N itself for quotient-scaled chains
   if constexpr (QS) {
@@ -422,6 +433,132 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs
     for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
     M.ninv = C0[3 * KD];
   }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
+  __builtin_amdgcn_wave_barrier();
+  M.mul(acc, acc, stream);
+  M.carry_exact(acc);
+  M.sub_if_ge(acc);
+  __builtin_amdgcn_wave_barrier();
+  lds_put<KD, G>(stream, acc, g);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* O = a.out + (size_t)(a.out_idx ? a.out_idx[inst] : inst) * K32;
+  constexpr int LO = K32 / G;
+#pragma unroll
+  for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
+}
+
+// The tail of a split chain (ModexpArgs lo_bit / tail): resumes the head's
+// accumulator x^(E >> lo) and runs the exponent bits below lo with the head's
+// sliding windows (wave-uniform E, the head's odd-power table), and with base2 set
+// multiplies in base2^exp2 along the same squarings: 4-bit fixed windows of the
+// instance's own exp2 (< 2^lo) over a 16-entry table base2^0..15.  GA's joint tail
+// (collect_prepare.cpp): s2^N * c^-e_pdl and s^N * c^-e_A mod N^2 in one chain,
+// base2 = c^-1, instead of a separate 256-bit chain c^e per proof and its inverse
+// (zk_pdl_with_slack.rs:136-142 via commitment_unknown_order :170-188,
+// range_proofs.rs:140-148).  Quotient-scaled rows, as the head.  Exact results.
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(BLOCK, 2) void modexp_tail_kernel(const ModexpArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int IPB = BLOCK / G;
+  constexpr int STRIDE = cons_stride(KD);
+  static_assert(scaled_ok(KD, K32), "quotient-scaled chains: N' within R/4");
+  __shared__ uint32_t lds[IPB * KD];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * (blockDim.x / G) + li;
+  if (inst >= a.count) return;
+  if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (a.prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
+  uint32_t* stream = lds + li * KD;
+  const uint32_t* C0 = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  const uint32_t* C = C0 + cons_scaled(KD);
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
+  M.ninv = C[3 * KD];
+  const uint32_t w = a.window, tw = 1u << (w - 1);
+  const uint32_t* T = a.table + (size_t)inst * (tw + 1) * KD;
+  const uint64_t ea = a.exp_ptr[inst];
+  const uint32_t* E = reinterpret_cast<const uint32_t*>(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(ea >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ea));
+  const int exp_limbs = __builtin_amdgcn_readfirstlane((int)a.exp_len[inst]);
+  auto bit = [&](int i) -> uint32_t { return (i >> 5) < exp_limbs ? (E[i >> 5] >> (i & 31)) & 1u : 0u; };
+  const int lo = (int)a.lo_bit;
+  uint32_t acc[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) acc[j] = a.state[(size_t)inst * KD + g * L + j];
+  auto put_row = [&](const uint32_t* row) {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < L; ++j) stream[g * L + j] = row[g * L + j];
+    __builtin_amdgcn_wave_barrier();
+  };
+  // the joint base's table T2[u] = base2^u (Montgomery form), u < 16
+  const bool joint = a.base2_ptr != nullptr;
+  uint32_t* T2 = joint ? a.table2 + (size_t)inst * 16 * KD : nullptr;
+  const uint32_t* E2 = nullptr;
+  uint32_t e2len = 0;
+  if (joint) {
+    E2 = reinterpret_cast<const uint32_t*>(a.base2_ptr ? a.exp2_ptr[inst] : 0);
+    e2len = a.exp2_len[inst];
+    const uint32_t* B2 = reinterpret_cast<const uint32_t*>(a.base2_ptr[inst]);
+    uint32_t y[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      y[j] = digit_of(B2, K32, g * L + j);
+      T2[g * L + j] = C[KD + g * L + j];   // T2[0] = 1 (R mod N')
+    }
+    put_row(C + 2 * KD);                   // R^2: y -> y R
+    M.mul_s(y, y, stream);
+#pragma unroll
+    for (int j = 0; j < L; ++j) T2[KD + g * L + j] = y[j];
+    __builtin_amdgcn_wave_barrier();
+    lds_put<KD, G>(stream, y, g);          // T2[1] streamed for the powers
+    __builtin_amdgcn_wave_barrier();
+    for (int u = 2; u < 16; ++u) {
+      M.mul_s(y, y, stream);
+#pragma unroll
+      for (int j = 0; j < L; ++j) T2[(size_t)u * KD + g * L + j] = y[j];
+    }
+  }
+  // bits lo-1 .. 0: square; the sliding window of E that ends at i multiplies
+  // T[d >> 1] in; every 4th bit the instance's exp2 digit multiplies T2[digit] in
+  int pend_at = -1;
+  uint32_t pend_d = 0, ew = 0;
+  for (int i = lo - 1; i >= 0; --i) {
+    if ((i & 31) == 31 && joint) ew = ((uint32_t)(i >> 5) < e2len) ? E2[i >> 5] : 0u;
+    if (pend_at < 0 && bit(i)) {   // a window starts: its lowest set bit jl >= max(i - w + 1, 0)
+      int j = max(i - (int)w + 1, 0);
+      while (!bit(j)) ++j;
+      uint32_t d = 0;
+      for (int k = i; k >= j; --k) d = (d << 1) | bit(k);
+      pend_at = j;
+      pend_d = d;
+    }
+    __builtin_amdgcn_wave_barrier();
+    lds_put<KD, G>(stream, acc, g);
+    __builtin_amdgcn_wave_barrier();
+    M.sqr_s(acc, acc, stream);
+    if (i == pend_at) {
+      put_row(T + (size_t)(pend_d >> 1) * KD);
+      M.mul_s(acc, acc, stream);
+      pend_at = -1;
+    }
+    if (joint && (i & 3) == 0) {
+      put_row(T2 + (size_t)((ew >> (i & 31)) & 15u) * KD);
+      M.mul_s(acc, acc, stream);
+    }
+  }
+  // exit: acc * 1 / R modulo N itself
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
+  M.ninv = C0[3 * KD];
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
@@ -563,6 +700,16 @@ static hipError_t launch_modexp_slide(const ModexpArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int KD, int G, int K32>
+static hipError_t launch_modexp_tail(const ModexpArgs& a, hipStream_t st) {
+  const uint32_t bs = block_threads(a.count * G);
+  const uint32_t ipb = bs / G;
+  const uint32_t blocks = (a.count + ipb - 1) / ipb;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((modexp_tail_kernel<KD, G, K32>), dim3(blocks), dim3(bs), 0, st, a);
+  return hipGetLastError();
+}
+
 template <int KR, int L, int K32>
 static hipError_t launch_modexp_wave(const ModexpArgs& a, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
@@ -657,6 +804,12 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
   const bool qs = qs_env == 1;
   if (a.slide) {   // shared exponent per wave: the 4096-bit shapes of GA
     if (k32 != 128 || a.ct || a.group == kWideGroup || a.group == kWaveGroup) return hipErrorInvalidValue;
+    if (a.lo_bit) {   // split chains: quotient-scaled 8 / 16-lane shapes only (the head's table layout)
+      if (!qs || !(a.group == 8 || a.group == 16)) return hipErrorInvalidValue;
+      if (a.tail)
+        return a.group == 16 ? launch_modexp_tail<144, 16, 128>(a, st) : launch_modexp_tail<144, 8, 128>(a, st);
+      return a.group == 16 ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, true>(a, st);
+    }
     switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
       case 16: return qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st);
       case 8: return qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st);

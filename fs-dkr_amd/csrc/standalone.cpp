@@ -11,6 +11,7 @@
 #include <cstring>
 #include <vector>
 
+#include "collect.hpp"
 #include "ctx.hpp"
 #include "fbjob.hpp"
 #include "fsdkr/fsdkr.h"
@@ -239,6 +240,96 @@ int fsdkr_ring_pedersen_verify(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, uint
     verdict[m] = mode[m] == 2 ? 2 : ped_verdict(e, M, panic[m]);
   }
   return FSDKR_OK;
+}
+
+// out[i] = base[i]^E[mod_idx[i]] * base2[i]^exp2[i] mod N[mod_idx[i]] through the
+// split chains of collect()'s GA (head over E's bits >= 256, joint tail), for
+// parity tests of that path (modexp.hip modexp_tail_kernel).
+int fsdkr_modexp_joint_batch(fsdkr_ctx* ctx, uint32_t count, const uint32_t* base, const uint32_t* base2,
+                             const uint32_t* exp2, const uint32_t* mod_idx, const uint32_t* mods,
+                             const uint32_t* mod_exp, uint32_t exp_limbs, uint32_t n_mod, uint32_t* out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  constexpr uint32_t K = 128, E2L = 8, LO = 256;
+  if (!base || !base2 || !exp2 || !mod_idx || !mods || !mod_exp || !out || !n_mod || !exp_limbs) {
+    c->fail("fsdkr_modexp_joint_batch: null pointer or empty table");
+    return FSDKR_E_ARG;
+  }
+  uint32_t ebits = 1;
+  for (uint32_t m = 0; m < n_mod; ++m) {
+    if ((mods[(size_t)m * K] & 1u) == 0) {
+      c->fail("fsdkr_modexp_joint_batch: modulus %u is even", m);
+      return FSDKR_E_ARG;
+    }
+    ebits = std::max(ebits, bit_len(mod_exp + (size_t)m * exp_limbs, exp_limbs));
+  }
+  for (uint32_t i = 0; i < count; ++i)
+    if (mod_idx[i] >= n_mod) {
+      c->fail("fsdkr_modexp_joint_batch: mod_idx[%u] out of range", i);
+      return FSDKR_E_ARG;
+    }
+  const uint32_t group = c->modexp_group == 8 ? 8u : 16u, per_wave = 64 / group;
+  const size_t o_b = 0, o_b2 = al256((size_t)count * K * 4), o_e2 = o_b2 + al256((size_t)count * K * 4),
+               o_m = o_e2 + al256((size_t)count * E2L * 4), o_me = o_m + al256((size_t)n_mod * K * 4),
+               o_out = o_me + al256((size_t)n_mod * exp_limbs * 4), o_desc = o_out + al256(((size_t)count + 1) * K * 4);
+  const size_t cap = (size_t)count + (size_t)n_mod * per_wave;   // instances + pads
+  const size_t o_desc2 = o_desc + al256(cap * 36), total = o_desc2 + al256(cap * 20);
+  uint8_t* dev = (uint8_t*)c->buf("mxj", total);
+  if (!dev) {
+    c->fail("fsdkr_modexp_joint_batch: device allocation failed");
+    return FSDKR_E_OOM;
+  }
+  auto DI = [&](size_t o) { return (uint64_t)(uintptr_t)(dev + o); };
+  ModexpJob J;
+  J.k32 = K;
+  for (uint32_t i = 0; i < count; ++i)
+    J.add(DI(o_b + (size_t)i * K * 4), K, DI(o_me + (size_t)mod_idx[i] * exp_limbs * 4), exp_limbs, ebits, mod_idx[i]);
+  const bool aligned = group_by_exponent(J, per_wave, count);
+  if (!aligned) {
+    c->fail("fsdkr_modexp_joint_batch: instances not wave-uniform");
+    return FSDKR_E_ARG;
+  }
+  std::vector<uint8_t> desc;
+  J.pack(desc);
+  const size_t n = J.size();
+  std::vector<uint8_t> desc2(n * 20, 0);
+  auto* b2p = reinterpret_cast<uint64_t*>(desc2.data());
+  auto* e2p = reinterpret_cast<uint64_t*>(desc2.data() + n * 8);
+  auto* e2l = reinterpret_cast<uint32_t*>(desc2.data() + n * 16);
+  for (size_t k = 0; k < n; ++k) {
+    const uint32_t r = J.out_idx[k];   // the pads write row `count`
+    const uint32_t src = r < count ? r : 0u;
+    b2p[k] = DI(o_b2 + (size_t)src * K * 4);
+    e2p[k] = DI(o_e2 + (size_t)src * E2L * 4);
+    e2l[k] = r < count ? E2L : 0u;
+  }
+  int rc;
+  auto up = [&](size_t o, const void* src, size_t bytes) {
+    return c->hip_check(hipMemcpyAsync(dev + o, src, bytes, hipMemcpyHostToDevice, c->stream), "H2D joint");
+  };
+  if ((rc = up(o_b, base, (size_t)count * K * 4)) || (rc = up(o_b2, base2, (size_t)count * K * 4)) ||
+      (rc = up(o_e2, exp2, (size_t)count * E2L * 4)) || (rc = up(o_m, mods, (size_t)n_mod * K * 4)) ||
+      (rc = up(o_me, mod_exp, (size_t)n_mod * exp_limbs * 4)) || (rc = up(o_desc, desc.data(), desc.size())) ||
+      (rc = up(o_desc2, desc2.data(), desc2.size())))
+    return rc;
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, K, reinterpret_cast<const uint32_t*>(dev + o_m), n_mod, &cons, "joint"))) return rc;
+  const uint32_t flags = ga_desc_flags(true, group);
+  SplitArgs head;
+  head.lo_bit = LO;
+  SplitArgs tail = head;
+  tail.tail = true;
+  tail.d_desc2 = dev + o_desc2;
+  uint32_t* d_out = reinterpret_cast<uint32_t*>(dev + o_out);
+  if ((rc = launch_modexp_desc(c, K, (uint32_t)n, ebits, dev + o_desc, cons, d_out, c->stream, "mxt_joint", 0, group,
+                               flags, &head)) ||
+      (rc = launch_modexp_desc(c, K, (uint32_t)n, ebits, dev + o_desc, cons, d_out, c->stream, "mxt_joint", 0, group,
+                               flags, &tail)))
+    return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(out, d_out, (size_t)count * K * 4, hipMemcpyDeviceToHost, c->stream), "D2H")))
+    return rc;
+  return c->sync();
 }
 
 }  // extern "C"

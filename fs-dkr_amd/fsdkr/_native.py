@@ -122,6 +122,9 @@ def lib():
                                      ctypes.c_uint32, u32p]
     L.fsdkr_modexp_batch.restype = ctypes.c_int
     L.fsdkr_modexp_batch_ct.argtypes = L.fsdkr_modexp_batch.argtypes
+    L.fsdkr_modexp_joint_batch.argtypes = [vp, ctypes.c_uint32, u32p, u32p, u32p, u32p, u32p, u32p, ctypes.c_uint32,
+                                           ctypes.c_uint32, u32p]
+    L.fsdkr_modexp_joint_batch.restype = ctypes.c_int
     L.fsdkr_modexp_batch_ct.restype = ctypes.c_int
     L.fsdkr_modexp_batch_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
                                             ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp]
@@ -272,6 +275,25 @@ class Context:
         O = np.zeros((count, mod_limbs), dtype=np.uint32)
         fn = self._lib.fsdkr_modexp_batch_ct if secret else self._lib.fsdkr_modexp_batch
         self.check(fn(self._h, mod_limbs, count, _ptr(B), _ptr(E), exp_limbs, _ptr(I), _ptr(Mo), len(mods), _ptr(O)))
+        return limbs_to_ints(O)
+
+    def modexp_joint_batch(self, bases, bases2, exps2, mods, mod_exps, mod_idx):
+        """[bases[i] ^ mod_exps[k] * bases2[i] ^ exps2[i] mod mods[k]], k = mod_idx[i],
+        4096-bit moduli, exps2 < 2^256, bases2 reduced: collect()'s split GA chains
+        (fsdkr_modexp_joint_batch)."""
+        count = len(bases)
+        if count == 0:
+            return []
+        exp_limbs = max(1, (max(e.bit_length() for e in mod_exps) + 31) // 32)
+        B = ints_to_limbs(bases, 128)
+        B2 = ints_to_limbs(bases2, 128)
+        E2 = ints_to_limbs(exps2, 8)
+        Mo = ints_to_limbs(mods, 128)
+        ME = ints_to_limbs(mod_exps, exp_limbs)
+        I = np.ascontiguousarray(np.asarray(mod_idx, dtype=np.uint32))
+        O = np.zeros((count, 128), dtype=np.uint32)
+        self.check(self._lib.fsdkr_modexp_joint_batch(self._h, count, _ptr(B), _ptr(B2), _ptr(E2), _ptr(I), _ptr(Mo),
+                                                      _ptr(ME), exp_limbs, len(mods), _ptr(O)))
         return limbs_to_ints(O)
 
     def fixed_base_modexp(self, bases, base_mod_idx, mods, base_idx, exps, mod_limbs):

@@ -243,6 +243,16 @@ int fsdkr_collect_finish(fsdkr_ctx* ctx, fsdkr_verdicts* out);
  * reuses each started part only if every row that part read is equal. */
 int fsdkr_collect_prestart(fsdkr_ctx* ctx, const fsdkr_collect_batch* batch);
 
+/* out[i] = base[i]^E[mod_idx[i]] * base2[i]^exp2[i] mod N[mod_idx[i]] (4096-bit
+ * moduli, 128 limbs; E: one exponent per modulus, exp_limbs limbs; exp2: 8 limbs,
+ * below 2^256; base2 reduced) through collect()'s split GA chains: a head over E's
+ * bits >= 256 and a joint tail, which is how collect() computes s2^N c^-e mod N^2
+ * (zk_pdl_with_slack.rs:136-142) and s^N c^-e mod N^2 (range_proofs.rs:140-148)
+ * with base2 = c^-1.  Parity tests of that path; odd moduli. */
+int fsdkr_modexp_joint_batch(fsdkr_ctx* ctx, uint32_t count, const uint32_t* base, const uint32_t* base2,
+                             const uint32_t* exp2, const uint32_t* mod_idx, const uint32_t* mods,
+                             const uint32_t* mod_exp, uint32_t exp_limbs, uint32_t n_mod, uint32_t* out);
+
 /* Which prestarted parts the last fsdkr_collect_prepare[_multi] reused (bit
  * mask): 1 GA chains, 2 fixed-base tables, 4 correct-key job, 8 ring-Pedersen
  * T^Z exponents (multi-session), 16 challenge jobs, 32 fixed-base exponents.  0 before any prepare.  Diagnostic (tests

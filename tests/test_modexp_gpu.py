@@ -120,3 +120,34 @@ def test_modexp_regular_access_equals_plain(gpu_ctx, limbs):
     got = gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs, secret=True)
     assert got == [pow(b, e, mods[i]) for b, e, i in zip(bases, exps, idx)]
     assert got == gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs)
+
+
+@pytest.mark.parametrize("group", [8, 16])
+def test_modexp_joint_split_chains(gpu_ctx, group):
+    """collect()'s GA chains split into a head (the exponent's bits >= 256) and a
+    joint tail that multiplies base2^exp2 in along the tail's squarings
+    (fsdkr_modexp_joint_batch): bit-exact against Python for s^N * (c^-1)^e mod N^2
+    shapes, exponents N shared per modulus (waves padded), exp2 = 0 / 1 / full 256
+    bits, base2 = 1, bases above N^2, and exponents shorter than the split point
+    (E < 2^256, E = 0: the head only builds the table or nothing)."""
+    rnd = random.Random(4242 + group)
+    Ns = [_odd(rnd, 2048) for _ in range(4)]
+    mods = [n * n for n in Ns]
+    exps = [Ns[0], Ns[1], Ns[2], rnd.getrandbits(200) | 1]   # the last one below 2^256
+    mods.append(_odd(rnd, 4090))
+    exps.append(0)
+    count = 150
+    idx = [rnd.randrange(len(mods)) for _ in range(count)]
+    bases = [rnd.getrandbits(4096) for _ in range(count)]
+    bases2 = [rnd.randrange(mods[i]) for i in idx]
+    e2 = [rnd.getrandbits(256) for _ in range(count)]
+    e2[:6] = [0, 1, 15, 16, (1 << 256) - 1, 1 << 255]
+    bases2[6] = 1
+    gpu_ctx.set_modexp_group(group)
+    try:
+        got = gpu_ctx.modexp_joint_batch(bases, bases2, e2, mods, exps, idx)
+    finally:
+        gpu_ctx.set_modexp_group(0)
+    want = [pow(b, exps[i], mods[i]) * pow(y, f, mods[i]) % mods[i] for b, y, f, i in zip(bases, bases2, e2, idx)]
+    bad = [k for k in range(count) if got[k] != want[k]]
+    assert not bad, f"G={group}: {len(bad)} mismatches, first at {bad[0]}"
