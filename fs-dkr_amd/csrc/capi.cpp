@@ -368,8 +368,8 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.slide = slide ? 1u : 0u;
   a.out_idx = (desc_flags & kDescOutIdx) ? reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 4 * n4) : nullptr;
   if (split && split->lo_bit) {   // head / tail of split chains: the slide shapes at the caller's lanes
-    if (!slide || grp != group || !(grp == 8 || grp == 16)) {
-      c->fail("split chains need the 8 / 16-lane sliding-window shapes (group %u)", grp);
+    if (!slide || grp != group || !(grp == 4 || grp == 8 || grp == 16)) {
+      c->fail("split chains need the 4 / 8 / 16-lane sliding-window shapes (group %u)", grp);
       return FSDKR_E_ARG;
     }
     const std::string base(table_tag);

@@ -329,6 +329,17 @@ struct CollectPlan {
   // prestart (ch_hit): the pipeline waits for ch_ev before its equalities
   bool ch_hit = false;
   hipEvent_t ch_ev[3] = {};
+  // GA's joint tail (ga_split_ok): J2 is not run; GA computes s2^N c^-e_pdl | s^N c^-e_A,
+  // the nn inverse is c's own (unit flags of c); job slot 2 then holds J9
+  bool joint = false;
+  size_t d_desc2 = 0;                  // the tail's descriptor block (in the image)
+  struct GaTail {                      // a split prestarted head's launch (ga_hit && joint)
+    const uint8_t* desc = nullptr;
+    const uint32_t* cons = nullptr;
+    uint32_t* out = nullptr;
+    uint32_t count = 0, bits = 0, group = 0, flags = 0;
+  } ga_tail;
+  std::vector<uint8_t> ae_zero;        // Alice e == 0: c^0 = 1 whatever c is
   // the fixed-base exponents computed by the prestart (fx_hit): J3 / J4 / RP rows there
   bool fx_hit = false;
   hipEvent_t fx_done = nullptr;
@@ -359,6 +370,12 @@ struct GaPre {
   std::vector<Sess> sess;
   uint32_t* out = nullptr;               // [2P][nn]: J1 instance order (s2^N rows, then s^N rows)
   hipEvent_t done = nullptr;
+  // split GA (ga_split_ok): the prestart ran the HEAD; prepare launches the joint tail
+  // with these descriptors (ga_rows: out_idx of every instance, pads = 2P)
+  bool split = false;
+  uint32_t ga_group = 0, ga_flags = 0, ga_count = 0, ga_bits = 0;
+  const uint8_t* ga_desc = nullptr;
+  std::vector<uint32_t> ga_rows;
   hipEvent_t ga_setup = nullptr;   // GA's Montgomery constants ready (before its chains)
   const uint32_t* cons = nullptr;   // those constants (KD 160 when `wide`, else the width's KD)
   bool wide = false;
@@ -546,6 +563,21 @@ inline uint32_t ga_desc_flags(bool aligned_for, uint32_t group) {
   const bool slide_shape = group == 4 || group == 8 || group == 16;
   return kDescOutIdx | ((aligned_for && slide_shape) ? kDescSlide : 0u);
 }
+
+// GA's joint tail (modexp.hip modexp_tail_kernel): the chains s2^N | s^N mod N^2 run
+// as a head over N's bits >= kGaSplit and a tail that multiplies c^-e_pdl | c^-e_A in
+// along its squarings (e < 2^256), so no separate c^e chain (J2) runs.  For the
+// sliding-window GA shapes (4096-bit, 4 / 8 / 16 lanes); FSDKR_JOINT=0 keeps J2
+// (A/B).  Read per call.
+constexpr uint32_t kGaSplit = 256;
+inline bool ga_split_ok(uint32_t nn, uint32_t group, uint32_t flags) {
+  const char* j = getenv("FSDKR_JOINT");
+  const char* s = getenv("FSDKR_SLIDE");
+  if ((j && atoi(j) == 0) || (s && atoi(s) == 0)) return false;
+  return nn == 128 && (flags & kDescSlide) && (flags & kDescOutIdx) && (group == 4 || group == 8 || group == 16);
+}
+// the tail's per-instance descriptor block: base2_ptr u64 | exp2_ptr u64 | exp2_len u32
+constexpr size_t kTailDescBytes = 20;
 
 // collect_prestart.cpp
 int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t* n_out, uint32_t* P_out);

@@ -98,6 +98,16 @@ int collect_launch_impl(Ctx* c) {
   // (1) chains that need only the inputs and the moduli constants start at once
   hipEvent_t consts_ready;
   if ((rc = fork(st, &consts_ready))) return rc;
+  hipEvent_t inv_done = nullptr;
+  if (pl.joint) {   // c^-1 mod N^2 of every pair: c's unit flag, and the joint tail's base2
+    hipStream_t s2 = c->side_stream(2);
+    InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
+                  PX(pl.x_unn), nullptr, pl.n_inv_nn};
+    c->mark("inverse", true, s2);
+    rc = c->hip_check(launch_inverse(nn, a, s2), "inverse c");
+    c->mark("inverse", false, s2);
+    if (rc || (rc = fork(s2, &inv_done))) return rc;
+  }
   {  // GA: s2^N, s^N mod N^2 (4096-bit, 2048-bit exponents): the longest chains
     hipStream_t ss = c->side_stream(0);
     (void)hipStreamWaitEvent(ss, consts_ready, 0);
@@ -106,7 +116,31 @@ int collect_launch_impl(Ctx* c) {
     // priority level below it (8-way shard: 33.4 -> 31.7 ms, tools/ab_hwq.sh)
     if (ga_group >= 16) prio[0] = 2;
     const uint32_t* cga = (ga_group == kWideGroup) ? cons_nn_w : cons_nn;
-    if ((rc = launch_group(0, ss, prio[0], ga_group, cga)) || (rc = join_later(ss))) return rc;
+    if (pl.joint) {
+      SplitArgs head, tail;
+      head.lo_bit = tail.lo_bit = kGaSplit;
+      tail.tail = true;
+      tail.d_desc2 = dev + pl.d_desc2;
+      if (pl.ga_hit) {   // the prestarted head runs on this stream: its tail follows c^-1
+        const CollectPlan::GaTail& t = pl.ga_tail;
+        (void)hipStreamWaitEvent(ss, inv_done, 0);
+        if ((rc = launch_modexp_desc(c, nn, t.count, t.bits, t.desc, t.cons, t.out, ss, "mxt_GApre", 2, t.group, t.flags,
+                                     &tail)) ||
+            (rc = c->hip_check(hipEventRecord(pl.ga_done, ss), "event record")))   // the s^N rows: after the tail
+          return rc;
+      } else if (pl.jcount[0]) {
+        if ((rc = launch_modexp_desc(c, nn, pl.jcount[0], pl.jbits[0], dev + pl.d_J[0], cga, PX(pl.x_J[0]), ss, "mxt_GA",
+                                     prio[0], ga_group, pl.jflags[0], &head)))
+          return rc;
+        (void)hipStreamWaitEvent(ss, inv_done, 0);
+        if ((rc = launch_modexp_desc(c, nn, pl.jcount[0], pl.jbits[0], dev + pl.d_J[0], cga, PX(pl.x_J[0]), ss, "mxt_GA",
+                                     prio[0], ga_group, pl.jflags[0], &tail)))
+          return rc;
+      }
+      if ((rc = join_later(ss))) return rc;
+    } else if ((rc = launch_group(0, ss, prio[0], ga_group, cga)) || (rc = join_later(ss))) {
+      return rc;
+    }
   }
   {  // FB: h1, h2, T fixed-base tables -> schedules -> exponents
     hipStream_t ss = c->side_stream(1);
@@ -175,8 +209,9 @@ int collect_launch_impl(Ctx* c) {
   {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses (prestarted on a chal hit)
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
-    if ((rc = launch_group(2, ss, 0, j2_group, cons_nn))) return rc;
-    if (!pl.ch_hit) {
+    // (joint: slot 2 holds J9, (N+1)^s1 for s1 >= N, at the generic lane count)
+    if ((rc = launch_group(2, ss, 0, pl.joint ? 0u : j2_group, cons_nn))) return rc;
+    if (!pl.ch_hit && !pl.joint) {
       InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
                     PX(pl.x_unn), nullptr, pl.n_inv_nn};
       c->mark("inverse", true, ss);
@@ -197,6 +232,7 @@ int collect_launch_impl(Ctx* c) {
   }
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
+  if (inv_done) (void)hipEventDestroy(inv_done);
   if (!pl.ch_hit) {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses (else prestarted)
     hipStream_t js = st;
     if ((rc = launch_group(3, js, prio[3], j5_group, cons_nl))) return rc;
@@ -301,6 +337,7 @@ int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
     if (hipEventElapsedTime(&c->span_ms, c->span_beg, c->span_end) != hipSuccess) c->span_ms = -1.0f;
   }
   // PDL unit test of c: c^eA witnesses it unless eA == 0 / the Alice proof was rejected early
+  // (joint: unn is c's own unit flag)
   std::vector<uint32_t> unit_c_pdl(unn.begin(), unn.begin() + P);
   for (size_t k = 0; k < pl.cpdl_extra.size(); ++k) unit_c_pdl[pl.cpdl_extra[k]] = unn[P + k];
   for (uint32_t s = 0; s < count; ++s) {
@@ -318,8 +355,10 @@ int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
       if (panic) bits |= 8;
       v.pdl[lp] = bits;
       v.feldman[lp] = fel[p];
-      // Alice: pre-checks, invertibility of z^e and c^e, transcript hash (range_proofs.rs:125-163)
-      v.range[lp] = (rng[p] && unn[p] && uzA[p]) ? 1 : 0;
+      // Alice: pre-checks, invertibility of z^e and c^e, transcript hash (range_proofs.rs:125-163);
+      // joint: c^e is a unit iff e == 0 or c is
+      const bool unit_ce = pl.joint ? (pl.ae_zero[p] || unn[p]) : unn[p] != 0;
+      v.range[lp] = (rng[p] && unit_ce && uzA[p]) ? 1 : 0;
     }
     for (uint32_t lm = 0; lm < x.Mt; ++lm) {
       const uint32_t m = x.mbase + lm;

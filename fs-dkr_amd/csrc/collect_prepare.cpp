@@ -107,7 +107,17 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   }
   // prestarted challenge jobs of this batch (stage 1c): J2, J5, their inverses,
   // pdl_u1 and Feldman are not launched again, the PDL challenges not hashed again
-  pl.ch_hit = chal_pre_matches(c, bs, count) && gpre->ch_P == P;
+  // GA's joint tail: the prestart ran the split head (gpre->split), or prepare's own GA
+  // (J1 alone, padded to whole waves) takes a sliding-window shape; the challenge
+  // prestart's c^e rows are then not used
+  {
+    const uint32_t g0 = ga_lanes(2 * P, nn);
+    pl.joint = pl.ga_hit ? gpre->split : ga_split_ok(nn, g0, ga_desc_flags(true, g0));
+  }
+  pl.ch_hit = !pl.joint && chal_pre_matches(c, bs, count) && gpre->ch_P == P;
+  if (pl.joint && pl.ga_hit)
+    pl.ga_tail = CollectPlan::GaTail{gpre->ga_desc, gpre->cons, gpre->out, gpre->ga_count, gpre->ga_bits, gpre->ga_group,
+                                     gpre->ga_flags};
   if (pl.ch_hit) {
     for (int k = 0; k < 3; ++k) pl.ch_ev[k] = gpre->ch_ev[k];
     gpre->ch_valid = false;   // consumed
@@ -127,7 +137,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     }
   });
   const hbn::Limbs& q3 = q_cubed();
-  std::vector<uint8_t> alice_pre(P), pdl_small(P);
+  std::vector<uint8_t> alice_pre(P), pdl_small(P), big_c(P);
   std::vector<uint32_t> ae_bits(P);
   struct Maxes {
     uint32_t s1 = 1, s3 = 1, as1 = 1, as2 = 1, ae = 1;
@@ -150,6 +160,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       const fsdkr_collect_batch* b = x.b;
       const size_t lp = p - x.pbase;
       if (hash && !pdl_challenge(sha, b, lp, EPDL.data() + p * 8)) sha_fail = true;
+      // a ciphertext at or above N^2 (GMP reduces it; the joint tail's inverse needs it reduced)
+      big_c[p] = hbn::cmp_raw(b->enc + lp * 2 * b->nl, 2 * b->nl, NN.data() + (size_t)recv_of_pair[p] * nn, nn) >= 0;
       const uint32_t* Np = b->recv_n + (size_t)(lp % x.n) * b->nl;
       const uint32_t* s1 = b->pdl_s1 + lp * b->s1l;
       // s1 < N -> (N+1)^s1 mod N^2 = 1 + s1*N  (binomial, bit-identical)
@@ -180,6 +192,20 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     mx.big_s1 = mx.big_s1 || t.big_s1;
   }
   clk.lap("pair scan + PDL challenges");
+  std::vector<uint32_t> RC;   // c mod N^2 of the ciphertexts at or above N^2 (joint tail only)
+  if (pl.joint && std::find(big_c.begin(), big_c.end(), 1) != big_c.end()) {
+    RC.assign((size_t)P * nn, 0u);
+    parallel_for(P, 64, [&](size_t b0, size_t b1) {
+      for (size_t p = b0; p < b1; ++p) {
+        if (!big_c[p]) continue;
+        const Sess& x = pl.ss[sess_of_pair[p]];
+        const hbn::Limbs cc = hbn::from(x.b->enc + (p - x.pbase) * 2 * x.b->nl, 2 * x.b->nl);
+        hbn::store(hbn::mod(cc, hbn::from(NN.data() + (size_t)recv_of_pair[p] * nn, nn)), RC.data() + p * nn, nn);
+      }
+    });
+  }
+  pl.ae_zero.assign(P, 0);
+  for (uint32_t p = 0; p < P; ++p) pl.ae_zero[p] = ae_bits[p] == 0;
   if (sha_fail) {
     c->fail("fsdkr_collect_prepare: SHA-256 (OpenSSL EVP) failed");
     return FSDKR_E_ARG;
@@ -484,6 +510,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   }
   const size_t o_finfo = I.own(finfo);
   const size_t o_epdl = I.own(EPDL);
+  const size_t o_rc = RC.empty() ? 0 : I.own(RC);
   clk.lap("layout plan");
 
   // ---------------- device layout: outputs (offsets relative to the output region)
@@ -501,7 +528,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   //   GD (nl, long)  = g^y1 | ni^y2 [2J] ++ ni^e1 | g^e2 [2J]
   //   GC (ckl)       = sigma^n [Mt*11]
   //   FB (nl, fixed bases h1_i, h2_i, T_m) = h2^s3 | h2^s2A [2P], h1^s1 | h1^s1A [2P], T^Z [Mt*M]
-  const size_t x_GA = OUT((size_t)3 * P * nn * 4 + 4);
+  const size_t x_GA = OUT(((size_t)3 * P + 1) * nn * 4);   // + the joint GA's pad row 3P
   const size_t x_J1 = x_GA, x_J9 = x_GA + (size_t)2 * P * nn * 4;
   // J1 result row k (device address): the GA job's output, or the prestart buffer
   auto J1_at = [&](size_t k) -> uint64_t {
@@ -549,7 +576,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       (2 * (size_t)n + Mt) * 8 + (4 * (size_t)P + (size_t)Mt * M) * 4 + 4 * (8192 + 2048) +   // its comb groups
       4 * (size_t)P * 8 + 4 * (size_t)P * 16 +                                            // binom, inverses
       n_eqall * (sizeof(EqOperand) + 4) + 2 * (size_t)P * sizeof(Prod3Operand) + 4 * (size_t)P +
-      2 * (size_t)P * 8 + P + (size_t)n_p2 * sizeof(Pow2Op) + 32 * 256 + 64 * 1024;
+      2 * (size_t)P * 8 + P + (size_t)n_p2 * sizeof(Pow2Op) + 32 * 256 + 64 * 1024 +
+      ((size_t)2 * P + (size_t)n * 63) * kTailDescBytes;                                 // the joint tail's block
   const size_t out_off = Img::al(in_bytes_pre + desc_bound);
   const size_t total = out_off + out_bytes;
   uint8_t* dev = (uint8_t*)c->buf("collect_arena", total);
@@ -627,7 +655,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
         J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
       const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
-      if (pl.ch_hit) {   // (prestarted)
+      if (pl.ch_hit || pl.joint) {   // (prestarted, or joined into GA's tail)
       } else if (which == 0) {
         J2.add(cp, nn, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
@@ -710,17 +738,48 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   };
   // GA: J1 receiver-major (every wave's chains share N_i: sliding windows when the
   // groups fill whole waves and no J9 instance joins the launch), then J9
-  const uint32_t ga_group = ga_lanes((uint32_t)(J1.size() + J9.size()), nn);
+  // joint: J1 alone (padded, pads write row 3P), J9 its own launch in job slot 2
+  const uint32_t ga_group = ga_lanes((uint32_t)(J1.size() + (pl.joint ? 0 : J9.size())), nn);
   // (pads write the first J9 row, unused when J9 is empty)
   const uint32_t ga_pw = ga_group <= 64 ? 64 / ga_group : 0;
-  const bool ga_aligned = J1.size() && group_by_exponent(J1, ga_pw, J9.size() ? kNoPad : (uint32_t)(2 * P)) &&
-                          J9.size() == 0;
+  const uint32_t pad_row = pl.joint ? (uint32_t)(3 * P) : J9.size() ? kNoPad : (uint32_t)(2 * P);
+  const bool ga_aligned = J1.size() && group_by_exponent(J1, ga_pw, pad_row) && (pl.joint || J9.size() == 0);
   ModexpJob GA = J1, GD = J7;
-  GA.append(J9);
+  if (!pl.joint) GA.append(J9);
   pl.jflags[0] = GA.out_idx.empty() ? 0u : ga_desc_flags(ga_aligned, ga_group);
+  if (pl.joint && !pl.ga_hit && !ga_split_ok(nn, ga_group, pl.jflags[0])) {
+    c->fail("internal: the joint GA lost its sliding-window shape");
+    return FSDKR_E_ARG;
+  }
   GD.append(J8);
-  const size_t d_GA = pack_job(GA), d_J2 = pack_job(J2), d_J5 = pack_job(J5), d_GD = pack_job(GD),
+  const size_t d_GA = pack_job(GA), d_J2 = pack_job(pl.joint ? J9 : J2), d_J5 = pack_job(J5), d_GD = pack_job(GD),
                d_GC = pack_job(GC);
+  // the joint tail's per-instance block (base2 = c^-1 mod N^2 of the pair, exp2 = e_pdl |
+  // e_A) in GA's instance order: the prestarted head's, or GA's own
+  if (pl.joint) {
+    const std::vector<uint32_t>& rows = pl.ga_hit ? gpre->ga_rows : GA.out_idx;
+    const size_t ni = rows.size();
+    std::vector<uint8_t> d2(ni * kTailDescBytes, 0);
+    auto* b2p = reinterpret_cast<uint64_t*>(d2.data());
+    auto* e2p = reinterpret_cast<uint64_t*>(d2.data() + ni * 8);
+    auto* e2l = reinterpret_cast<uint32_t*>(d2.data() + ni * 16);
+    for (size_t k = 0; k < ni; ++k) {
+      const uint32_t r = rows[k];
+      const uint32_t p = r < 2 * P ? r % P : 0u;
+      b2p[k] = DX(x_invc + (size_t)p * nn * 4);
+      if (r < P) {          // PDL: s2^N c^-e_pdl
+        e2p[k] = DI(o_epdl + (size_t)p * 32);
+        e2l[k] = 8;
+      } else if (r < 2 * P) {   // Alice: s^N c^-e_A (a rejected proof's e unused: 0)
+        e2p[k] = DI(o_ae + (size_t)p * el * 4);
+        e2l[k] = alice_pre[p] ? std::min(el, 8u) : 0u;
+      } else {              // pads
+        e2p[k] = DI(o_epdl);
+        e2l[k] = 0;
+      }
+    }
+    pl.d_desc2 = put(d2.data(), d2.size());
+  }
   if (fb_cand) {
     for (uint32_t r = 0; r < n; ++r) {
       FB.b_bits[fb_h1[r]] = gp->bits_h1;
@@ -762,11 +821,15 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   cpdl_extra.clear();
   inv_y_nn.reserve(2 * (size_t)P);
   inv_m_nn.reserve(2 * (size_t)P);
-  for (uint32_t p = 0; p < P && !pl.ch_hit; ++p) {
+  for (uint32_t p = 0; p < P && pl.joint; ++p) {   // joint: c^-1 mod N^2 (value for the tail, c's unit flag)
+    inv_y_nn.push_back(big_c[p] ? DI(o_rc + (size_t)p * nn * 4) : DI(o_enc + (size_t)p * nn * 4));
+    inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
+  }
+  for (uint32_t p = 0; p < P && !pl.ch_hit && !pl.joint; ++p) {
     inv_y_nn.push_back(DX(x_J2 + ((size_t)P + p) * nn * 4));
     inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
   }
-  for (uint32_t p = 0; p < P && !pl.ch_hit; ++p)
+  for (uint32_t p = 0; p < P && !pl.ch_hit && !pl.joint; ++p)
     if (ae_bits[p] == 0 || !alice_pre[p]) {  // c^eA does not witness c's unit-ness
       inv_y_nn.push_back(DX(x_J2 + (size_t)p * nn * 4));
       inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
@@ -806,7 +869,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     e.a = pdl_small[p] ? DX(x_Bpdl + (size_t)p * nn * 4) : DX(x_J9 + (size_t)j9_index[p] * nn * 4);
     e.b = pl.ga_hit ? J1_at(p) : DX(x_J1 + (size_t)p * nn * 4);
     e.c = DI(o_pu2 + (size_t)p * nn * 4);
-    e.d = J2_row(p);
+    e.d = pl.joint ? DI(o_one) : J2_row(p);   // joint: b = s2^N c^-e_pdl already
     e.a_len = e.b_len = e.c_len = e.d_len = nn;
     e.sel = 0xFFFFFFFFu;
     e.flags = 1;
@@ -880,7 +943,9 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   std::vector<Prod3Operand> p3_nn(P), p3_nl(P);
   for (uint32_t p = 0; p < P; ++p) {
     p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), pl.ga_hit ? J1_at((size_t)P + p) : DX(x_J1 + ((size_t)P + p) * nn * 4),
-                pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invc + (size_t)p * nn) : DX(x_invc + (size_t)p * nn * 4),
+                pl.joint    ? DI(o_one)   // joint: b = s^N c^-e_A already
+                : pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invc + (size_t)p * nn)
+                            : DX(x_invc + (size_t)p * nn * 4),
                 nn, nn, nn, 0};
     p3_nl[p] = {J3_row((size_t)P + p), J4_row((size_t)P + p),
                 pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invz + (size_t)p * nl) : DX(x_invz + (size_t)p * nl * 4),
@@ -985,9 +1050,10 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   pl.n_mods_nl = n_mods_nl;
   pl.o_epdl = o_epdl; pl.x_pbits = x_pbits; pl.x_ppanic = x_ppanic; pl.x_Bpdl = x_Bpdl; pl.x_gs1 = x_gs1;
   // with a prestarted J1 the GA job is J9 alone, written where J9's rows live
-  const size_t xs[CollectPlan::NJOB] = {pl.ga_hit ? x_J9 : x_GA, x_GD, x_J2, x_J5, x_GC};
+  // (joint: GA = J1 alone, or nothing after a split prestart; slot 2 = J9 at its rows)
+  const size_t xs[CollectPlan::NJOB] = {pl.ga_hit ? x_J9 : x_GA, x_GD, pl.joint ? x_J9 : x_J2, x_J5, x_GC};
   const size_t ds[CollectPlan::NJOB] = {d_GA, d_GD, d_J2, d_J5, d_GC};
-  const ModexpJob* js[CollectPlan::NJOB] = {&GA, &GD, &J2, &J5, &GC};
+  const ModexpJob* js[CollectPlan::NJOB] = {pl.joint && pl.ga_hit ? &J2 : &GA, &GD, pl.joint ? &J9 : &J2, &J5, &GC};
   for (int k = 0; k < CollectPlan::NJOB; ++k) {
     pl.x_J[k] = xs[k];
     pl.d_J[k] = ds[k];
@@ -1002,7 +1068,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_eqck = d_eqck;
   pl.d_eqckm = d_eqckm; pl.d_p3nn = d_p3nn; pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc;
   pl.d_alpre = d_alpre;
-  pl.n_inv_nn = pl.ch_hit ? gpre->ch_n_inv_nn : (uint32_t)inv_y_nn.size();
+  pl.n_inv_nn = pl.ch_hit && !pl.joint ? gpre->ch_n_inv_nn : (uint32_t)inv_y_nn.size();
   pl.r_unn = pl.ch_hit ? (const void*)gpre->ch_unn : out_base + x_unn;
   pl.r_uzA = pl.ch_hit ? (const void*)gpre->ch_uzA : out_base + x_uzA;
   pl.r_uzp = pl.ch_hit ? (const void*)gpre->ch_uzp : out_base + x_uzp;

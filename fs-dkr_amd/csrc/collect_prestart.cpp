@@ -1014,9 +1014,19 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // priority 3, profiles/r03s_ga_prio_ab.jsonl; again 0.5 ms in round 4 with
   // 16-lane GA, profiles/r04/r04g_*)
   constexpr uint32_t ga_prio = 2;
+  // the head of the split chains when the tail can join c^-e in (prepare launches it)
+  g.split = ga_split_ok(nn, group, flags);
+  SplitArgs head;
+  head.lo_bit = kGaSplit;
   if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, group,
-                               flags)))
+                               flags, g.split ? &head : nullptr)))
     return rc;
+  g.ga_group = group;
+  g.ga_flags = flags;
+  g.ga_count = (uint32_t)J1.size();
+  g.ga_bits = recvn_max;
+  g.ga_desc = dev + o_desc;
+  g.ga_rows = J1.out_idx;
   if (!g.done && (rc = c->hip_check(hipEventCreateWithFlags(&g.done, hipEventDisableTiming), "event"))) return rc;
   if ((rc = c->hip_check(hipEventRecord(g.done, gs), "event record"))) return rc;
   g.nl = nl;

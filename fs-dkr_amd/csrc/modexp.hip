@@ -457,14 +457,15 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_slide_kernel(const ModexpArgs
 // (collect_prepare.cpp): s2^N * c^-e_pdl and s^N * c^-e_A mod N^2 in one chain,
 // base2 = c^-1, instead of a separate 256-bit chain c^e per proof and its inverse
 // (zk_pdl_with_slack.rs:136-142 via commitment_unknown_order :170-188,
-// range_proofs.rs:140-148).  Quotient-scaled rows, as the head.  Exact results.
-template <int KD, int G, int K32>
+// range_proofs.rs:140-148).  QS as the head (the 8 / 16-lane shapes quotient-
+// scaled, the 4-lane throughput shape plain).  Exact results.
+template <int KD, int G, int K32, bool QS>
 __global__ __launch_bounds__(BLOCK, 2) void modexp_tail_kernel(const ModexpArgs a) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
   constexpr int STRIDE = cons_stride(KD);
-  static_assert(scaled_ok(KD, K32), "quotient-scaled chains: N' within R/4");
+  static_assert(!QS || scaled_ok(KD, K32), "quotient-scaled chains: N' within R/4");
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
@@ -475,12 +476,16 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_tail_kernel(const ModexpArgs 
   else if (a.prio >= 3) __builtin_amdgcn_s_setprio(3);
   uint32_t* stream = lds + li * KD;
   const uint32_t* C0 = a.consts + (size_t)a.mod_idx[inst] * STRIDE;
-  const uint32_t* C = C0 + cons_scaled(KD);
+  const uint32_t* C = QS ? C0 + cons_scaled(KD) : C0;
   MT M;
   M.init_lane(g);
 #pragma unroll
   for (int j = 0; j < L; ++j) M.n[j] = C[g * L + j];
   M.ninv = C[3 * KD];
+  auto mulx = [&](uint32_t* x) {
+    if constexpr (QS) M.mul_s(x, x, stream);
+    else M.mul(x, x, stream);
+  };
   const uint32_t w = a.window, tw = 1u << (w - 1);
   const uint32_t* T = a.table + (size_t)inst * (tw + 1) * KD;
   const uint64_t ea = a.exp_ptr[inst];
@@ -515,14 +520,14 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_tail_kernel(const ModexpArgs 
       T2[g * L + j] = C[KD + g * L + j];   // T2[0] = 1 (R mod N')
     }
     put_row(C + 2 * KD);                   // R^2: y -> y R
-    M.mul_s(y, y, stream);
+    mulx(y);
 #pragma unroll
     for (int j = 0; j < L; ++j) T2[KD + g * L + j] = y[j];
     __builtin_amdgcn_wave_barrier();
     lds_put<KD, G>(stream, y, g);          // T2[1] streamed for the powers
     __builtin_amdgcn_wave_barrier();
     for (int u = 2; u < 16; ++u) {
-      M.mul_s(y, y, stream);
+      mulx(y);
 #pragma unroll
       for (int j = 0; j < L; ++j) T2[(size_t)u * KD + g * L + j] = y[j];
     }
@@ -544,21 +549,24 @@ __global__ __launch_bounds__(BLOCK, 2) void modexp_tail_kernel(const ModexpArgs 
     __builtin_amdgcn_wave_barrier();
     lds_put<KD, G>(stream, acc, g);
     __builtin_amdgcn_wave_barrier();
-    M.sqr_s(acc, acc, stream);
+    if constexpr (QS) M.sqr_s(acc, acc, stream);
+    else M.sqr(acc, acc, stream);
     if (i == pend_at) {
       put_row(T + (size_t)(pend_d >> 1) * KD);
-      M.mul_s(acc, acc, stream);
+      mulx(acc);
       pend_at = -1;
     }
     if (joint && (i & 3) == 0) {
       put_row(T2 + (size_t)((ew >> (i & 31)) & 15u) * KD);
-      M.mul_s(acc, acc, stream);
+      mulx(acc);
     }
   }
   // exit: acc * 1 / R modulo N itself
+  if constexpr (QS) {
 #pragma unroll
-  for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
-  M.ninv = C0[3 * KD];
+    for (int j = 0; j < L; ++j) M.n[j] = C0[g * L + j];
+    M.ninv = C0[3 * KD];
+  }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int j = 0; j < L; ++j) stream[g * L + j] = (g == 0 && j == 0) ? 1u : 0u;
@@ -700,13 +708,13 @@ static hipError_t launch_modexp_slide(const ModexpArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int KD, int G, int K32>
+template <int KD, int G, int K32, bool QS>
 static hipError_t launch_modexp_tail(const ModexpArgs& a, hipStream_t st) {
   const uint32_t bs = block_threads(a.count * G);
   const uint32_t ipb = bs / G;
   const uint32_t blocks = (a.count + ipb - 1) / ipb;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((modexp_tail_kernel<KD, G, K32>), dim3(blocks), dim3(bs), 0, st, a);
+  hipLaunchKernelGGL((modexp_tail_kernel<KD, G, K32, QS>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
@@ -804,11 +812,15 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
   const bool qs = qs_env == 1;
   if (a.slide) {   // shared exponent per wave: the 4096-bit shapes of GA
     if (k32 != 128 || a.ct || a.group == kWideGroup || a.group == kWaveGroup) return hipErrorInvalidValue;
-    if (a.lo_bit) {   // split chains: quotient-scaled 8 / 16-lane shapes only (the head's table layout)
-      if (!qs || !(a.group == 8 || a.group == 16)) return hipErrorInvalidValue;
-      if (a.tail)
-        return a.group == 16 ? launch_modexp_tail<144, 16, 128>(a, st) : launch_modexp_tail<144, 8, 128>(a, st);
-      return a.group == 16 ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, true>(a, st);
+    if (a.lo_bit) {   // split chains: head and tail at the caller's lanes, QS as the full chain's
+      switch (a.group) {
+        case 16: return a.tail ? (qs ? launch_modexp_tail<144, 16, 128, true>(a, st) : launch_modexp_tail<144, 16, 128, false>(a, st))
+                               : (qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st));
+        case 8: return a.tail ? (qs ? launch_modexp_tail<144, 8, 128, true>(a, st) : launch_modexp_tail<144, 8, 128, false>(a, st))
+                              : (qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st));
+        case 4: return a.tail ? launch_modexp_tail<144, 4, 128, false>(a, st) : launch_modexp_slide<144, 4, 128, false>(a, st);
+        default: return hipErrorInvalidValue;
+      }
     }
     switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
       case 16: return qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st);

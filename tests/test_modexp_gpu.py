@@ -122,7 +122,7 @@ def test_modexp_regular_access_equals_plain(gpu_ctx, limbs):
     assert got == gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs)
 
 
-@pytest.mark.parametrize("group", [8, 16])
+@pytest.mark.parametrize("group", [4, 8, 16])
 def test_modexp_joint_split_chains(gpu_ctx, group):
     """collect()'s GA chains split into a head (the exponent's bits >= 256) and a
     joint tail that multiplies base2^exp2 in along the tail's squarings
