@@ -570,6 +570,12 @@ inline uint32_t ga_desc_flags(bool aligned_for, uint32_t group) {
 // sliding-window GA shapes (4096-bit, 4 / 8 / 16 lanes); FSDKR_JOINT=0 keeps J2
 // (A/B).  Read per call.
 constexpr uint32_t kGaSplit = 256;
+// GA's issue priority (s_setprio of the prestarted chains and of the joint tail);
+// FSDKR_GA_PRIO overrides it (A/B)
+inline uint32_t ga_prio() {
+  const char* e = getenv("FSDKR_GA_PRIO");
+  return e ? (uint32_t)std::min(3, std::max(0, atoi(e))) : 2u;
+}
 inline bool ga_split_ok(uint32_t nn, uint32_t group, uint32_t flags) {
   const char* j = getenv("FSDKR_JOINT");
   const char* s = getenv("FSDKR_SLIDE");

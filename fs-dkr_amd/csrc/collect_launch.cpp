@@ -124,8 +124,8 @@ int collect_launch_impl(Ctx* c) {
       if (pl.ga_hit) {   // the prestarted head runs on this stream: its tail follows c^-1
         const CollectPlan::GaTail& t = pl.ga_tail;
         (void)hipStreamWaitEvent(ss, inv_done, 0);
-        if ((rc = launch_modexp_desc(c, nn, t.count, t.bits, t.desc, t.cons, t.out, ss, "mxt_GApre", 2, t.group, t.flags,
-                                     &tail)) ||
+        if ((rc = launch_modexp_desc(c, nn, t.count, t.bits, t.desc, t.cons, t.out, ss, "mxt_GApre", ga_prio(), t.group,
+                                     t.flags, &tail)) ||
             (rc = c->hip_check(hipEventRecord(pl.ga_done, ss), "event record")))   // the s^N rows: after the tail
           return rc;
       } else if (pl.jcount[0]) {

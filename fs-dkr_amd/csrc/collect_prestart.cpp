@@ -1013,12 +1013,12 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // the issue slots more (n = 64 median of 7 interleaved calls 56.4 -> 55.3 ms vs
   // priority 3, profiles/r03s_ga_prio_ab.jsonl; again 0.5 ms in round 4 with
   // 16-lane GA, profiles/r04/r04g_*)
-  constexpr uint32_t ga_prio = 2;
+  const uint32_t gprio = ga_prio();
   // the head of the split chains when the tail can join c^-e in (prepare launches it)
   g.split = ga_split_ok(nn, group, flags);
   SplitArgs head;
   head.lo_bit = kGaSplit;
-  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", ga_prio, group,
+  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", gprio, group,
                                flags, g.split ? &head : nullptr)))
     return rc;
   g.ga_group = group;
