@@ -30,17 +30,27 @@ def _own(msgs, k):
     return m
 
 
+PAIR_KINDS = ("pdl_s1", "pdl_s2", "pdl_s3", "pdl_u2", "pdl_z", "range_s", "range_s2", "range_e", "range_z", "enc",
+              "feldman")
+MSG_KINDS = ("rp_Z", "rp_A", "ck")
+
+
 def inject(msgs, joins, spec):
-    """spec: list of (kind, k, i).  kinds: pdl_s1, pdl_u2, pdl_s3 (pair k, i), range_s2,
-    range_e (pair), feldman (pair), rp_Z (message k, index i), ck (message k), dlog (join k)."""
+    """spec: list of (kind, k, i).  kinds: pdl_s1, pdl_s2, pdl_s3, pdl_u2, pdl_z (pair k, i),
+    range_s, range_s2, range_e, range_z (pair), enc (the pair's ciphertext c), feldman
+    (pair), rp_Z / rp_A (message k, index i), ck (message k), dlog (join k)."""
     msgs, joins = list(msgs), list(joins)
     for kind, k, i in spec:
-        if kind in ("pdl_s1", "pdl_u2", "pdl_s3"):
+        if kind in ("pdl_s1", "pdl_s2", "pdl_s3", "pdl_u2", "pdl_z"):
             m = _own(msgs, k)
             p = m.pdl_proof_vec[i]
             f = kind.split("_")[1]
             m.pdl_proof_vec[i] = dataclasses.replace(p, **{f: getattr(p, f) + 1})
-        elif kind in ("range_s2", "range_e"):
+        elif kind == "enc":
+            m = _own(msgs, k)
+            m.points_encrypted_vec = list(m.points_encrypted_vec)
+            m.points_encrypted_vec[i] += 1
+        elif kind in ("range_s", "range_s2", "range_e", "range_z"):
             m = _own(msgs, k)
             a = m.range_proofs[i]
             f = kind.split("_")[1]
@@ -48,10 +58,11 @@ def inject(msgs, joins, spec):
         elif kind == "feldman":
             m = _own(msgs, k)
             m.points_committed_vec[i] = ec.mul(ec.G, 12345 + i)
-        elif kind == "rp_Z":
+        elif kind in ("rp_Z", "rp_A"):
             m = copy.copy(msgs[k]) if k < len(msgs) else copy.copy(joins[k - len(msgs)])
             pf = m.ring_pedersen_proof
-            m.ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(z + (j == i) for j, z in enumerate(pf.Z)))
+            f = kind.split("_")[1]
+            m.ring_pedersen_proof = dataclasses.replace(pf, **{f: tuple(z + (j == i) for j, z in enumerate(getattr(pf, f)))})
             if k < len(msgs):
                 msgs[k] = m
             else:
@@ -114,12 +125,12 @@ def expected(msgs, joins, lk, spec, key_bits):
     n = R + J
     pairs, mres, jres = {}, {}, {}
     for kind, k, i in spec:
-        if kind in ("pdl_s1", "pdl_u2", "pdl_s3", "range_s2", "range_e", "feldman"):
+        if kind in PAIR_KINDS:
             m = msgs[k]
             vss = VerifiableSS(lk.t, n, list(m.coefficients_committed_vec.commitments))
             fel = vss.validate_share_public(m.points_committed_vec[i], i + 1)
             pairs[(k, i)] = (fel,) + oracle_pair(m, lk, i)
-        elif kind in ("rp_Z", "ck"):
+        elif kind in MSG_KINDS:
             mm = msgs[k] if k < R else joins[k - R]
             mres[k] = oracle_message(mm)
         elif kind == "dlog":
