@@ -108,7 +108,13 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
         e->f[0] = i;
         return FSDKR_OK;
       }
-      if (!v->range[(size_t)k * n + i]) {
+      if (v->range[(size_t)k * n + i] & 2) {   // a negative Alice exponent (host layer)
+        e->panic = 1;
+        e->variant = FSDKR_ERR_RANGE_PROOF;
+        e->f[0] = i;
+        return FSDKR_OK;
+      }
+      if (!(v->range[(size_t)k * n + i] & 1)) {
         e->variant = FSDKR_ERR_RANGE_PROOF;
         e->f[0] = i;
         return FSDKR_OK;
@@ -165,6 +171,12 @@ int first_error_impl(const fsdkr_collect_batch* b, const fsdkr_verdicts* v, fsdk
     }
     if (!(v->ck[R + j] & 1)) {
       e->variant = FSDKR_ERR_PAILLIER_VERIFICATION;
+      e->f[0] = pi;
+      return FSDKR_OK;
+    }
+    if (v->dlog[j] & 4) {   // a negative DLog response y (host layer)
+      e->panic = 1;
+      e->variant = FSDKR_ERR_DLOG_PROOF_VALIDATION;
       e->f[0] = pi;
       return FSDKR_OK;
     }

@@ -376,7 +376,7 @@ class Context:
         from .batch import Verdicts
         v = Verdicts(batch.R, batch.J, batch.n)
         self.check(self._lib.fsdkr_verify_collect(self._h, ctypes.byref(batch.c), ctypes.byref(v.c)))
-        return v
+        return batch.settle(v)
 
     def collect_prepare(self, batch):
         """Host pre-pass + one upload of the batch image (device-resident afterwards)."""
@@ -387,7 +387,7 @@ class Context:
         from .batch import Verdicts
         v = Verdicts(batch.R, batch.J, batch.n)
         self.check(self._lib.fsdkr_collect_run(self._h, ctypes.byref(v.c)))
-        return v
+        return batch.settle(v)
 
     def collect_prestart(self, batch):
         """Start the s^N mod N^2 chains of a batch whose GA fields are packed
@@ -415,7 +415,7 @@ class Context:
         from .batch import Verdicts
         v = Verdicts(batch.R, batch.J, batch.n)
         self.check(self._lib.fsdkr_collect_finish(self._h, ctypes.byref(v.c)))
-        return v
+        return batch.settle(v)
 
     def collect_prepare_many(self, batches):
         """Prepare many sessions (fsdkr.batch.CollectBatch each) as ONE device image."""
@@ -446,7 +446,7 @@ class Context:
         """Wait for the launched multi-session pipeline; SetVerdicts of the live sessions."""
         v = sset.verdicts()
         self.check(self._lib.fsdkr_collect_finish_multi(self._h, v.c_array, len(sset.live)))
-        return v
+        return sset.settle(v)
 
     def collect_finish_many(self, batches):
         """Wait for the launched multi-session pipeline; one Verdicts per session."""
@@ -454,7 +454,7 @@ class Context:
         vs = [Verdicts(b.R, b.J, b.n) for b in batches]
         arr = (VerdictsC * len(vs))(*[v.c for v in vs])
         self.check(self._lib.fsdkr_collect_finish_multi(self._h, arr, len(vs)))
-        return vs
+        return [b.settle(v) for b, v in zip(batches, vs)]
 
     def paillier_decrypt(self, cts, p, q, nl):
         """Decrypt ciphertexts under dk = (p, q) on the GPU (CRT form)."""

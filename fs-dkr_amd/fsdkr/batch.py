@@ -14,10 +14,15 @@ each message's own vector, refresh_message.rs:180-182), range_proofs / A / Z /
 sigma_vec shorter than the loops index (the reference's index panic at that
 check), a LocalKey with fewer keys than receivers (panic at the first pair
 past them, :334-339), an ek.n wider than the batch's moduli (its correct-key
-proof runs at its own width before ModuliTooSmall, :376-391).  Still outside
-the representable set (UnsupportedInput): negative BigInts and values wider
-than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
+proof runs at its own width before ModuliTooSmall, :376-391), and negative
+BigInts where the reference's outcome for that instance is a panic, an error
+or a plain residue (_Negatives: PDL s1 / u2 / u3 / s2, Alice s / s1 / s2 / e,
+ring-Pedersen Z, DLog y).  Still outside the representable set
+(UnsupportedInput): other negative fields (hashed AND reduced values such as
+c, z, A, or h2^-1 exponents such as PDL s3) and values wider than 3072 bits in
+a proof field (6144 bits for ek.n / sigma)."""
 import ctypes
+import math
 import os
 import threading
 import weakref
@@ -29,6 +34,7 @@ from ._native import CollectBatchC, ErrorC, VerdictsC, lib
 
 M2 = 11   # zk-paillier NiCorrectKeyProof sigma_vec length
 _CK_WIDTHS = (64, 96, 128, 192)
+_Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141   # secp256k1 group order
 
 
 class UnsupportedInput(ValueError):
@@ -168,6 +174,105 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
 
 
+class _Negatives:
+    """Per-instance outcomes of negative operands:
+    the gather of a field that may hold a negative value falls back, only when
+    the C gather rejects it, to a Python pass that packs a stand-in row and
+    records the instance; decide() derives each instance's rule once the batch
+    is gathered, and after the device pass apply() rewrites that
+    instance's verdict to the reference's outcome.  The rest of the batch runs
+    unchanged.
+
+    Reference semantics (curv BigInt::mod_pow -> GMP mpz_powm: a negative
+    exponent panics, a negative base is reduced; to_bytes hashes |v|):
+    - PDL (zk_pdl_with_slack.rs:113-167): s1 < 0 panics in h^s1 (u2_test_tmp,
+      :139) whatever else holds; u2 / u3 < 0 hash as |u| (the challenge, and so
+      u1's check, is unchanged) and can never equal a residue (flag false);
+      s2 < 0 is the base of s2^N mod N^2: packed as s2 mod N^2.
+    - Alice (range_proofs.rs:112-164): s1 > q^3 -> false first; e < 0 panics
+      in z^e; z^e not invertible -> false; then s1 / s2 < 0 panic in h1^s1 /
+      h2^s2; s < 0 is the base of s^N mod N^2 (packed as s mod N^2).
+    - ring-Pedersen (ring_pedersen_proof.rs:126-157): Z[i] < 0 panics at
+      iteration i, after checks 0..i-1 -- exactly the short-Z mechanism
+      (ped_lens: Z "ends" at its first negative entry).
+    - composite DLog (zk-paillier, joins :417-424): y < 0 panics in g^y once the
+      N > 2^128 and gcd checks pass (else false); proof 2 runs only if proof 1
+      holds."""
+
+    def __init__(self):
+        self.rows = {}     # field -> rows packed with a stand-in
+        self.pdl = {}      # pair -> (or-bits, and-mask)
+        self.range = {}    # pair -> verdict (0 false, 2 panic)
+        self.dlog = {}     # join -> "y1-panic" | "y1-false" | "y2"
+
+    def __bool__(self):
+        return bool(self.rows)
+
+    def field(self, G, name, objs, attr, fix):
+        """G.field(objs, attr); a negative value at row k is packed as fix(k, v)"""
+        try:
+            return G.field(objs, attr)
+        except UnsupportedInput:
+            vals = [o if attr is None else getattr(o, attr) for o in objs]
+            bad = [k for k, v in enumerate(vals) if isinstance(v, int) and v < 0]
+            if not bad:
+                raise
+            for k in bad:
+                vals[k] = fix(k, vals[k])
+            self.rows[name] = bad
+            return G.field(vals)
+
+    def decide(self, msgs, joins, n, avail, pdl, rng, sts):
+        """the verdict rules, once every field is gathered"""
+        for p in self.rows.get("pdl_s1", ()):
+            self.pdl[p] = (8, 0xFF)
+        for name, bit in (("pdl_u2", 2), ("pdl_u3", 4)):
+            for p in self.rows.get(name, ()):
+                o, a = self.pdl.get(p, (0, 0xFF))
+                self.pdl[p] = (o, a & ~bit)
+        q3 = _Q ** 3
+        for p in sorted(set().union(*(self.rows.get(x, ()) for x in ("rp_s1", "rp_s2", "rp_e")))):
+            i = p % n
+            if i >= avail:          # the pair panics at its statement (refresh_message.rs:334)
+                continue
+            a = rng[p]
+            if a.s1 > q3:
+                self.range[p] = 0
+            elif a.e < 0:
+                self.range[p] = 2
+            elif a.e > 0 and math.gcd(a.z, sts[i].N) != 1:
+                self.range[p] = 0
+            else:                   # s1 or s2 < 0
+                self.range[p] = 2
+        for j in sorted(set(self.rows.get("dlog_y1", ())) | set(self.rows.get("dlog_y2", ()))):
+            st = joins[j].dlog_statement
+            if joins[j].composite_dlog_proof_base_h1.y < 0:
+                pre = st.N > (1 << 128) and math.gcd(st.g, st.N) == 1 and math.gcd(st.ni, st.N) == 1
+                self.dlog[j] = "y1-panic" if pre else "y1-false"
+            else:
+                self.dlog[j] = "y2"
+
+    def apply(self, pdl, rng, dlog):
+        """rewrite the device verdicts (this batch's rows) to the reference's outcome"""
+        for p, (o, a) in self.pdl.items():
+            pdl[p] = (pdl[p] & a) | o
+        for p, v in self.range.items():
+            rng[p] = v
+        for j, rule in self.dlog.items():
+            if rule == "y1-panic" or (rule == "y2" and dlog[j] & 1):
+                dlog[j] = 4
+            elif rule == "y1-false":
+                dlog[j] = 0
+
+
+def _zero(k, v):
+    return 0
+
+
+def _magnitude(k, v):
+    return -v
+
+
 class Verdicts:
     def __init__(self, R, J, n):
         P = R * n
@@ -230,6 +335,7 @@ class CollectBatch:
         G = _Gather()
         k = self._k
         self._ga, self._pending, self._stage1b, self._stage1c = None, None, None, False
+        self.negs = _Negatives()
         if self.header_only:
             f_ckn = G.field([m.ek.n for m in all_m] or [0])
             ck_bits = max(1, f_ckn[1])
@@ -256,15 +362,21 @@ class CollectBatch:
         rst = list(sts[:avail]) + [None] * (n - avail)
         # gathered first: GA's fields and what sets stage 1's width; every other
         # field is gathered by _rest() (stage1b / complete), after GA has started
-        F = {"recv_n": G.field([x.n for x in keys[:avail]] + [3] * (n - avail)),
+        rn = [x.n for x in keys[:avail]] + [3] * (n - avail)
+        neg = self.negs
+
+        def residue(k, v):   # a negative base of x^N mod N^2: GMP reduces it
+            nn = rn[k % n] ** 2
+            return v % nn if nn else 0
+        F = {"recv_n": G.field(rn),
              "recv_ntilde": G.field([s.N if s else 3 for s in rst]),
              "recv_h1": G.field([s.g if s else 1 for s in rst]),
              "recv_h2": G.field([s.ni if s else 1 for s in rst]),
-             "pdl_s2": G.field(pdl, "s2"), "rp_s": G.field(rng, "s")}
+             "pdl_s2": neg.field(G, "pdl_s2", pdl, "s2", residue), "rp_s": neg.field(G, "rp_s", rng, "s", residue)}
         for a in ("T", "N"):
             F["ped_" + a] = G.field([m.ring_pedersen_statement for m in all_m], a)
         self._pending = dict(msgs=msgs, joins=joins, all_m=all_m, n=n, M=M, G=G, F=F, pdl=pdl, rng=rng,
-                             t=local_key.t, rest=False)
+                             t=local_key.t, rest=False, avail=avail, sts=sts)
         # stage 1: the fields fsdkr_collect_prestart reads (GA's bases and moduli, the
         # h1/h2 table bases and the exponents that size the tables), at the width they
         # need; stage 2 (complete) keeps them if the batch width agrees
@@ -321,21 +433,31 @@ class CollectBatch:
         ckl = next((w for w in _CK_WIDTHS if ck_bits <= 32 * w), None)
         if ckl is None:
             raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
-        for a in ("s1", "s3"):
-            F["pdl_" + a] = G.field(pdl, a)
+        neg = self.negs
+        F["pdl_s1"] = neg.field(G, "pdl_s1", pdl, "s1", _zero)
+        F["pdl_s3"] = G.field(pdl, "s3")
         for a in ("s1", "s2"):
-            F["rp_" + a] = G.field(rng, a)
+            F["rp_" + a] = neg.field(G, "rp_" + a, rng, a, _zero)
         F["ped_S"] = G.field([m.ring_pedersen_statement for m in all_m], "S")
         rpp = [m.ring_pedersen_proof for m in all_m]
-        if any(len(r.A) < M or len(r.Z) < M for r in rpp):   # short vectors: zero-padded rows
-            c.ped_lens = k(np.array([[min(len(r.A), M), min(len(r.Z), M)] for r in rpp], dtype=np.uint32))
-            A = [list(r.A[:M]) for r in rpp]
-            Z = [list(r.Z[:M]) for r in rpp]
-            F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
-            F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
-        else:   # the first M of every vector, flattened in C
+        short = any(len(r.A) < M or len(r.Z) < M for r in rpp)
+        if not short:   # the first M of every vector, flattened in C
             F["ped_A"] = G.rows(rpp, "A", M)
-            F["ped_Z"] = G.rows(rpp, "Z", M)
+            try:
+                F["ped_Z"] = G.rows(rpp, "Z", M)
+            except UnsupportedInput:   # a negative Z[i]: Z "ends" there (see _Negatives)
+                short = True
+        if short:   # short vectors (or a negative Z entry): zero-padded rows
+            Z = [list(r.Z[:M]) for r in rpp]
+            zlen = [next((i for i, v in enumerate(row) if isinstance(v, int) and v < 0), len(row)) for row in Z]
+            if any(zl < len(row) for zl, row in zip(zlen, Z)):
+                neg.rows["ped_Z"] = [m for m, (zl, row) in enumerate(zip(zlen, Z)) if zl < len(row)]
+                Z = [row[:zl] for zl, row in zip(zlen, Z)]
+            c.ped_lens = k(np.array([[min(len(r.A), M), zl] for r, zl in zip(rpp, zlen)], dtype=np.uint32))
+            if "ped_A" not in F:
+                A = [list(r.A[:M]) for r in rpp]
+                F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
+            F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
         c.s1l = _limbs_for(max(F["pdl_s1"][1], F["rp_s1"][1], 1))
         c.s3l = _limbs_for(max(F["pdl_s3"][1], F["rp_s2"][1], 1))
         c.zl = _limbs_for(max(F["ped_Z"][1], 1))
@@ -393,6 +515,8 @@ class CollectBatch:
         G.run()
         if "commit" not in ga_arrs:   # (stage1c packed the points already)
             self._points(st)
+        if self.negs:
+            self.negs.decide(msgs, joins, n, st["avail"], st["pdl"], st["rng"], st["sts"])
         self.nl = nl
         return self
 
@@ -403,17 +527,20 @@ class CollectBatch:
             return
         st["late"] = True
         F, G, pdl, rng, n = st["F"], st["G"], st["pdl"], st["rng"], st["n"]
+        neg = self.negs
         F["enc"] = G.field([m.points_encrypted_vec[i] for m in st["msgs"] for i in range(n)])
-        for a in ("z", "u2", "u3"):
-            F["pdl_" + a] = G.field(pdl, a)
-        for a in ("z", "e"):
-            F["rp_" + a] = G.field(rng, a)
+        F["pdl_z"] = G.field(pdl, "z")
+        for a in ("u2", "u3"):
+            F["pdl_" + a] = neg.field(G, "pdl_" + a, pdl, a, _magnitude)
+        F["rp_z"] = G.field(rng, "z")
+        F["rp_e"] = neg.field(G, "rp_e", rng, "e", _zero)
         if st["joins"]:
             for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):
                 F["dlog_" + name] = G.field([j.dlog_statement for j in st["joins"]], attr)
             for name, which, attr in (("x1", 1, "x"), ("x2", 2, "x"), ("y1", 1, "y"), ("y2", 2, "y")):
-                F["dlog_" + name] = G.field([getattr(j, f"composite_dlog_proof_base_h{which}") for j in st["joins"]],
-                                            attr)
+                pf = [getattr(j, f"composite_dlog_proof_base_h{which}") for j in st["joins"]]
+                F["dlog_" + name] = neg.field(G, "dlog_" + name, pf, attr, _zero) if attr == "y" else \
+                    G.field(pf, attr)
 
     def _points(self, st):
         """secp256k1 points: the shares' commitments Q, PDL u1 and the VSS commitments"""
@@ -495,6 +622,12 @@ class CollectBatch:
         self._keep.append(arr)
         return _ptr(arr)
 
+    def settle(self, verdicts):
+        """the device verdicts with the negative-operand instances' outcomes (_Negatives)"""
+        if self.negs:
+            self.negs.apply(verdicts.pdl, verdicts.range, verdicts.dlog)
+        return verdicts
+
     def first_error(self, verdicts):
         err = ErrorC()
         rc = lib().fsdkr_collect_first_error(ctypes.byref(self.c),
@@ -537,6 +670,39 @@ def _struct_dtype(cls):
 
 _BATCH_DT = _struct_dtype(CollectBatchC)
 _VERD_DT = _struct_dtype(VerdictsC)
+
+
+def _has_negative(session):
+    """any negative integer among the proof / key fields of one session (the slow
+    scan that runs only after a set-wide gather rejected a value)"""
+    msgs, lk, joins = session
+
+    def neg(*xs):
+        return any(isinstance(x, int) and x < 0 for x in xs)
+
+    def fields(o, names):
+        return neg(*(getattr(o, a, 0) for a in names))
+    for k in lk.paillier_key_vec:
+        if fields(k, ("n",)):
+            return True
+    for s in lk.h1_h2_n_tilde_vec:
+        if fields(s, ("N", "g", "ni")):
+            return True
+    for m in list(msgs) + list(joins):
+        rp = m.ring_pedersen_proof
+        if fields(m.ek, ("n",)) or fields(m.ring_pedersen_statement, ("S", "T", "N")) or neg(*rp.A) or \
+                neg(*rp.Z) or neg(*m.dk_correctness_proof.sigma_vec):
+            return True
+    for m in msgs:
+        if neg(*m.points_encrypted_vec) or \
+                any(fields(p, ("z", "u2", "u3", "s1", "s2", "s3")) for p in m.pdl_proof_vec) or \
+                any(fields(a, ("z", "e", "s", "s1", "s2")) for a in m.range_proofs):
+            return True
+    for j in joins:
+        if fields(j.dlog_statement, ("N", "g", "ni")) or \
+                fields(j.composite_dlog_proof_base_h1, ("x", "y")) or fields(j.composite_dlog_proof_base_h2, ("x", "y")):
+            return True
+    return False
 
 
 def _regular(msgs, lk, joins, M):
@@ -607,9 +773,22 @@ class SessionSet:
             return self
         sessions, reg, M, key_bits = self._pending
         self._pending = None
-        regset = set(reg)
         if reg:
-            self._pack_regular(sessions, reg, M, key_bits)
+            try:
+                self._pack_regular(sessions, reg, M, key_bits)
+            except UnsupportedInput:
+                # negative operands: those sessions get their own CollectBatch, whose
+                # instances carry the reference's per-instance outcome (_Negatives)
+                neg = [s for s in reg if _has_negative(sessions[s])]
+                if not neg:
+                    raise
+                for s in neg:
+                    self.batches[s] = CollectBatch(*sessions[s], M, key_bits)
+                reg = [s for s in reg if s not in set(neg)]
+                self._z = None   # (stage 1b's Z rows covered the old list)
+                if reg:
+                    self._pack_regular(sessions, reg, M, key_bits)
+        regset = set(reg)
         for s in self.live:
             if s not in regset:
                 b = self.batches[s]
@@ -631,16 +810,21 @@ class SessionSet:
         if any(len(lk.paillier_key_vec) < nn for (m, lk, j), nn in zip(ses, n)):
             return
         G = _Gather(self._owned)
-        f_rn = G.field([k for (ms, lk, js), nn in zip(ses, n) for k in lk.paillier_key_vec[:nn]], "n")
-        f_s2 = G.field([m.pdl_proof_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s2")
-        f_s = G.field([m.range_proofs[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)], "s")
-        sts = [st for (ms, lk, js), nn in zip(ses, n) for st in lk.h1_h2_n_tilde_vec[:nn]]
-        if len(sts) != int(n.sum()):
+        try:   # (a negative operand: no prestart; complete() moves its session out)
+            f_rn = G.field([k for (ms, lk, js), nn in zip(ses, n) for k in lk.paillier_key_vec[:nn]], "n")
+            f_s2 = G.field([m.pdl_proof_vec[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)],
+                           "s2")
+            f_s = G.field([m.range_proofs[i] for (ms, lk, js), nn in zip(ses, n) for m in ms for i in range(nn)],
+                          "s")
+            sts = [st for (ms, lk, js), nn in zip(ses, n) for st in lk.h1_h2_n_tilde_vec[:nn]]
+            if len(sts) != int(n.sum()):
+                return
+            f_nt, f_h1, f_h2 = G.field(sts, "N"), G.field(sts, "g"), G.field(sts, "ni")
+            am = [m for ms, lk, js in ses for m in ms + js]
+            rps = [m.ring_pedersen_statement for m in am]
+            f_T, f_N = G.field(rps, "T"), G.field(rps, "N")
+        except UnsupportedInput:
             return
-        f_nt, f_h1, f_h2 = G.field(sts, "N"), G.field(sts, "g"), G.field(sts, "ni")
-        am = [m for ms, lk, js in ses for m in ms + js]
-        rps = [m.ring_pedersen_statement for m in am]
-        f_T, f_N = G.field(rps, "T"), G.field(rps, "N")
         bits = max(1, f_rn[1], f_s2[1], f_s[1], f_nt[1], f_h1[1], f_h2[1], f_T[1], f_N[1])
         nl = 64 if bits <= 2048 else 96 if bits <= 3072 else None
         if nl is None:
@@ -706,7 +890,10 @@ class SessionSet:
         n, nl, M, *rest = self._s1b
         self._s1b = None
         G = _Gather(self._owned)
-        self._stage1_rest(G, n, nl, M, *rest)
+        try:
+            self._stage1_rest(G, n, nl, M, *rest)
+        except UnsupportedInput:
+            return False
         G.run()
         self._stage1_fill()
         return True
@@ -721,7 +908,10 @@ class SessionSet:
         sessions, reg, M, key_bits = self._pending
         ses = [sessions[s] for s in reg]
         G = _Gather(self._owned)
-        f_z = G.rows([m.ring_pedersen_proof for ms, lk, js in ses for m in ms + js], "Z", M)
+        try:
+            f_z = G.rows([m.ring_pedersen_proof for ms, lk, js in ses for m in ms + js], "Z", M)
+        except UnsupportedInput:
+            return False
         zl = _limbs_for(max(1, f_z[1]))
         a_z = G.slot(f_z, zl)
         G.run()
@@ -852,6 +1042,17 @@ class SessionSet:
     def verdicts(self):
         """Verdict arrays of the live sessions and their fsdkr_verdicts array."""
         return SetVerdicts(self)
+
+    def settle(self, v):
+        """CollectBatch.settle for the sessions packed on their own (the only ones
+        that may carry negative operands)"""
+        for s, b in enumerate(self.batches):
+            if b is not None and b.negs and s in self.row:
+                r = self.row[s]
+                p, j = int(v.off["pair"][r]), int(v.off["join"][r])
+                P, J = int(v.P[r]), int(v.Jn[r])
+                b.negs.apply(v.pdl[p:p + P], v.range[p:p + P], v.dlog[j:j + J])
+        return v
 
     def first_error(self, s, verdicts):
         """fsdkr_collect_first_error of session s (live: its prepared verdicts; else header only)."""

@@ -198,14 +198,18 @@ typedef struct fsdkr_collect_batch {
 
 /* Verdicts (caller-allocated). 1 bits mean "check passed".  cap_* are the
  * element capacities of the arrays; a call fails with FSDKR_E_ARG if the
- * prepared batch needs more (R*n pairs, R+J messages, J joins). */
+ * prepared batch needs more (R*n pairs, R+J messages, J joins).  The device
+ * pass never sets range bit1 / dlog bit2: the host layer sets them for
+ * instances whose negative operand makes the reference panic (a negative
+ * exponent in curv's mod_pow), and fsdkr_collect_first_error maps them. */
 typedef struct fsdkr_verdicts {
   uint8_t* feldman;  /* [R*n]  bit0 validate_share_public ok; bit1: reference panics  */
   uint8_t* pdl;      /* [R*n]  bit0 u1, bit1 u2, bit2 u3 equal; bit3: reference panics */
-  uint8_t* range;    /* [R*n]  AliceProof::verify                                      */
+  uint8_t* range;    /* [R*n]  bit0 AliceProof::verify ok; bit1: reference panics        */
   uint8_t* ped;      /* [R+J]  bit0 RingPedersenProof::verify ok; bit1: panics         */
   uint8_t* ck;       /* [R+J]  bit0 NiCorrectKeyProof::verify ok; bit1: reference panics */
-  uint8_t* dlog;     /* [J]    bit0 base-h1 proof ok, bit1 base-h2 proof ok (may be NULL if J = 0) */
+  uint8_t* dlog;     /* [J]    bit0 base-h1 proof ok, bit1 base-h2 proof ok, bit2: reference
+                      *         panics (may be NULL if J = 0) */
   uint32_t cap_pairs, cap_msgs, cap_joins;
 } fsdkr_verdicts;
 

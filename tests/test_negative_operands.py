@@ -1,0 +1,193 @@
+"""Negative operands, per instance.  A negative
+BigInt in one sender's proof gets that instance's reference outcome -- the
+oracle's panic, error or plain residue -- instead of rejecting the whole batch
+with UnsupportedInput (fsdkr/batch.py _Negatives).
+
+CPU part (no device pass): the host layer's rules on top of an all-valid
+verdict image give exactly the oracle's outcome (restatement of
+refresh_message.rs:321-437; zk_pdl_with_slack.rs:113-167, range_proofs.rs:112-164,
+ring_pedersen_proof.rs:126-157, zk-paillier CompositeDLogProof::verify), and
+the stand-in rows are what the kernels need (negative bases packed as their
+residue mod N^2).  The GPU part is tests/test_negative_operands_gpu.py."""
+import copy
+import dataclasses
+
+import numpy as np
+import pytest
+
+from oracle import protocol
+from oracle.rng import Rng
+
+KB = 1024
+
+
+def _dkr(t, n, seed):
+    rng = Rng(seed)
+    keys = protocol.simulate_keygen(t, n, rng, KB)
+    msgs, dks = [], []
+    for key in keys:
+        m, dk = protocol.distribute(key.i, key, n, rng, KB)
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks
+
+
+def _joins(seed):
+    rng = Rng(seed)
+    keys = [k.clone() for k in protocol.simulate_keygen(1, 4, rng, KB)[:3]]
+    jm, _ = protocol.join_distribute(rng, KB)
+    jm.set_party_index(4)
+    msgs, dks = [], []
+    for key in keys:
+        m, dk = protocol.replace([jm], key, {1: 1, 2: 2, 3: 3}, 4, rng, KB)
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks, jm
+
+
+@pytest.fixture(scope="module")
+def dkr4():
+    return _dkr(1, 4, "neg-t1n4")
+
+
+@pytest.fixture(scope="module")
+def joined():
+    return _joins("neg-join")
+
+
+def oracle_outcome(msgs, key, dk, joins=()):
+    k = key.clone()
+    try:
+        protocol.collect(copy.deepcopy(msgs), k, dk, copy.deepcopy(list(joins)), Rng("neg"), KB)
+    except protocol.FsDkrError as e:
+        return (e.variant, e.fields)
+    except Exception:   # PanicError / IndexError: the reference panics
+        return ("panic",)
+    return None
+
+
+def host_outcome(msgs, key, joins=()):
+    """the host layer over an all-valid device verdict image"""
+    from fsdkr.batch import CollectBatch, Verdicts
+    from fsdkr.refresh import FsDkrError, FsDkrPanic, _error_of
+    b = CollectBatch(msgs, key, list(joins), 256, KB)
+    v = Verdicts(b.R, b.J, b.n)
+    v.feldman[:], v.pdl[:], v.range[:], v.ped[:], v.ck[:], v.dlog[:] = 1, 7, 1, 1, 1, 3
+    e = _error_of(b.first_error(b.settle(v)))
+    if isinstance(e, FsDkrPanic):
+        return ("panic",)
+    if isinstance(e, FsDkrError):
+        return (e.variant, e.fields)
+    return None
+
+
+def _pdl(msgs, k, i, **kw):
+    m2 = copy.deepcopy(msgs)
+    p = m2[k].pdl_proof_vec[i]
+    m2[k].pdl_proof_vec[i] = dataclasses.replace(p, **{f: g(p) for f, g in kw.items()})
+    return m2
+
+
+def _alice(msgs, k, i, **kw):
+    m2 = copy.deepcopy(msgs)
+    a = m2[k].range_proofs[i]
+    m2[k].range_proofs[i] = dataclasses.replace(a, **{f: g(a) for f, g in kw.items()})
+    return m2
+
+
+CASES = {
+    "pdl_s1": lambda ms: _pdl(ms, 2, 3, s1=lambda p: -p.s1),
+    "pdl_s1_small": lambda ms: _pdl(ms, 0, 1, s1=lambda p: -1),
+    "pdl_u2": lambda ms: _pdl(ms, 1, 0, u2=lambda p: -p.u2),
+    "pdl_u3": lambda ms: _pdl(ms, 3, 2, u3=lambda p: -p.u3),
+    "pdl_u2_u3": lambda ms: _pdl(ms, 3, 3, u2=lambda p: -p.u2, u3=lambda p: -p.u3),
+    "alice_e": lambda ms: _alice(ms, 1, 2, e=lambda a: -a.e),
+    "alice_s1": lambda ms: _alice(ms, 2, 0, s1=lambda a: -a.s1),
+    "alice_s2": lambda ms: _alice(ms, 0, 3, s2=lambda a: -a.s2),
+    "alice_e_z_not_unit": lambda ms: _alice(ms, 1, 1, s1=lambda a: -a.s1, z=lambda a: 0),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_negative_host_rules_match_oracle(dkr4, case):
+    keys, msgs, dks = dkr4
+    m2 = CASES[case](msgs)
+    want = oracle_outcome(m2, keys[0], dks[0])
+    assert want is not None
+    if case == "alice_e_z_not_unit":   # z^e not invertible: false before the s1 panic
+        assert want == ("RangeProof", {"party_index": 1})
+    assert host_outcome(m2, keys[0]) == want
+
+
+def test_negative_ring_pedersen_z(dkr4):
+    keys, msgs, dks = dkr4
+    m2 = copy.deepcopy(msgs)
+    pf = m2[2].ring_pedersen_proof
+    m2[2].ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(-z if k == 7 else z for k, z in enumerate(pf.Z)))
+    assert oracle_outcome(m2, keys[0], dks[0]) == ("panic",)
+    from fsdkr.batch import CollectBatch
+    b = CollectBatch(m2, keys[0], [], 256, KB)
+    lens = np.ctypeslib.as_array(b.c.ped_lens, shape=(len(m2), 2))
+    # Z "ends" at its negative entry: the device's short-Z rule (ped bit1 unless a
+    # check before index 7 fails) -- the GPU test compares the outcome
+    assert lens.tolist() == [[256, 256]] * 2 + [[256, 7]] + [[256, 256]]
+
+
+def test_negative_bases_packed_as_residues(dkr4):
+    """PDL s2 and Alice s are bases of x^N mod N^2: s - N^2 (negative, same residue)
+    is packed as s, so the device sees the valid proof (GPU test: Ok)."""
+    keys, msgs, dks = dkr4
+    key = keys[0]
+    nn = [k.n ** 2 for k in key.paillier_key_vec]
+    m2 = _pdl(msgs, 1, 2, s2=lambda p: p.s2 - nn[2])
+    m2 = _alice(m2, 3, 1, s=lambda a: a.s - 3 * nn[1])
+    assert oracle_outcome(m2, key, dks[0]) is None
+    from fsdkr.batch import CollectBatch
+    from fsdkr._native import limbs_to_ints
+    b = CollectBatch(m2, key, [], 256, KB)
+    P, nl = 16, b.nl
+    s2 = limbs_to_ints(np.ctypeslib.as_array(b.c.pdl_s2, shape=(P, nl)))
+    s = limbs_to_ints(np.ctypeslib.as_array(b.c.rp_s, shape=(P, nl)))
+    assert s2 == [m.pdl_proof_vec[i].s2 for m in msgs for i in range(4)]
+    assert s == [m.range_proofs[i].s for m in msgs for i in range(4)]
+    assert not b.negs.pdl and not b.negs.range and set(b.negs.rows) == {"pdl_s2", "rp_s"}
+    assert host_outcome(m2, key) is None
+
+
+@pytest.mark.parametrize("which", ["y1", "y2"])
+def test_negative_dlog_response(joined, which):
+    keys, msgs, dks, jm = joined
+    j2 = copy.deepcopy(jm)
+    attr = "composite_dlog_proof_base_h1" if which == "y1" else "composite_dlog_proof_base_h2"
+    p = getattr(j2, attr)
+    setattr(j2, attr, dataclasses.replace(p, y=-p.y))
+    want = oracle_outcome(msgs, keys[1], dks[1], [j2])
+    assert want == ("panic",)
+    assert host_outcome(msgs, keys[1], [j2]) == want
+
+
+def test_negative_outside_the_rules_still_unsupported(dkr4):
+    """a negative PDL s3 is an h2^-1 exponent in the reference (a valid value, not a
+    panic): still UnsupportedInput for the batch"""
+    from fsdkr.batch import CollectBatch, UnsupportedInput
+    keys, msgs, dks = dkr4
+    m2 = _pdl(msgs, 0, 0, s3=lambda p: -p.s3)
+    with pytest.raises(UnsupportedInput):
+        CollectBatch(m2, keys[0], [], 256, KB)
+
+
+def test_session_set_moves_negative_sessions_out(dkr4):
+    """SessionSet: a session with a negative operand is packed on its own (its
+    instances get their rules); the others stay in the set-wide gather."""
+    from fsdkr.batch import SessionSet
+    keys, msgs, dks = dkr4
+    m2 = _pdl(msgs, 2, 3, s1=lambda p: -p.s1)
+    for staged in (False, True):
+        ss = SessionSet([(msgs, keys[0], []), (m2, keys[1], []), (msgs, keys[2], [])], 256, KB, staged=staged)
+        if staged:
+            ss.stage1b()
+            ss.stage_z()
+            ss.complete()
+        assert ss.batches[0] is None and ss.batches[2] is None
+        assert ss.batches[1] is not None and ss.batches[1].negs.pdl == {2 * 4 + 3: (8, 0xFF)}
+        assert ss.live == [0, 1, 2]

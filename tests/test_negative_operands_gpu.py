@@ -1,0 +1,126 @@
+"""Negative operands on the GPU path: one
+sender's negative BigInt gets the reference's outcome for that instance --
+the oracle's panic, error or plain residue -- and every other instance of the
+batch is verified as usual.  Each case runs refresh.collect (or collect_many)
+and the oracle (restatement of refresh_message.rs:321-467) on the same
+messages: the outcome (Ok / FsDkrError variant + payload / panic), the
+paillier_key_vec side effects and, on success, the updated LocalKey must be
+identical (helpers of tests/test_edge_outcomes_gpu.py)."""
+import copy
+import dataclasses
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from test_edge_outcomes_gpu import KB, _check, _dkr, _joins_setup  # noqa: E402
+from test_negative_operands import _alice, _pdl  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dkr5():
+    return _dkr(2, 5, "neg-gpu-t2n5")
+
+
+def test_negative_s1_from_one_sender(gpu_ctx, dkr5):
+    """The verdict's case: one sender's PDL s1 < 0 among valid proofs -> that
+    pair's panic (u2_test_tmp = h^s1, zk_pdl_with_slack.rs:139); an earlier
+    failing pair is reported first; the same s1 in another message alone."""
+    keys, msgs, dks, _ = dkr5
+    m2 = _pdl(msgs, 3, 1, s1=lambda p: -p.s1)
+    _check(gpu_ctx, m2, keys[0], dks[0], expect="panic")
+    m3 = _pdl(m2, 1, 4, u2=lambda p: p.u2 + 1)      # pair (1, 4) precedes (3, 1)
+    _check(gpu_ctx, m3, keys[0], dks[0], expect="PDLwSlackProof")
+    m4 = _pdl(msgs, 0, 0, s1=lambda p: -1)
+    _check(gpu_ctx, m4, keys[0], dks[0], expect="panic")
+
+
+def test_negative_pdl_u2_u3(gpu_ctx, dkr5):
+    keys, msgs, dks, _ = dkr5
+    ro = _check(gpu_ctx, _pdl(msgs, 2, 2, u2=lambda p: -p.u2), keys[0], dks[0], expect="PDLwSlackProof")
+    assert ro[1] == {"is_u1_eq": True, "is_u2_eq": False, "is_u3_eq": True}
+    ro = _check(gpu_ctx, _pdl(msgs, 4, 0, u3=lambda p: -p.u3, u2=lambda p: -p.u2), keys[0], dks[0],
+                expect="PDLwSlackProof")
+    assert ro[1] == {"is_u1_eq": True, "is_u2_eq": False, "is_u3_eq": False}
+
+
+def test_negative_alice_operands(gpu_ctx, dkr5):
+    keys, msgs, dks, _ = dkr5
+    _check(gpu_ctx, _alice(msgs, 1, 2, e=lambda a: -a.e), keys[0], dks[0], expect="panic")
+    _check(gpu_ctx, _alice(msgs, 2, 0, s1=lambda a: -a.s1), keys[0], dks[0], expect="panic")
+    _check(gpu_ctx, _alice(msgs, 0, 3, s2=lambda a: -a.s2), keys[0], dks[0], expect="panic")
+    # z^e not invertible (z = 0): false before the negative s1's panic
+    ro = _check(gpu_ctx, _alice(msgs, 1, 1, s1=lambda a: -a.s1, z=lambda a: 0), keys[0], dks[0], expect="RangeProof")
+    assert ro[1] == {"party_index": 1}
+    # the PDL check of the same pair fails first
+    m2 = _pdl(_alice(msgs, 2, 4, e=lambda a: -a.e), 2, 4, u2=lambda p: p.u2 + 1)
+    _check(gpu_ctx, m2, keys[0], dks[0], expect="PDLwSlackProof")
+
+
+def test_negative_bases_are_residues(gpu_ctx, dkr5):
+    """s2 - k N^2 and s - k N^2: the same proof to GMP's mod_pow -> Ok, and the
+    LocalKey is updated exactly as the oracle's."""
+    keys, msgs, dks, _ = dkr5
+    nn = [k.n ** 2 for k in keys[0].paillier_key_vec]
+    m2 = _pdl(msgs, 1, 2, s2=lambda p: p.s2 - nn[2])
+    m2 = _alice(m2, 3, 4, s=lambda a: a.s - 2 * nn[4])
+    assert _check(gpu_ctx, m2, keys[0], dks[0]) is None
+    m3 = _alice(m2, 0, 0, s=lambda a: -a.s)           # a different residue: the proof fails
+    _check(gpu_ctx, m3, keys[0], dks[0], expect="RangeProof")
+
+
+def test_negative_ring_pedersen_z(gpu_ctx, dkr5):
+    keys, msgs, dks, _ = dkr5
+    m2 = copy.deepcopy(msgs)
+    pf = m2[2].ring_pedersen_proof
+    m2[2].ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(-z if k == 40 else z for k, z in enumerate(pf.Z)))
+    _check(gpu_ctx, m2, keys[0], dks[0], expect="panic")
+    m3 = copy.deepcopy(m2)                             # check 3 fails before index 40 is reached
+    pf = m3[2].ring_pedersen_proof
+    m3[2].ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(z + (k == 3) for k, z in enumerate(pf.Z)))
+    _check(gpu_ctx, m3, keys[0], dks[0], expect="RingPedersenProofError")
+
+
+@pytest.mark.parametrize("which", ["y1", "y2"])
+def test_negative_dlog_response(gpu_ctx, which):
+    keys, msgs, dks, jm, _ = _joins_setup("neg-dlog")
+    attr = "composite_dlog_proof_base_h1" if which == "y1" else "composite_dlog_proof_base_h2"
+    j2 = copy.deepcopy(jm)
+    p = getattr(j2, attr)
+    setattr(j2, attr, dataclasses.replace(p, y=-p.y))
+    _check(gpu_ctx, msgs, keys[1], dks[1], [j2], expect="panic")
+    if which == "y2":   # proof 1 fails: proof 2 (and its panic) never runs
+        p1 = j2.composite_dlog_proof_base_h1
+        j2.composite_dlog_proof_base_h1 = dataclasses.replace(p1, x=p1.x + 1)
+        _check(gpu_ctx, msgs, keys[1], dks[1], [j2], expect="DLogProofValidation")
+
+
+def test_collect_many_negative_session_alone(gpu_ctx, dkr5):
+    """collect_many: the session holding a negative s1 panics, the regular
+    sessions around it succeed, each as the oracle says."""
+    from fsdkr import refresh
+    from test_edge_outcomes_gpu import _same_key
+    from oracle import protocol
+    from oracle.rng import Rng
+    keys, msgs, dks, _ = dkr5
+    m2 = _pdl(msgs, 4, 2, s1=lambda p: -p.s1)
+    sessions = [(msgs, 0), (m2, 1), (msgs, 2)]
+    gk = [keys[p].clone() for _, p in sessions]
+    out = refresh.collect_many([(copy.deepcopy(m), k, dks[p], []) for (m, p), k in zip(sessions, gk)],
+                               ctx=gpu_ctx, key_bits=KB)
+    for (m, p), k, o in zip(sessions, gk, out):
+        ko = keys[p].clone()
+        try:
+            protocol.collect(copy.deepcopy(m), ko, dks[p], [], Rng("a8"), KB)
+            want = None
+        except Exception:
+            want = "panic"
+        if want is None:
+            assert o is None, o
+            _same_key(ko, k)
+        else:
+            assert isinstance(o, refresh.FsDkrPanic), o

@@ -17,6 +17,7 @@ prepares the tampered one: every prestarted part the tamper touches must be
 recomputed (fsdkr_collect_reuse_mask), so the verdicts still equal the oracle's
 (this fails if prepare trusted a stale prestart)."""
 import copy
+import dataclasses
 import os
 import sys
 
@@ -124,6 +125,31 @@ def test_timed_path_config2_tampers(gpu_ctx, timed2):
 def test_timed_path_config2_stale_prestart(gpu_ctx, timed2, spec, must_miss):
     msgs, joins, lk, dk = timed2
     _stale_prestart(gpu_ctx, msgs, joins, lk, spec, must_miss)
+
+
+def test_timed_path_config2_negative_operands(gpu_ctx, timed2):
+    """VERDICT r4 item 8 at full size: one sender's negative PDL s1 -> that pair's
+    panic (zk_pdl_with_slack.rs:139), no key written (the PDL loop precedes every
+    write); s2 - N^2 in another pair (GA's base: the same residue) -> Ok, with the
+    LocalKey the clean batch gives."""
+    from fsdkr import refresh
+    msgs, joins, lk, dk = timed2
+    m2 = list(msgs)
+    m = tamper._own(m2, 17)
+    p = m.pdl_proof_vec[9]
+    m.pdl_proof_vec[9] = dataclasses.replace(p, s1=-p.s1)
+    key = copy.deepcopy(lk)
+    with pytest.raises(refresh.FsDkrPanic):
+        refresh.collect(m2, key, dk, joins, ctx=gpu_ctx, key_bits=2048)
+    _check_side_effects(lk, key, m2, joins, ("PDLwSlackProof", {}))
+    m3 = list(msgs)
+    m = tamper._own(m3, 40)
+    p = m.pdl_proof_vec[5]
+    m.pdl_proof_vec[5] = dataclasses.replace(p, s2=p.s2 - lk.paillier_key_vec[5].n ** 2)
+    got, key3 = _collect(gpu_ctx, m3, joins, lk, dk)
+    assert got is None, got
+    ref, key0 = _collect(gpu_ctx, msgs, joins, lk, dk)
+    assert (key3.x_i, key3.y, key3.pk_vec) == (key0.x_i, key0.y, key0.pk_vec)
 
 
 # ------------------------------------------------------------------ configs[3]
