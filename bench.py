@@ -138,23 +138,29 @@ def pmc_per_call(label):
     if not files:
         return None
     d = json.load(open(files[-1]))
-    return d["per_call"]["SQ_INSTS_VALU_INT64"], os.path.relpath(files[-1], REPO)
+    return d["per_call"]["SQ_INSTS_VALU_INT64"], os.path.relpath(files[-1], REPO), d.get("pmc_mac_per_call")
 
 
 def efficiency(work, issued, seconds, world=1, pmc=None):
-    """MAC accounting of a timed step.  algorithmic_equiv_tmac_per_s
-    is the SURVEY work (32-bit limbs, 2k^2+k per modmul, no fixed-base or
-    squaring savings) per second: an equivalent rate, NOT a fraction of the peak
-    (the fixed-base savings alone can put it above the peak).  issued_model_frac
-    models the MACs the kernels issue (collect_issued).  pmc_issued_frac is
-    measured: the step's SQ_INSTS_VALU_INT64 (one committed --pmc pass) x 64
-    lanes over the step time and the v_mad_u64_u32 peak (64-bit integer VALU
-    lane-ops: the MACs and the few 64-bit carry ops of each Montgomery row)."""
-    out = {"algorithmic_mac_per_step": work, "algorithmic_equiv_tmac_per_s": work / seconds / 1e12 / world,
+    """MAC accounting of a timed step.  algorithmic_mac_per_step is
+    the SURVEY work (32-bit limbs, 2k^2+k per modmul, no fixed-base or squaring
+    savings): a work count, not a rate against the peak.  issued_model_frac
+    models the MACs the kernels issue (collect_issued).  Measured (one committed
+    --pmc pass over whole calls at HEAD, tools/pmc_step.py): pmc_issued_frac =
+    SQ_INSTS_VALU_INT64 x 64 lanes over the step time and the v_mad_u64_u32 peak
+    -- every 64-bit integer VALU instruction, i.e. the MACs AND the rows' 64-bit
+    carry shifts / adds; pmc_mac_frac counts only the v_mad_u64_u32 MACs: each
+    kernel's INT64 count times its MAC share from the disassembly of the same
+    build (tools/mac_share.py: the smallest share over its product cycle loops,
+    rolling-normalisation folds excluded)."""
+    out = {"algorithmic_mac_per_step": work,
            "issued_model_mac_per_step": issued, "issued_model_frac": issued / seconds / PEAK_MAC / world}
     if pmc:
         out["pmc_int64_lane_ops_per_step"] = pmc[0] * 64
         out["pmc_issued_frac"] = pmc[0] * 64 / seconds / PEAK_MAC / world
+        if pmc[2]:
+            out["pmc_mac_lane_ops_per_step"] = pmc[2] * 64
+            out["pmc_mac_frac"] = pmc[2] * 64 / seconds / PEAK_MAC / world
         out["pmc_source"] = pmc[1]
     return out
 
@@ -379,7 +385,8 @@ def sessions_bench(ctx, count, steps, seed):
             "proofs_per_step": proofs, "steps": steps, "ms_per_step": el * 1e3, "value": proofs / el,
             "unit": "proofs/s", "sessions_per_s": count / el, "workload_gen_s": gen_s,
             "collect_efficiency": efficiency(count * collect_work(3, 0, 3, k=96),
-                                             count * collect_issued(3, 0, 3, k=96), el),
+                                             count * collect_issued(3, 0, 3, k=96), el,
+                                             pmc=pmc_per_call("c4") if count == 1024 else None),
             "data": "synthetic (seeded GPU prover; keys are distinct products of pairs from a shared prime pool)"}
 
 
@@ -612,10 +619,8 @@ def main():
                                    "kernel's own v_mad_u64_u32 lane-ops (29-bit digits, squaring rows)",
                      "issued": roof["issued_mac_per_s"] / 1e12, "issued_frac": roof["issued_mac_per_s"] / PEAK_MAC,
                      "lanes_per_instance": roof["group"]},
-        "collect_efficiency": dict(efficiency(W_collect, collect_issued(R, J, n), ms_per_step * 1e-3, world,
-                                              pmc=pmc_per_call("n64") if (n, J) == (64, 4) else None),
-                                   device_pipeline_algorithmic_equiv_tmac_per_s=W_collect /
-                                   (ph["device_pipeline_ms"] * 1e-3) / 1e12),
+        "collect_efficiency": efficiency(W_collect, collect_issued(R, J, n), ms_per_step * 1e-3, world,
+                                         pmc=pmc_per_call("n64") if (n, J) == (64, 4) else None),
         "config3": c3,
         "config4_sessions": s4,
         "keygen": kg,

@@ -13,8 +13,10 @@
 #   trace            kernel trace of whole n = 64 collect() calls + timeline of one -> trace_summary.txt
 #   trace4           the same for whole configs[4] collect_many() calls (1024 sessions) -> trace4_summary.txt
 #   trace256         the same for whole n = 256 collect() calls (configs[3])  -> trace256_summary.txt
-#   pmc64 | pmc256   one --pmc pass over whole n = 64 / n = 256 calls (tools/pmc_step.py)
-#                    -> pmc_step_n64.json / pmc_step_n256.json (per-call counter totals)
+#   pmc64 | pmc256 | pmc4   one --pmc pass over whole n = 64 / n = 256 collect() calls or
+#                    configs[4] collect_many() calls (tools/pmc_step.py) -> pmc_step_n64.json /
+#                    pmc_step_n256.json / pmc_step_c4.json (per-call counter totals; with
+#                    tools/mac_share.py's per-kernel MAC shares of this build: pmc_mac_per_call)
 #   pmcmx            PMC passes over the metric-2 modexp launch (tools/pmc.sh)
 #   shard256         bench.py --emulate-shard 2 / 4 / 8 at n = 256 -> shard_n256.jsonl
 #   shard64          the same at n = 64                            -> shard_n64.jsonl
@@ -41,7 +43,12 @@ pmc_step() {   # $1 = label, $2.. = pmc_step.py shape args
      > $OUT/pmc_$label.log 2>&1) || fail "pmc $label" $? $OUT/pmc_$label.log
   local f
   f=$(find $OUT/pmc_$label -name "*counter_collection.csv" | head -1)
-  python3 $R/tools/pmc_summary_step.py "$f" 3 --label $label > $OUT/pmc_step_$label.json || exit 1
+  python3 $R/tools/mac_share.py --out $OUT/mac_share.json 2> $OUT/mac_share.err || echo "mac_share failed (no llvm-objdump?)"
+  if [ -s $OUT/mac_share.json ]; then
+    python3 $R/tools/pmc_summary_step.py "$f" 3 --label $label --mac-share $OUT/mac_share.json > $OUT/pmc_step_$label.json || exit 1
+  else
+    python3 $R/tools/pmc_summary_step.py "$f" 3 --label $label > $OUT/pmc_step_$label.json || exit 1
+  fi
 }
 for step in "$@"; do
   case $step in
@@ -74,6 +81,7 @@ for step in "$@"; do
               python $R/tools/prof_summary.py "$f" --gap 10 --step -1 > $OUT/trace256_summary.txt || exit 1 ;;
     pmc64) pmc_step n64 --n 64 --joins 4 --t 32 ;;
     pmc256) pmc_step n256 --n 256 --joins 0 --t 128 ;;
+    pmc4) pmc_step c4 --sessions 1024 --seed 2028 ;;
     pmcmx) bash $R/tools/pmc.sh $TAG/pmcmx || exit 1 ;;
     shard256|shard64)
       n=${step#shard}; t=$((n / 2)); j=$([ $n = 64 ] && echo 4 || echo 0)

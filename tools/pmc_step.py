@@ -2,9 +2,10 @@
 """PMC target for whole collect() calls (bench.py's step) with no other kernels
 in the process: the synthetic workload is generated once (--gen-only, outside
 the profiler) and pickled to --cache; a profiled run loads it and makes
-1 + --steps refresh.collect() calls, so every dispatch rocprofv3 records
-belongs to a collect() call (tools/pmc_summary_step.py divides the counter
-totals by the call count)."""
+1 + --steps refresh.collect() calls (with --sessions S: refresh.collect_many()
+calls over S independent t=1 n=3 3072-bit sessions, bench.py's configs[4]
+step), so every dispatch rocprofv3 records belongs to one of those calls
+(tools/pmc_summary_step.py divides the counter totals by the call count)."""
 import argparse
 import copy
 import os
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--t", type=int, default=32)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--sessions", type=int, default=0)
     ap.add_argument("--cache", required=True)
     ap.add_argument("--gen-only", action="store_true")
     a = ap.parse_args()
@@ -31,13 +33,26 @@ def main():
     from fsdkr import Context, refresh, synth
     ctx = Context()
     if a.gen_only:
-        msgs, joins, lk = synth.synth_collect(ctx, a.n - a.joins, a.joins, a.t, a.seed)
+        if a.sessions:
+            data = synth.synth_sessions(ctx, a.sessions, n=3, t=1, seed=a.seed, key_bits=3072)
+        else:
+            data = synth.synth_collect(ctx, a.n - a.joins, a.joins, a.t, a.seed)
         with open(a.cache, "wb") as f:
-            pickle.dump((msgs, joins, lk), f)
+            pickle.dump(data, f)
         print(f"workload cached: {a.cache}", flush=True)
         return
     with open(a.cache, "rb") as f:   # written by this script (--gen-only) in the same session
-        msgs, joins, lk = pickle.load(f)
+        data = pickle.load(f)
+    if a.sessions:
+        for k in range(a.steps + 1):
+            work = [(m, copy.deepcopy(lk), dk, j) for (m, j, lk, dk) in data]
+            t0 = time.perf_counter()
+            res = refresh.collect_many(work, ctx=ctx, key_bits=3072)
+            assert all(r is None for r in res)
+            print(f"collect_many {k} {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+        print(f"calls {a.steps + 1}", flush=True)
+        return
+    msgs, joins, lk = data
     keys = [copy.deepcopy(lk) for _ in range(a.steps + 1)]
     for k in range(a.steps + 1):
         t0 = time.perf_counter()

@@ -8,7 +8,11 @@ ms_per_step) it adds the counter-based issue fraction
 i.e. the 64-bit integer VALU lane-operations the chip issued per call
 (v_mad_u64_u32 MACs plus the few 64-bit carry shifts/adds of each Montgomery
 row) against the measured v_mad_u64_u32 peak (profiles/r01_intrates.jsonl).
-Usage: pmc_summary_step.py COUNTER_CSV CALLS [--ms MS] [--label L]"""
+With --mac-share (tools/mac_share.py's JSON for the SAME libfsdkr.so) it adds
+the MAC count: pmc_mac_per_call = sum over kernels of SQ_INSTS_VALU_INT64 x
+that kernel's v_mad_u64_u32 share of its INT64 instructions (kernels absent
+from the file are not credited).
+Usage: pmc_summary_step.py COUNTER_CSV CALLS [--ms MS] [--label L] [--mac-share F]"""
 import argparse
 import collections
 import csv
@@ -23,6 +27,7 @@ def main():
     ap.add_argument("calls", type=int)
     ap.add_argument("--ms", type=float, default=0.0)
     ap.add_argument("--label", default="")
+    ap.add_argument("--mac-share", default="")
     a = ap.parse_args()
     tot = collections.defaultdict(float)
     per_kernel = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -48,7 +53,19 @@ def main():
         out["int64_by_kernel"] = {k: {"int64_per_call": c.get("SQ_INSTS_VALU_INT64", 0.0) / a.calls,
                                       "int64_share": (c.get("SQ_INSTS_VALU_INT64", 0.0) / c["SQ_INSTS_VALU"])
                                       if c.get("SQ_INSTS_VALU") else None}
-                                  for k, c in ks[:16]}
+                                  for k, c in ks}
+        if a.mac_share:
+            ms = json.load(open(a.mac_share))["kernels"]
+            mac = 0.0
+            for k, c in out["int64_by_kernel"].items():
+                r = ms.get(k, {}).get("mac_share_of_int64", 0.0)
+                c["mac_share_of_int64"] = r
+                mac += c["int64_per_call"] * r
+            out["mac_share_source"] = a.mac_share
+            out["pmc_mac_per_call"] = mac
+            out["mac_share_of_int64"] = mac / i64 if i64 else None
+            if a.ms:
+                out["pmc_mac_frac"] = mac * 64 / (a.ms * 1e-3 * PEAK)
     print(json.dumps(out, indent=1))
 
 
