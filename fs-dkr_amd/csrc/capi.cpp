@@ -327,13 +327,13 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   if (grp == kWideGroup && (group != kWideGroup || k32 != 128)) grp = 16;
   if (grp == kWaveGroup && k32 != 128) grp = 16;
   if (c->ct) grp = 0;   // the regular-access kernels have one shape per width
-  // sliding windows: the 4096-bit 4/8/16-lane shapes, public exponents, waves of
+  // sliding windows: the 4096-bit 4/8/16/32-lane shapes, public exponents, waves of
   // `group` lanes uniform (caller), so only at the caller's lane count
   // FSDKR_SLIDE=0: fixed windows (A/B; n = 64 and n = 256 whole calls within
   // noise of each other, profiles/r04/r04h_*: fewer products, more control flow)
   static const bool slide_off = getenv("FSDKR_SLIDE") && atoi(getenv("FSDKR_SLIDE")) == 0;
   const bool slide = !slide_off && (desc_flags & kDescSlide) && (desc_flags & kDescOutIdx) && k32 == 128 && !c->ct &&
-                     grp == group && (grp == 4 || grp == 8 || grp == 16);
+                     grp == group && (grp == 4 || grp == 8 || grp == 16 || grp == kWideGroup);
   const int KD = table_digits(k32, grp);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
@@ -368,8 +368,8 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   a.slide = slide ? 1u : 0u;
   a.out_idx = (desc_flags & kDescOutIdx) ? reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 4 * n4) : nullptr;
   if (split && split->lo_bit) {   // head / tail of split chains: the slide shapes at the caller's lanes
-    if (!slide || grp != group || !(grp == 4 || grp == 8 || grp == 16)) {
-      c->fail("split chains need the 4 / 8 / 16-lane sliding-window shapes (group %u)", grp);
+    if (!slide || grp != group || !(grp == 4 || grp == 8 || grp == 16 || grp == kWideGroup)) {
+      c->fail("split chains need the 4 / 8 / 16 / 32-lane sliding-window shapes (group %u)", grp);
       return FSDKR_E_ARG;
     }
     const std::string base(table_tag);

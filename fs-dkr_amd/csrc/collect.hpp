@@ -489,20 +489,36 @@ inline void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, ui
 // the 16-lane 4096-bit shape issues fewer instructions per row than 8 lanes and
 // fits three waves per SIMD (98 VGPRs): n = 64 (7 680 chains) went from 57.4 to
 // 51.5 ms per call against 8 lanes (profiles/r04/r04d_ab_lanes_v*).  Small
-// batches (multi-GPU shards) get 32 lanes (KD = 160 constants), and at most one
-// wave per SIMD (1024 chains) one wave per chain (modexp_wave_kernel), for
-// latency.  Past 16 384 chains the launch fills the chip several times over and
-// the most MAC-efficient 4-lane shape wins: n = 256 (131 072 chains) 592 ms per
-// call at 8 lanes, 571 ms at 4, 628 ms at 16 (profiles/r04/r04e_ab_n256_lanes_v*).
-// 32 lanes at n = 64: 51 -> 64 ms (profiles/r04/r04g_*).
-// Used by the prestart and by launch().
+// batches (multi-GPU shards) keep 16 lanes too: with the sliding windows and the
+// joint tail (which the one-wave-per-chain modexp_wave_kernel and the fixed-window
+// 32-lane shape lack) an emulated 8-way n = 64 rank-0 call takes 18.6 ms against
+// 22.3 (wave shape) and 20.5-21.2 (32-lane sliding windows), and 4-way ranks
+// 24.0-24.8 against 26.3-26.9 (profiles/r05/r05k_*, r05l_*, r05m_*).  Past 16 384
+// chains the launch fills the chip several times over and the most MAC-efficient
+// 4-lane shape wins: n = 256 (131 072 chains) 592 ms per call at 8 lanes, 571 ms
+// at 4, 628 ms at 16 (profiles/r04/r04e_ab_n256_lanes_v*).  Used by the prestart
+// and by launch().
+// FSDKR_GA_LANES / FSDKR_J2_LANES (4, 8, 16; 32 and 64 at 4096 bits) override the
+// choice (A/B runs).
+inline uint32_t lanes_env(const char* name, uint32_t nn) {
+  const char* e = getenv(name);
+  if (!e) return 0;
+  const uint32_t g = (uint32_t)atoi(e);
+  if (g == 4 || g == 8 || g == 16) return g;
+  if (nn == 128 && (g == kWideGroup || g == kWaveGroup)) return g;
+  return 0;
+}
 inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
-  uint32_t g = nn != 128 ? 8 : count <= 16384u ? 16 : 4;
-  for (uint32_t x : {16u, kWideGroup})
-    if ((uint64_t)count * x <= 65536u) g = x;
-  if (g == kWideGroup && nn != 128) g = 16;
-  if (nn == 128 && count <= 1024) g = kWaveGroup;
-  return g;
+  if (uint32_t e = lanes_env("FSDKR_GA_LANES", nn)) return e;
+  if (nn != 128) return (uint64_t)count * 16 <= 65536u ? 16 : 8;
+  return count <= 16384u ? 16 : 4;
+}
+
+// J2 (c^e mod N^2, 256-bit exponents) lanes per instance, when the joint tail
+// does not absorb it
+inline uint32_t j2_lanes(size_t count, uint32_t nn) {
+  if (uint32_t e = lanes_env("FSDKR_J2_LANES", nn)) return e;
+  return nn == 128 ? (count <= 1024 ? kWaveGroup : count <= 16384 ? 16 : 8) : 8;
 }
 
 // J1 (s2^N_i | s^N_i mod N_i^2) regrouped so the instances of every wave share
@@ -560,14 +576,14 @@ inline bool group_by_exponent(ModexpJob& J, uint32_t per_wave, uint32_t pad_row)
 }
 // the descriptor flags of a regrouped GA job launched with `group` lanes
 inline uint32_t ga_desc_flags(bool aligned_for, uint32_t group) {
-  const bool slide_shape = group == 4 || group == 8 || group == 16;
+  const bool slide_shape = group == 4 || group == 8 || group == 16 || group == kWideGroup;
   return kDescOutIdx | ((aligned_for && slide_shape) ? kDescSlide : 0u);
 }
 
 // GA's joint tail (modexp.hip modexp_tail_kernel): the chains s2^N | s^N mod N^2 run
 // as a head over N's bits >= kGaSplit and a tail that multiplies c^-e_pdl | c^-e_A in
 // along its squarings (e < 2^256), so no separate c^e chain (J2) runs.  For the
-// sliding-window GA shapes (4096-bit, 4 / 8 / 16 lanes); FSDKR_JOINT=0 keeps J2
+// sliding-window GA shapes (4096-bit, 4 / 8 / 16 / 32 lanes); FSDKR_JOINT=0 keeps J2
 // (A/B).  Read per call.
 constexpr uint32_t kGaSplit = 256;
 // GA's issue priority (s_setprio of the prestarted chains and of the joint tail);
@@ -580,7 +596,8 @@ inline bool ga_split_ok(uint32_t nn, uint32_t group, uint32_t flags) {
   const char* j = getenv("FSDKR_JOINT");
   const char* s = getenv("FSDKR_SLIDE");
   if ((j && atoi(j) == 0) || (s && atoi(s) == 0)) return false;
-  return nn == 128 && (flags & kDescSlide) && (flags & kDescOutIdx) && (group == 4 || group == 8 || group == 16);
+  return nn == 128 && (flags & kDescSlide) && (flags & kDescOutIdx) &&
+         (group == 4 || group == 8 || group == 16 || group == kWideGroup);
 }
 // the tail's per-instance descriptor block: base2_ptr u64 | exp2_ptr u64 | exp2_len u32
 constexpr size_t kTailDescBytes = 20;

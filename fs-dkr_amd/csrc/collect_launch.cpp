@@ -48,7 +48,7 @@ int collect_launch_impl(Ctx* c) {
   // instance per wave: its chain is on the critical path of the rank (J2 ->
   // inverses -> equalities); J5 (2048-bit) at 8 lanes (4 lanes measured no
   // better, profiles/r04/r04a_ab_ck_j2j5_v*)
-  const uint32_t j2_group = nn == 128 ? (pl.jcount[2] <= 1024 ? kWaveGroup : pl.jcount[2] <= 16384 ? 16 : 8) : 8;
+  const uint32_t j2_group = j2_lanes(pl.jcount[2], nn);
   const uint32_t j5_group = 8;
   const uint32_t ga_group = ga_lanes(pl.jcount[0], nn);
   uint32_t* cons_nn_w = nullptr;

@@ -741,7 +741,7 @@ static int prestart_chal(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, 
   }
   // the lanes launch() gives them: J2 at 16 lanes (one instance per wave for <= 1024
   // chains), J5 at 8 lanes (collect_launch.cpp)
-  const uint32_t j2_group = nn == 128 ? (J2.size() <= 1024 ? kWaveGroup : J2.size() <= 16384 ? 16 : 8) : 8;
+  const uint32_t j2_group = j2_lanes(J2.size(), nn);
   if ((rc = launch_modexp_desc(c, nn, (uint32_t)J2.size(), J2.exp_bits, dev + o_dJ2, cons_nn,
                                reinterpret_cast<uint32_t*>(dev + x_J2), s2, "mxt_J2pre", 0, j2_group)) ||
       (rc = launch_modexp_desc(c, nl, (uint32_t)J5.size(), J5.exp_bits, dev + o_dJ5, g.fb_cons,

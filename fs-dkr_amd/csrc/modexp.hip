@@ -811,7 +811,12 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
   }
   const bool qs = qs_env == 1;
   if (a.slide) {   // shared exponent per wave: the 4096-bit shapes of GA
-    if (k32 != 128 || a.ct || a.group == kWideGroup || a.group == kWaveGroup) return hipErrorInvalidValue;
+    if (k32 != 128 || a.ct || a.group == kWaveGroup) return hipErrorInvalidValue;
+    if (a.group == kWideGroup) {   // 32 lanes (KD = 160 constants, the caller's): small launches
+      if (a.lo_bit && a.tail)
+        return qs ? launch_modexp_tail<160, 32, 128, true>(a, st) : launch_modexp_tail<160, 32, 128, false>(a, st);
+      return qs ? launch_modexp_slide<160, 32, 128, true>(a, st) : launch_modexp_slide<160, 32, 128, false>(a, st);
+    }
     if (a.lo_bit) {   // split chains: head and tail at the caller's lanes, QS as the full chain's
       switch (a.group) {
         case 16: return a.tail ? (qs ? launch_modexp_tail<144, 16, 128, true>(a, st) : launch_modexp_tail<144, 16, 128, false>(a, st))

@@ -269,7 +269,9 @@ int fsdkr_modexp_joint_batch(fsdkr_ctx* ctx, uint32_t count, const uint32_t* bas
       c->fail("fsdkr_modexp_joint_batch: mod_idx[%u] out of range", i);
       return FSDKR_E_ARG;
     }
-  const uint32_t group = (c->modexp_group == 8 || c->modexp_group == 4) ? c->modexp_group : 16u, per_wave = 64 / group;
+  const uint32_t group = (c->modexp_group == 8 || c->modexp_group == 4 || c->modexp_group == kWideGroup)
+                             ? c->modexp_group : 16u,
+                 per_wave = 64 / group;
   const size_t o_b = 0, o_b2 = al256((size_t)count * K * 4), o_e2 = o_b2 + al256((size_t)count * K * 4),
                o_m = o_e2 + al256((size_t)count * E2L * 4), o_me = o_m + al256((size_t)n_mod * K * 4),
                o_out = o_me + al256((size_t)n_mod * exp_limbs * 4), o_desc = o_out + al256(((size_t)count + 1) * K * 4);
@@ -314,7 +316,9 @@ int fsdkr_modexp_joint_batch(fsdkr_ctx* ctx, uint32_t count, const uint32_t* bas
       (rc = up(o_desc2, desc2.data(), desc2.size())))
     return rc;
   uint32_t* cons = nullptr;
-  if ((rc = setup_moduli(c, K, reinterpret_cast<const uint32_t*>(dev + o_m), n_mod, &cons, "joint"))) return rc;
+  if ((rc = setup_moduli(c, K, reinterpret_cast<const uint32_t*>(dev + o_m), n_mod, &cons,
+                         group == kWideGroup ? "joint_w" : "joint", group == kWideGroup ? kWideGroup : 0u)))
+    return rc;
   const uint32_t flags = ga_desc_flags(true, group);
   SplitArgs head;
   head.lo_bit = LO;

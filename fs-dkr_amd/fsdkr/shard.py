@@ -20,6 +20,7 @@ verdicts to the reference's first error on a header-only batch of the whole
 message set (threshold, sizes, party indices, ek.n) and applies collect()'s
 side effects and the merged share recovery on every rank."""
 import os
+import time
 
 import numpy as np
 
@@ -152,10 +153,25 @@ def merge(dist, local_vec, device=None):
     return t.cpu().numpy()
 
 
-def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=2048, launch_only=False):
+class _Clock:
+    """phase durations (ms) of one rank's call into `out` (None: no timing)"""
+
+    def __init__(self, out):
+        self.out = out
+        self.t = time.perf_counter()
+
+    def __call__(self, name):
+        if self.out is not None:
+            now = time.perf_counter()
+            self.out[name] = self.out.get(name, 0.0) + (now - self.t) * 1e3
+            self.t = now
+
+
+def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=2048, launch_only=False, clock=None):
     """This rank's slice as a CollectBatch (n_recv = n); launched on the GPU.
     Returns (batch or None, verdicts or None); with launch_only the caller
     finishes it (ctx.collect_finish) after overlapping host work."""
+    clock = clock or _Clock(None)
     R, J = len(msgs), len(joins)
     n = R + J
     r0, r1 = shard_range(R, world, rank)
@@ -169,51 +185,63 @@ def verify_slice(ctx, msgs, lk, joins, world, rank, m_security=256, key_bits=204
     if hasattr(ctx, "set_cu_split"):
         ctx.set_cu_split(GA_SPLIT_CUS if 2 * (r1 - r0) * n <= GA_SPLIT_MAX_CHAINS else 0)
     b = CollectBatch(msgs[r0:r1], lk, joins[j0:j1], m_security, key_bits, n_recv=n, staged=True)
+    clock("slice_stage1_ms")
     if b.header_only:   # an empty refresh slice (joins only) or a size failure the header batch reports
         return None, None
     from .refresh import prestart
     prestart(ctx, b)   # the long chains start while stage 2 packs
+    clock("prestart_ms")
     b.complete()
+    clock("slice_stage2_ms")
     ctx.collect_prepare(b)
+    clock("prepare_ms")
     ctx.collect_launch()
+    clock("launch_ms")
     if launch_only:
         return b, None
     return b, ctx.collect_finish(b)
 
 
 def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, device=None, m_security=256,
-            key_bits=2048, recovery="speculative"):
+            key_bits=2048, recovery="speculative", timings=None):
     """RefreshMessage::collect (refresh_message.rs:321-467) sharded over the ranks of
     `dist` (torch.distributed, initialised): every rank holds every message (the
     broadcast channel of README.md:19) and the same LocalKey; each verifies its
     slice, the verdict bytes are all-reduced once, and every rank returns the
     reference's outcome: None after updating `local_key` as collect() does, or
     raises the FsDkrError / FsDkrPanic collect() raises (with its partial
-    paillier_key_vec updates).  `recovery` as in refresh.collect."""
+    paillier_key_vec updates).  `recovery` as in refresh.collect.  `timings`
+    (a dict) receives this rank's host phases in ms (bench.py --emulate-shard)."""
     from .refresh import _check_mode, _conclude, _finish_both, _mapped, _recover_after, _speculative_launch
+    clock = _Clock(timings)
     _check_mode(recovery)
     world, rank = dist.get_world_size(), dist.get_rank()
     msgs, joins = list(refresh_messages), list(join_messages)
     R, J = len(msgs), len(joins)
     n = R + J
     header = CollectBatch(msgs, local_key, joins, m_security, key_bits, header_only=True)
+    clock("header_ms")
     job = (msgs, local_key, n)
     spec = None
     if header.size_fail:
         merged = None
     else:
-        b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True)
+        b, _ = verify_slice(ctx, msgs, local_key, joins, world, rank, m_security, key_bits, launch_only=True,
+                            clock=clock)
         rows, decrypt = shard_range(n, world, rank), rank == DEC_RANK
         pend = None
         try:   # this rank's part of the share recovery overlaps its pipeline on the recovery stream
             if recovery == "speculative":
                 pend = _speculative_launch(ctx, [job + (rows, decrypt)])
+            clock("recovery_launch_ms")
         finally:   # neither the slice nor the recovery stays in flight
             v, specs = _finish_both(ctx, (lambda: ctx.collect_finish(b)) if b is not None else (lambda: None), pend)
+        clock("finish_wait_ms")
         vec = scatter(v, R, J, n, world, rank)
         if recovery == "speculative":
             vec = np.concatenate([vec, encode_recovery(specs[0], n, rows, decrypt)])
         mvec = merge(dist, vec, device)
+        clock("merge_ms")
         G = global_len(R, J, n)
         merged = MergedVerdicts(mvec[:G], R, J, n)
         if recovery == "speculative":
@@ -222,5 +250,6 @@ def collect(dist, refresh_messages, local_key, new_dk, join_messages, ctx, devic
     if recovery == "after" or header.size_fail:
         spec = _recover_after(ctx, [job], [err])[0]
     err = _conclude(local_key, new_dk, msgs, joins, err, applied, spec)
+    clock("conclude_ms")
     if err is not None:
         raise err

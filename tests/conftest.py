@@ -22,3 +22,14 @@ def gpu_ctx():
     ctx = Context(timing=True)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(autouse=True)
+def _whole_chip(request):
+    """Each test starts on the whole chip: a shard test's GA CU split
+    (shard.verify_slice -> fsdkr_ctx_set_cu_split) stays on the shared context,
+    and tests that drive prestart / prepare directly (not refresh.collect, which
+    resets it) would otherwise inherit it."""
+    if "gpu_ctx" in request.fixturenames:
+        request.getfixturevalue("gpu_ctx").set_cu_split(0)
+    yield

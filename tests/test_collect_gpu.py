@@ -404,6 +404,9 @@ def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field, monkeypatch):
     from fsdkr.refresh import prestart
     monkeypatch.setenv("FSDKR_STAGE1C", "1")   # both stages are opt-in (profiles/r05/r05c_ab_*)
     monkeypatch.setenv("FSDKR_FBX", "1")
+    # the challenge jobs include the c^e chains (J2), which GA's joint tail replaces
+    # on the sliding-window shapes: this test runs the separate-J2 path
+    monkeypatch.setenv("FSDKR_JOINT", "0")
     keys, msgs, dks, _ = _dkr(1, 3, "prestart-chal")
     lk = keys[0]
     a = CollectBatch(msgs, lk, [], 256, KB, staged=True)

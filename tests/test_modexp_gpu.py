@@ -122,14 +122,15 @@ def test_modexp_regular_access_equals_plain(gpu_ctx, limbs):
     assert got == gpu_ctx.modexp_batch(bases, exps, mods, idx, limbs)
 
 
-@pytest.mark.parametrize("group", [4, 8, 16])
+@pytest.mark.parametrize("group", [4, 8, 16, 32])
 def test_modexp_joint_split_chains(gpu_ctx, group):
     """collect()'s GA chains split into a head (the exponent's bits >= 256) and a
     joint tail that multiplies base2^exp2 in along the tail's squarings
     (fsdkr_modexp_joint_batch): bit-exact against Python for s^N * (c^-1)^e mod N^2
     shapes, exponents N shared per modulus (waves padded), exp2 = 0 / 1 / full 256
     bits, base2 = 1, bases above N^2, and exponents shorter than the split point
-    (E < 2^256, E = 0: the head only builds the table or nothing)."""
+    (E < 2^256, E = 0: the head only builds the table or nothing).  32 lanes: the
+    KD = 160 shape small launches (multi-GPU shards) take."""
     rnd = random.Random(4242 + group)
     Ns = [_odd(rnd, 2048) for _ in range(4)]
     mods = [n * n for n in Ns]
