@@ -531,23 +531,23 @@ def main():
         for k in range(a.warmup):
             shard.collect(_Rank0(), msgs, keys[k], new_dk, joins, ctx, key_bits=a.key_bits)
         torch.cuda.synchronize()
-        tot, phases = 0.0, {}
+        tot, rank_ph = 0.0, {}
         for k in range(a.steps):
             if a.gap_ms:   # idle gap between steps so a kernel trace can be cut per step
                 time.sleep(a.gap_ms * 1e-3)
             t0 = time.perf_counter()
             shard.collect(_Rank0(), msgs, keys[a.warmup + k], new_dk, joins, ctx, key_bits=a.key_bits,
-                          timings=phases)
+                          timings=rank_ph)
             torch.cuda.synchronize()
             tot += time.perf_counter() - t0
         full_ms = tot / a.steps * 1e3
-        phases = {k: v / a.steps for k, v in phases.items()}
+        rank_ph = {k: v / a.steps for k, v in rank_ph.items()}
         span = ctx.collect_last_span_ms() if hasattr(ctx, "collect_last_span_ms") else None
-        host = sum(v for k, v in phases.items() if k != "finish_wait_ms")
+        host = sum(v for k, v in rank_ph.items() if k != "finish_wait_ms")
         print(json.dumps({"emulated_shard": a.emulate_shard, "note": "emulated rank 0 of a W-way shard on one GPU, "
                           "not a scaling curve", "refresh_slice": [r0, r1], "join_slice": [j0, j1],
                           "device_ms_per_step": dev_ms, "rank0_collect_ms_per_step": full_ms,
-                          "rank0_phases_ms": phases, "rank0_host_ms": host, "rank0_device_span_ms": span}),
+                          "rank0_phases_ms": rank_ph, "rank0_host_ms": host, "rank0_device_span_ms": span}),
               flush=True)
         return
     keys = [copy.deepcopy(lk) for _ in range(a.warmup + a.steps)]   # a fresh LocalKey per collect()
