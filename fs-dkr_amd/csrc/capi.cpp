@@ -649,9 +649,42 @@ int fsdkr_mod_inverse(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const 
       (rc = c->hip_check(hipMemcpyAsync(d_yp, ptrs.data(), ptrs.size() * 8, hipMemcpyHostToDevice, c->stream),
                          "H2D ptrs")))
     return rc;
-  InverseArgs a{d_yp, d_mp, d_o, d_u, nullptr, count};
+  // instances sharing a modulus (equal rows) are inverted together (Montgomery's
+  // simultaneous inversion, inverse_batch_kernel) where the width has that shape
+  std::vector<uint32_t> order(count), gstart;
+  for (uint32_t i = 0; i < count; ++i) order[i] = i;
+  const size_t kd = batch_inv_on() ? inverse_batch_scratch_words(mod_limbs) : 0;
+  if (kd) {
+    auto row = [&](uint32_t i) { return m + (size_t)i * mod_limbs; };
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y2) {
+      return memcmp(row(x), row(y2), 4 * (size_t)mod_limbs) < 0;
+    });
+    for (uint32_t t = 0; t < count; ++t)
+      if (t == 0 || memcmp(row(order[t]), row(order[t - 1]), 4 * (size_t)mod_limbs) != 0) gstart.push_back(t);
+    gstart.push_back(count);
+  }
   c->mark("inverse", true);
-  rc = c->hip_check(launch_inverse(mod_limbs, a, c->stream), "inverse launch");
+  if (kd && gstart.size() - 1 < count) {
+    uint8_t* g = (uint8_t*)c->buf("inv_grp", 4 * ((size_t)count + gstart.size()) + 1024);
+    uint32_t* scr = (uint32_t*)c->buf("inv_grp_scratch", (size_t)count * kd * 4);
+    if (!g || !scr) {
+      c->fail("fsdkr_mod_inverse: device allocation failed");
+      return FSDKR_E_OOM;
+    }
+    uint32_t* d_ord = (uint32_t*)g;
+    uint32_t* d_gs = d_ord + count;
+    if ((rc = c->hip_check(hipMemcpyAsync(d_ord, order.data(), 4 * (size_t)count, hipMemcpyHostToDevice, c->stream),
+                           "H2D order")) ||
+        (rc = c->hip_check(hipMemcpyAsync(d_gs, gstart.data(), 4 * gstart.size(), hipMemcpyHostToDevice, c->stream),
+                           "H2D groups")))
+      return rc;
+    BatchInverseArgs b{d_yp, d_mp, d_ord, d_gs, d_o, d_u, scr, (uint32_t)gstart.size() - 1};
+    rc = c->hip_check(launch_inverse_batch(mod_limbs, b, c->stream), "batch inverse launch");
+    if (!rc) rc = c->sync();   // (the host order / group vectors go out of scope)
+  } else {
+    InverseArgs a{d_yp, d_mp, d_o, d_u, nullptr, count};
+    rc = c->hip_check(launch_inverse(mod_limbs, a, c->stream), "inverse launch");
+  }
   c->mark("inverse", false);
   if (rc) return rc;
   if (out && (rc = c->hip_check(hipMemcpyAsync(out, d_o, nb, hipMemcpyDeviceToHost, c->stream), "D2H inv")))

@@ -294,6 +294,10 @@ struct CollectPlan {
   size_t d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_eqck, d_eqckm, d_p3nn, d_p3nl,
       d_p3m, d_ahn, d_ahc, d_alpre;
   uint32_t n_inv_nn = 0, n_eq_nn = 0, n_eq_nl = 0, n_eq_ck = 0;
+  // the pairs grouped by receiver (Montgomery's simultaneous inversion of the
+  // per-pair inverses: c^-1 mod N_i^2, (z^e)^-1 mod Ñ_i; inverse_batch_kernel)
+  size_t d_binv_order = 0, d_binv_gstart = 0;
+  uint32_t binv_ngroups = 0;
   // host-side pre-verdicts
   std::vector<uint32_t> cpdl_extra;
   std::vector<uint8_t> ck_pre, dlog_pre;   // dlog_pre: bit0 / bit1 per proof

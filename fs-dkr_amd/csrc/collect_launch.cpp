@@ -98,13 +98,30 @@ int collect_launch_impl(Ctx* c) {
   // (1) chains that need only the inputs and the moduli constants start at once
   hipEvent_t consts_ready;
   if ((rc = fork(st, &consts_ready))) return rc;
+  // per-pair inverses (one per pair, in pair order): Montgomery's simultaneous
+  // inversion per receiver where the width has the shape, else one inverse each
+  auto pair_inverse = [&](uint32_t k32, const uint64_t* y, const uint64_t* m, uint32_t* out, uint32_t* unit,
+                          uint32_t count, hipStream_t s, const char* scratch_tag, const char* what) -> int {
+    const size_t kd = inverse_batch_scratch_words(k32);
+    if (batch_inv_on() && kd && count == P && pl.binv_ngroups) {
+      uint32_t* scr = (uint32_t*)c->buf(scratch_tag, (size_t)count * kd * 4);
+      if (!scr) {
+        c->fail("device allocation failed (inverse scratch)");
+        return FSDKR_E_OOM;
+      }
+      BatchInverseArgs b{y, m, (const uint32_t*)(dev + pl.d_binv_order), (const uint32_t*)(dev + pl.d_binv_gstart),
+                         out, unit, scr, pl.binv_ngroups};
+      return c->hip_check(launch_inverse_batch(k32, b, s), what);
+    }
+    InverseArgs a{y, m, out, unit, nullptr, count};
+    return c->hip_check(launch_inverse(k32, a, s), what);
+  };
   hipEvent_t inv_done = nullptr;
   if (pl.joint) {   // c^-1 mod N^2 of every pair: c's unit flag, and the joint tail's base2
     hipStream_t s2 = c->side_stream(2);
-    InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
-                  PX(pl.x_unn), nullptr, pl.n_inv_nn};
     c->mark("inverse", true, s2);
-    rc = c->hip_check(launch_inverse(nn, a, s2), "inverse c");
+    rc = pair_inverse(nn, (const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
+                      PX(pl.x_unn), pl.n_inv_nn, s2, "binv_nn", "inverse c");
     c->mark("inverse", false, s2);
     if (rc || (rc = fork(s2, &inv_done))) return rc;
   }
@@ -236,15 +253,14 @@ int collect_launch_impl(Ctx* c) {
   if (!pl.ch_hit) {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses (else prestarted)
     hipStream_t js = st;
     if ((rc = launch_group(3, js, prio[3], j5_group, cons_nl))) return rc;
-    InverseArgs b1{(const uint64_t*)(dev + pl.d_iynl), (const uint64_t*)(dev + pl.d_imnl), PX(pl.x_invz),
-                   PX(pl.x_uzA), nullptr, P};
     c->mark("inverse", true, js);
-    rc = c->hip_check(launch_inverse(nl, b1, js), "inverse nl");
+    rc = pair_inverse(nl, (const uint64_t*)(dev + pl.d_iynl), (const uint64_t*)(dev + pl.d_imnl), PX(pl.x_invz),
+                      PX(pl.x_uzA), P, js, "binv_nl", "inverse nl");
     c->mark("inverse", false, js);
     if (rc) return rc;
-    InverseArgs b2{(const uint64_t*)(dev + pl.d_iynl) + P, (const uint64_t*)(dev + pl.d_imnl) + P, nullptr,
-                   PX(pl.x_uzp), nullptr, P};
-    if ((rc = c->hip_check(launch_inverse(nl, b2, js), "inverse nl 2"))) return rc;
+    if ((rc = pair_inverse(nl, (const uint64_t*)(dev + pl.d_iynl) + P, (const uint64_t*)(dev + pl.d_imnl) + P,
+                           nullptr, PX(pl.x_uzp), P, js, "binv_nl", "inverse nl 2")))
+      return rc;
   }
   for (hipEvent_t ev : done) {
     (void)hipStreamWaitEvent(st, ev, 0);

@@ -845,6 +845,22 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   }
   const size_t d_iynn = put(inv_y_nn.data(), inv_y_nn.size() * 8), d_imnn = put(inv_m_nn.data(), inv_m_nn.size() * 8);
   const size_t d_iynl = put(inv_y_nl.data(), inv_y_nl.size() * 8), d_imnl = put(inv_m_nl.data(), inv_m_nl.size() * 8);
+  // the pairs by receiver (counting sort): the groups of the simultaneous inversions
+  {
+    uint32_t nrecv = 0;
+    for (uint32_t r : recv_of_pair) nrecv = std::max(nrecv, r + 1);
+    std::vector<uint32_t> cnt((size_t)nrecv + 1, 0), order(P), gstart;
+    for (uint32_t r : recv_of_pair) ++cnt[r + 1];
+    for (size_t r = 1; r <= nrecv; ++r) cnt[r] += cnt[r - 1];
+    gstart.reserve((size_t)nrecv + 1);
+    for (size_t r = 0; r < nrecv; ++r)
+      if (cnt[r + 1] > cnt[r]) gstart.push_back(cnt[r]);
+    gstart.push_back(P);
+    for (uint32_t p = 0; p < P; ++p) order[cnt[recv_of_pair[p]]++] = p;
+    pl.binv_ngroups = (uint32_t)gstart.size() - 1;
+    pl.d_binv_order = put(order.data(), order.size() * 4);
+    pl.d_binv_gstart = put(gstart.data(), gstart.size() * 4);
+  }
   // the fixed-base rows (J3, J4, RP): the prestart's (fx_hit) or this plan's outputs
   const GaPre* gfx = reinterpret_cast<const GaPre*>(c->ga_pre);
   auto J3_row = [&](size_t k) {

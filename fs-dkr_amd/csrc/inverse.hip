@@ -107,26 +107,27 @@ struct Coop {
   }
 };
 
+// The inverse of one instance by its G lanes: Y (value, K32 u32 limbs, any
+// pointer: global or LDS), Mo (odd modulus); O (K32 limbs) receives y^-1 mod m
+// when not null; `mir` is the instance's 2 NLT-word LDS mirror.  Returns the
+// unit flag (gcd(y, m) == 1), group-uniform.
 template <int K32, int G>
-__global__ __launch_bounds__(256) void inverse_coop_kernel(const InverseArgs a) {
-  constexpr int NLT0 = (32 * K32 + 29) / 30 + 1;
-  constexpr int LL = (NLT0 + G - 1) / G;
-  constexpr int NLT = LL * G;
-  constexpr int IPB = 256 / G;
-  __shared__ uint32_t lds[IPB * 2 * NLT];
-  const int g = threadIdx.x % G;
-  const int li = threadIdx.x / G;
-  const uint32_t inst = blockIdx.x * IPB + li;
-  if (inst >= a.count) return;
-  uint32_t* mir = lds + li * 2 * NLT;       // [a | b] mirror for the approximations
+struct CoopShape {
+  static constexpr int NLT0 = (32 * K32 + 29) / 30 + 1;
+  static constexpr int LL = (NLT0 + G - 1) / G;
+  static constexpr int NLT = LL * G;
+};
+
+template <int K32, int G>
+__device__ bool coop_inverse(const uint32_t* Y, const uint32_t* Mo, uint32_t* O, uint32_t* mir, int g) {
+  constexpr int LL = CoopShape<K32, G>::LL;
+  constexpr int NLT = CoopShape<K32, G>::NLT;
   Coop<G, LL> C;
   C.g = g;
   C.m_first = (g == 0) ? 0u : 0xFFFFFFFFu;
   C.m_top = (g == G - 1) ? 0u : 0xFFFFFFFFu;
   asm volatile("" : "+v"(C.m_first), "+v"(C.m_top));
 
-  const uint32_t* Y = reinterpret_cast<const uint32_t*>(a.y_ptr[inst]);
-  const uint32_t* Mo = reinterpret_cast<const uint32_t*>(a.m_ptr[inst]);
   uint32_t A[LL], B[LL], U[LL], V[LL], Mx[LL];
 #pragma unroll
   for (int j = 0; j < LL; ++j) {
@@ -246,17 +247,187 @@ __global__ __launch_bounds__(256) void inverse_coop_kernel(const InverseArgs a) 
 #pragma unroll
   for (int j = 0; j < LL; ++j) nz |= (g == 0 && j == 0) ? (B[j] ^ 1u) : B[j];
   nz = C.group_or(nz);
-  if (g == 0) a.unit[inst] = nz ? 0u : 1u;
-  if (a.out) {
+  if (O) {
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int j = 0; j < LL; ++j) mir[g * LL + j] = V[j];
     __builtin_amdgcn_wave_barrier();
-    uint32_t* O = a.out + (size_t)inst * K32;
     for (int k = g; k < K32; k += G) {
       const int bit = 32 * k, j = bit / 30, s = bit % 30;
       const uint64_t d0 = mir[j], d1 = (j + 1 < NLT) ? mir[j + 1] : 0u, d2 = (j + 2 < NLT) ? mir[j + 2] : 0u;
       O[k] = (uint32_t)((d0 | (d1 << 30) | (d2 << 60)) >> s);
     }
+    __builtin_amdgcn_wave_barrier();
+  }
+  return nz == 0;
+}
+
+template <int K32, int G>
+__global__ __launch_bounds__(256) void inverse_coop_kernel(const InverseArgs a) {
+  constexpr int NLT = CoopShape<K32, G>::NLT;
+  constexpr int IPB = 256 / G;
+  __shared__ uint32_t lds[IPB * 2 * NLT];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t inst = blockIdx.x * IPB + li;
+  if (inst >= a.count) return;
+  uint32_t* mir = lds + li * 2 * NLT;       // [a | b] mirror for the approximations
+  const uint32_t* Y = reinterpret_cast<const uint32_t*>(a.y_ptr[inst]);
+  const uint32_t* Mo = reinterpret_cast<const uint32_t*>(a.m_ptr[inst]);
+  const bool unit = coop_inverse<K32, G>(Y, Mo, a.out ? a.out + (size_t)inst * K32 : nullptr, mir, g);
+  if (g == 0) a.unit[inst] = unit ? 1u : 0u;
+}
+
+// Montgomery's simultaneous inversion over the instances of one modulus (one
+// group of G lanes per modulus).  With mont(a, b) = a b / R and raw values:
+//   P'_1 = y_1,  P'_k = mont(P'_{k-1}, y_k) = (y_1 .. y_k) R^-(k-1)
+//   I_m  = P'_m^-1 (one binary-GCD inverse, coop_inverse)
+//   y_k^-1 = mont(P'_{k-1}, I_k),  I_{k-1} = mont(I_k, y_k),  y_1^-1 = I_1
+// so m elements cost 3 (m - 1) products and one inverse instead of m inverses,
+// with no conversion into or out of Montgomery form.  The values are exact
+// (carry_exact + sub_if_ge on every output).  gcd(P'_m, N) = 1 iff every y_k is a
+// unit; otherwise every element of the group is inverted on its own (the unit
+// flags and values the reference's per-element mod_inv gives).  Even moduli
+// (no Montgomery form) take the per-element path too.
+template <int KD, int G, int K32>
+__global__ __launch_bounds__(64) void inverse_batch_kernel(const BatchInverseArgs a) {
+  using MT = Mont29<KD, G>;
+  constexpr int L = MT::L;
+  constexpr int NLT = CoopShape<K32, G>::NLT;
+  constexpr int IPB = 64 / G;
+  constexpr int W = KD + 2 * NLT + K32;
+  constexpr int LO = K32 / G;
+  __shared__ uint32_t lds[IPB * W];
+  const int g = threadIdx.x % G;
+  const int li = threadIdx.x / G;
+  const uint32_t grp = blockIdx.x * IPB + li;
+  if (grp >= a.ngroups) return;
+  uint32_t* stream = lds + li * W;      // the streamed product operand (KD digits)
+  uint32_t* mir = stream + KD;          // coop_inverse's mirror
+  uint32_t* limbs = mir + 2 * NLT;      // u32 limbs of the inverse's operand / result
+  const uint32_t s0 = a.gstart[grp], s1 = a.gstart[grp + 1];
+  if (s1 <= s0) return;
+  auto Yp = [&](uint32_t t) { return reinterpret_cast<const uint32_t*>(a.y_ptr[a.order[t]]); };
+  const uint32_t* Mo = reinterpret_cast<const uint32_t*>(a.m_ptr[a.order[s0]]);
+  auto put_out = [&](uint32_t t, const uint32_t* x) {   // exact digits x -> u32 limbs of instance order[t]
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < L; ++j) stream[g * L + j] = x[j];
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* O = a.out + (size_t)a.order[t] * K32;
+#pragma unroll
+    for (int k = 0; k < LO; ++k) O[g * LO + k] = limb_of(stream, KD, g * LO + k);
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto per_element = [&]() {
+    for (uint32_t t = s0; t < s1; ++t) {
+      const uint32_t i = a.order[t];
+      const bool u = coop_inverse<K32, G>(Yp(t), Mo, a.out ? a.out + (size_t)i * K32 : nullptr, mir, g);
+      if (g == 0) a.unit[i] = u ? 1u : 0u;
+    }
+  };
+  if ((Mo[0] & 1u) == 0u || s1 - s0 == 1) {   // even modulus, or one element: nothing to share
+    per_element();
+    return;
+  }
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = digit_of(Mo, K32, g * L + j);
+  {
+    const uint32_t n0 = Mo[0];
+    uint32_t inv = n0;
+#pragma unroll
+    for (int it = 0; it < 5; ++it) inv *= 2u - n0 * inv;   // N^-1 mod 2^32
+    M.ninv = (0u - inv) & M29;
+  }
+  uint32_t* S = a.scratch;
+  // ---- prefix products P'_k (scratch row t holds P'_{t - s0 + 1})
+  uint32_t acc[L];
+  {
+    const uint32_t* Y = Yp(s0);
+#pragma unroll
+    for (int j = 0; j < L; ++j) acc[j] = digit_of(Y, K32, g * L + j);
+  }
+#pragma unroll
+  for (int j = 0; j < L; ++j) S[(size_t)s0 * KD + g * L + j] = acc[j];
+  for (uint32_t t = s0 + 1; t < s1; ++t) {
+    const uint32_t* Y = Yp(t);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < L; ++j) stream[g * L + j] = digit_of(Y, K32, g * L + j);
+    __builtin_amdgcn_wave_barrier();
+    M.mul(acc, acc, stream);
+#pragma unroll
+    for (int j = 0; j < L; ++j) S[(size_t)t * KD + g * L + j] = acc[j];
+  }
+  // ---- one inverse of the product (exact u32 limbs in and out, through LDS)
+  M.carry_exact(acc);
+  M.sub_if_ge(acc);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < L; ++j) stream[g * L + j] = acc[j];
+  __builtin_amdgcn_wave_barrier();
+  for (int k = g; k < K32; k += G) limbs[k] = limb_of(stream, KD, k);
+  __builtin_amdgcn_wave_barrier();
+  if (!coop_inverse<K32, G>(limbs, Mo, limbs, mir, g)) {   // group-uniform
+    per_element();
+    return;
+  }
+  // every element is a unit
+  for (uint32_t t = s0 + g; t < s1; t += G) a.unit[a.order[t]] = 1u;
+  if (!a.out) return;
+  // ---- backward pass: y_k^-1 = mont(P'_{k-1}, I_k), I_{k-1} = mont(I_k, y_k)
+  uint32_t I[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) I[j] = digit_of(limbs, K32, g * L + j);
+  for (uint32_t t = s1 - 1; t > s0; --t) {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < L; ++j) stream[g * L + j] = S[(size_t)(t - 1) * KD + g * L + j];
+    __builtin_amdgcn_wave_barrier();
+    uint32_t x[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) x[j] = I[j];
+    M.mul(x, x, stream);
+    M.carry_exact(x);
+    M.sub_if_ge(x);
+    put_out(t, x);
+    const uint32_t* Y = Yp(t);
+#pragma unroll
+    for (int j = 0; j < L; ++j) stream[g * L + j] = digit_of(Y, K32, g * L + j);
+    __builtin_amdgcn_wave_barrier();
+    M.mul(I, I, stream);
+  }
+  M.carry_exact(I);
+  M.sub_if_ge(I);
+  put_out(s0, I);
+}
+
+template <int KD, int G, int K32>
+static hipError_t launch_batch(const BatchInverseArgs& a, hipStream_t st) {
+  constexpr int IPB = 64 / G;
+  const uint32_t blocks = (a.ngroups + IPB - 1) / IPB;
+  hipLaunchKernelGGL((inverse_batch_kernel<KD, G, K32>), dim3(blocks), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+// the 2048 / 4096-bit widths (2048-bit keys: Ñ and N^2); others: 0 (per-element
+// inverse_coop; their 8-lane Montgomery and inverse shapes do not share a lane count)
+size_t inverse_batch_scratch_words(uint32_t k32) {
+  switch (k32) {
+    case 64: return 72;
+    case 128: return 144;
+    default: return 0;
+  }
+}
+
+hipError_t launch_inverse_batch(uint32_t k32, const BatchInverseArgs& a, hipStream_t st) {
+  if (!a.ngroups) return hipSuccess;
+  switch (k32) {
+    case 64: return launch_batch<72, 8, 64>(a, st);
+    case 128: return launch_batch<144, 8, 128>(a, st);
+    default: return hipErrorInvalidValue;
   }
 }
 

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -41,6 +42,22 @@ struct InverseArgs {
   uint32_t* unit;           // [count] 1 if gcd(y, m) == 1
   uint32_t* scratch;        // unused (lane-cooperative inverse keeps its state in registers)
   uint32_t count;
+};
+
+// Montgomery's simultaneous inversion: the instances of one modulus (a group)
+// share ONE inverse -- prefix products, the inverse of the last, a backward pass
+// of two products per element -- with a per-element fallback (inverse_coop's
+// algorithm) for a group whose product is not a unit.  y_ptr / out / unit are
+// indexed as InverseArgs; order lists the instances group by group.
+struct BatchInverseArgs {
+  const uint64_t* y_ptr;    // [count] values (reduced)
+  const uint64_t* m_ptr;    // [count] moduli (every instance of a group: the same odd modulus)
+  const uint32_t* order;    // [count] instance indices, grouped by modulus
+  const uint32_t* gstart;   // [ngroups + 1] group offsets into order
+  uint32_t* out;            // [count][K32] inverses (may be null: unit flags only)
+  uint32_t* unit;           // [count] 1 if gcd(y, m) == 1
+  uint32_t* scratch;        // [count][KD] prefix products (device)
+  uint32_t ngroups;
 };
 
 struct EqOperand {
@@ -133,6 +150,15 @@ hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st);
 hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);
 // lane-cooperative Pornin inverse (inverse.hip): registers + DPP
 hipError_t launch_inverse_coop(uint32_t k32, const InverseArgs& a, hipStream_t st);
+hipError_t launch_inverse_batch(uint32_t k32, const BatchInverseArgs& a, hipStream_t st);
+// Montgomery's simultaneous inversion where instances share a modulus (one
+// binary-GCD inverse per modulus instead of one per instance); FSDKR_BATCH_INV=0:
+// one inverse each (A/B).  Read per call.
+inline bool batch_inv_on() {
+  const char* e = getenv("FSDKR_BATCH_INV");
+  return !(e && atoi(e) == 0);
+}
+size_t inverse_batch_scratch_words(uint32_t k32);
 hipError_t launch_eq_check(uint32_t k32, const EqCheckArgs& a, hipStream_t st);
 hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st);
 hipError_t launch_pdl_u1(const PdlU1Args& a, hipStream_t st);

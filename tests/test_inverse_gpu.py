@@ -50,3 +50,38 @@ def test_inverse_matches_python(gpu_ctx, limbs):
         if m == 1:
             continue
         assert g == want, (k, hex(y)[:40], hex(m)[:40])
+
+
+@pytest.mark.parametrize("limbs", [64, 128])
+@pytest.mark.parametrize("kind", ["units", "one_non_unit", "zero", "singletons"])
+def test_simultaneous_inverse_groups(gpu_ctx, limbs, kind, monkeypatch):
+    """Instances sharing a modulus are inverted together (Montgomery's trick,
+    inverse_batch_kernel: prefix products, ONE binary-GCD inverse, a backward
+    pass): exact inverses and unit flags equal pow(y, -1, m), including a group
+    whose product is not a unit (every element of it then inverted on its own),
+    y = 0 and groups of one.  FSDKR_BATCH_INV=0 (one inverse each) gives the
+    same results."""
+    rnd = random.Random(1000 * limbs + len(kind))
+    bits = 32 * limbs
+    mods = [_case(rnd, bits, "rsa2" if limbs == 128 else "odd") for _ in range(5)]
+    # modulus 2 with a small factor 3: its group gets a non-unit in "one_non_unit"
+    mods[2] = 3 * (rnd.getrandbits(bits - 3) | 1 | (1 << (bits - 4)))
+    ys, ms = [], []
+    for k in range(5 * 37 if kind != "singletons" else 5):
+        m = mods[k % 5]
+        ys.append(rnd.randrange(1, m))
+        ms.append(m)
+    if kind == "one_non_unit":
+        ys[7] = 3 * rnd.randrange(1, mods[2] // 3)   # k = 7: modulus 2's group
+    if kind == "zero":
+        ys[3] = 0
+    got = gpu_ctx.mod_inverse(ys, ms, limbs)
+    monkeypatch.setenv("FSDKR_BATCH_INV", "0")
+    ref = gpu_ctx.mod_inverse(ys, ms, limbs)
+    for k, (y, m, g) in enumerate(zip(ys, ms, got)):
+        try:
+            want = pow(y, -1, m)
+        except ValueError:
+            want = None
+        assert g == want, (kind, k)
+    assert got == ref

@@ -119,11 +119,12 @@ class _RankDist:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tamper", [None, "pdl", "ck"])
+@pytest.mark.parametrize("tamper", [None, "pdl", "ck", "neg_s1", "neg_alice_e"])
 def test_sharded_collect_two_emulated_ranks(gpu_ctx, tamper):
     """fsdkr.shard.collect with two ranks emulated as threads (one HIP context
     each, one GPU): every rank's outcome and LocalKey equal the single-process
-    GPU collect() and the oracle's."""
+    GPU collect() and the oracle's (negative operands: the panic of that
+    sender's pair, found by the rank that holds it and merged to every rank)."""
     import threading
     from fsdkr import Context, refresh, shard
     from oracle import protocol
@@ -134,6 +135,12 @@ def test_sharded_collect_two_emulated_ranks(gpu_ctx, tamper):
     if tamper == "pdl":
         p = msgs[3].pdl_proof_vec[1]
         msgs[3].pdl_proof_vec[1] = dataclasses.replace(p, s3=p.s3 + 1)
+    elif tamper == "neg_s1":
+        p = msgs[3].pdl_proof_vec[1]
+        msgs[3].pdl_proof_vec[1] = dataclasses.replace(p, s1=-p.s1)
+    elif tamper == "neg_alice_e":
+        a = msgs[4].range_proofs[0]
+        msgs[4].range_proofs[0] = dataclasses.replace(a, e=-a.e)
     elif tamper == "ck":
         sv = msgs[4].dk_correctness_proof.sigma_vec
         msgs[4].dk_correctness_proof = dataclasses.replace(msgs[4].dk_correctness_proof,
