@@ -293,6 +293,8 @@ struct CollectPlan {
   // descriptor offsets
   size_t d_bs, d_bn, d_iynn, d_imnn, d_iynl, d_imnl, d_eqnn, d_eqnnm, d_eqnl, d_eqnlm, d_eqck, d_eqckm, d_p3nn, d_p3nl,
       d_p3m, d_ahn, d_ahc, d_alpre;
+  size_t d_p3mnl = 0;    // moduli of the nl prod3 rows (d_p3m, + the negative-s3 rows)
+  uint32_t n_p3nl = 0;   // P + pairs with a negative PDL s3
   uint32_t n_inv_nn = 0, n_eq_nn = 0, n_eq_nl = 0, n_eq_ck = 0;
   // the pairs grouped by receiver (Montgomery's simultaneous inversion of the
   // per-pair inverses: c^-1 mod N_i^2, (z^e)^-1 mod Ñ_i; inverse_batch_kernel)

@@ -271,8 +271,12 @@ int collect_launch_impl(Ctx* c) {
   if (pl.fx_hit) (void)hipStreamWaitEvent(st, pl.fx_done, 0);   // the prestarted fixed-base exponents
   if (pl.ch_hit)   // the prestarted challenge jobs (J2, J5 -> inverses; pdl_u1 -> Feldman)
     for (hipEvent_t ev : pl.ch_ev) (void)hipStreamWaitEvent(st, ev, 0);
-  // equality checks and exact products
+  // exact products (first: the negative-s3 pairs' u3 check reads rows of x_w), equality checks
   {
+    Prod3Args pa{(const Prod3Operand*)(dev + pl.d_p3nn), PI(pl.d_p3m), cons_nn, PX(pl.x_u), P};
+    if ((rc = c->hip_check(launch_prod3(nn, pa, st), "prod3 nn"))) return rc;
+    Prod3Args pb{(const Prod3Operand*)(dev + pl.d_p3nl), PI(pl.d_p3mnl), cons_nl, PX(pl.x_w), pl.n_p3nl};
+    if ((rc = c->hip_check(launch_prod3(nl, pb, st), "prod3 nl"))) return rc;
     EqCheckArgs a{(const EqOperand*)(dev + pl.d_eqnn), PI(pl.d_eqnnm), cons_nn, PX(pl.x_pbits), DI(pl.o_one),
                   PX(pl.x_eq2), pl.n_eq_nn};
     c->mark("eq_check", true);
@@ -286,10 +290,6 @@ int collect_launch_impl(Ctx* c) {
     rc = c->hip_check(launch_eq_check(nl, b1, st), "eq_check nl");
     c->mark("eq_check", false);
     if (rc) return rc;
-    Prod3Args pa{(const Prod3Operand*)(dev + pl.d_p3nn), PI(pl.d_p3m), cons_nn, PX(pl.x_u), P};
-    if ((rc = c->hip_check(launch_prod3(nn, pa, st), "prod3 nn"))) return rc;
-    Prod3Args pb{(const Prod3Operand*)(dev + pl.d_p3nl), PI(pl.d_p3m), cons_nl, PX(pl.x_w), P};
-    if ((rc = c->hip_check(launch_prod3(nl, pb, st), "prod3 nl"))) return rc;
   }
   {
     AliceHashArgs a{(const uint64_t*)(dev + pl.d_ahn), (const uint64_t*)(dev + pl.d_ahc), PI(pl.o_az), PX(pl.x_u),

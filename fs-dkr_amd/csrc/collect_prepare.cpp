@@ -95,6 +95,14 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     const Sess& x = pl.ss[sess_of_pair[p]];
     recv_of_pair[p] = x.rbase + (p - x.pbase) % x.n;
   }
+  // pairs whose PDL s3 is negative (pdl_s3 holds |s3|): u3 is checked as
+  // h1^s1 == u3 * (z^e * h2^|s3|), the bracket an extra exact product row
+  std::vector<uint32_t> neg3;
+  for (const Sess& x : pl.ss)
+    if (x.b->pdl_s3_neg)
+      for (uint32_t lp = 0; lp < x.P; ++lp)
+        if (x.b->pdl_s3_neg[lp]) neg3.push_back(x.pbase + lp);
+  const size_t K3 = neg3.size();
   // a prestarted GA of this batch: J1 is not launched again
   pl.ga_hit = ga_pre_matches(c, bs, count);
   GaPre* gpre = reinterpret_cast<GaPre*>(c->ga_pre);
@@ -548,7 +556,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   const size_t n_eqnl = (size_t)P + (size_t)Mt * M + 2 * (size_t)J;
   const size_t x_eq3 = OUT(n_eqnl * 4);               // [u3 P | RP Mt*M | DLog 2J]
   const size_t x_eqck = OUT((size_t)Mt * CK_M2 * 4);
-  const size_t x_u = OUT((size_t)P * nn * 4), x_w = OUT((size_t)P * nl * 4);
+  const size_t x_u = OUT((size_t)P * nn * 4), x_w = OUT(((size_t)P + K3) * nl * 4);   // + z^e h2^|s3| [K3]
   const size_t x_fel = OUT(P), x_pdlv = OUT(P), x_rng = OUT(P);
   // 2-adic checks of even moduli
   uint32_t n_p2 = 0;
@@ -576,6 +584,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       (2 * (size_t)n + Mt) * 8 + (4 * (size_t)P + (size_t)Mt * M) * 4 + 4 * (8192 + 2048) +   // its comb groups
       4 * (size_t)P * 8 + 4 * (size_t)P * 16 +                                            // binom, inverses
       n_eqall * (sizeof(EqOperand) + 4) + 2 * (size_t)P * sizeof(Prod3Operand) + 4 * (size_t)P +
+      (K3 ? K3 * (sizeof(Prod3Operand) + 4) + 4 * (size_t)P + 1024 : 0) +               // negative s3 rows
       2 * (size_t)P * 8 + P + (size_t)n_p2 * sizeof(Pow2Op) + 32 * 256 + 64 * 1024 +
       ((size_t)2 * P + (size_t)n * 63) * kTailDescBytes;                                 // the joint tail's block
   const size_t out_off = Img::al(in_bytes_pre + desc_bound);
@@ -905,6 +914,11 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     eq_nl.push_back(e);
     eq_nl_mod.push_back(recv_of_pair[p]);
   }
+  for (size_t k = 0; k < K3; ++k) {   // s3 < 0: h1^s1 * 1 == u3 * (z^e * h2^|s3|), prod3 row P + k
+    EqOperand& e = eq_nl[neg3[k]];
+    e.b = DI(o_one);
+    e.d = DX(x_w + ((size_t)P + k) * nl * 4);
+  }
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N; the odd part here)
       EqOperand e;
@@ -967,9 +981,18 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
                 pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invz + (size_t)p * nl) : DX(x_invz + (size_t)p * nl * 4),
                 nl, nl, nl, 0};
   }
+  std::vector<uint32_t> p3_nl_mod;
+  if (K3) {   // the negative-s3 rows: z^e * h2^|s3| * 1  (mod N~)
+    p3_nl_mod = recv_of_pair;
+    for (size_t k = 0; k < K3; ++k) {
+      p3_nl.push_back({J5_row(neg3[k]), J4_row(neg3[k]), DI(o_one), nl, nl, nl, 0});
+      p3_nl_mod.push_back(recv_of_pair[neg3[k]]);
+    }
+  }
   const size_t d_p3nn = put(p3_nn.data(), p3_nn.size() * sizeof(Prod3Operand)),
                d_p3nl = put(p3_nl.data(), p3_nl.size() * sizeof(Prod3Operand)),
-               d_p3m = put(recv_of_pair.data(), recv_of_pair.size() * 4);
+               d_p3m = put(recv_of_pair.data(), recv_of_pair.size() * 4),
+               d_p3mnl = K3 ? put(p3_nl_mod.data(), p3_nl_mod.size() * 4) : d_p3m;
   // alice hash descriptors + pre-verdicts
   std::vector<uint64_t> ah_n(P), ah_c(P);
   for (uint32_t p = 0; p < P; ++p) {
@@ -1083,6 +1106,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   pl.d_bs = d_bs; pl.d_bn = d_bn; pl.d_iynn = d_iynn; pl.d_imnn = d_imnn; pl.d_iynl = d_iynl; pl.d_imnl = d_imnl;
   pl.d_eqnn = d_eqnn; pl.d_eqnnm = d_eqnnm; pl.d_eqnl = d_eqnl; pl.d_eqnlm = d_eqnlm; pl.d_eqck = d_eqck;
   pl.d_eqckm = d_eqckm; pl.d_p3nn = d_p3nn; pl.d_p3nl = d_p3nl; pl.d_p3m = d_p3m; pl.d_ahn = d_ahn; pl.d_ahc = d_ahc;
+  pl.d_p3mnl = d_p3mnl;
+  pl.n_p3nl = (uint32_t)(P + K3);
   pl.d_alpre = d_alpre;
   pl.n_inv_nn = pl.ch_hit && !pl.joint ? gpre->ch_n_inv_nn : (uint32_t)inv_y_nn.size();
   pl.r_unn = pl.ch_hit ? (const void*)gpre->ch_unn : out_base + x_unn;

@@ -15,12 +15,12 @@ sigma_vec shorter than the loops index (the reference's index panic at that
 check), a LocalKey with fewer keys than receivers (panic at the first pair
 past them, :334-339), an ek.n wider than the batch's moduli (its correct-key
 proof runs at its own width before ModuliTooSmall, :376-391), and negative
-BigInts where the reference's outcome for that instance is a panic, an error
-or a plain residue (_Negatives: PDL s1 / u2 / u3 / s2, Alice s / s1 / s2 / e,
-ring-Pedersen Z, DLog y).  Still outside the representable set
-(UnsupportedInput): other negative fields (hashed AND reduced values such as
-c, z, A, or h2^-1 exponents such as PDL s3) and values wider than 3072 bits in
-a proof field (6144 bits for ek.n / sigma)."""
+BigInts where the reference's outcome for that instance is a panic, an error,
+a plain residue or an h2^-1 exponent (_Negatives: PDL s1 / u2 / u3 / s2 / s3,
+Alice s / s1 / s2 / e, ring-Pedersen Z, DLog y).  Still outside the
+representable set (UnsupportedInput): other negative fields (hashed AND reduced
+values such as c, z, A) and values wider than 3072 bits in a proof field (6144
+bits for ek.n / sigma)."""
 import ctypes
 import math
 import os
@@ -188,7 +188,10 @@ class _Negatives:
     - PDL (zk_pdl_with_slack.rs:113-167): s1 < 0 panics in h^s1 (u2_test_tmp,
       :139) whatever else holds; u2 / u3 < 0 hash as |u| (the challenge, and so
       u1's check, is unchanged) and can never equal a residue (flag false);
-      s2 < 0 is the base of s2^N mod N^2: packed as s2 mod N^2.
+      s2 < 0 is the base of s2^N mod N^2: packed as s2 mod N^2; s3 < 0 raises
+      h2^-1 to |s3| (commitment_unknown_order, :177-184): mod_inv(h2).unwrap()
+      panics when h2 is not a unit mod N~, else |s3| is packed with the pair's
+      pdl_s3_neg flag and the device checks h1^s1 == u3 * z^e * h2^|s3|.
     - Alice (range_proofs.rs:112-164): s1 > q^3 -> false first; e < 0 panics
       in z^e; z^e not invertible -> false; then s1 / s2 < 0 panic in h1^s1 /
       h2^s2; s < 0 is the base of s^N mod N^2 (packed as s mod N^2).
@@ -204,6 +207,7 @@ class _Negatives:
         self.pdl = {}      # pair -> (or-bits, and-mask)
         self.range = {}    # pair -> verdict (0 false, 2 panic)
         self.dlog = {}     # join -> "y1-panic" | "y1-false" | "y2"
+        self.s3 = None     # [pairs] uint8 pdl_s3_neg flags (None: no negative s3)
 
     def __bool__(self):
         return bool(self.rows)
@@ -226,6 +230,13 @@ class _Negatives:
         """the verdict rules, once every field is gathered"""
         for p in self.rows.get("pdl_s1", ()):
             self.pdl[p] = (8, 0xFF)
+        if self.rows.get("pdl_s3"):
+            self.s3 = np.zeros(len(pdl), np.uint8)
+            for p in self.rows["pdl_s3"]:
+                self.s3[p] = 1
+                i = p % n
+                if i < avail and math.gcd(sts[i].ni, sts[i].N) != 1:   # mod_inv(h2, N~).unwrap()
+                    self.pdl[p] = (8, 0xFF)
         for name, bit in (("pdl_u2", 2), ("pdl_u3", 4)):
             for p in self.rows.get(name, ()):
                 o, a = self.pdl.get(p, (0, 0xFF))
@@ -435,7 +446,7 @@ class CollectBatch:
             raise UnsupportedInput(f"{ck_bits}-bit Paillier key / correct-key proof")
         neg = self.negs
         F["pdl_s1"] = neg.field(G, "pdl_s1", pdl, "s1", _zero)
-        F["pdl_s3"] = G.field(pdl, "s3")
+        F["pdl_s3"] = neg.field(G, "pdl_s3", pdl, "s3", _magnitude)
         for a in ("s1", "s2"):
             F["rp_" + a] = neg.field(G, "rp_" + a, rng, a, _zero)
         F["ped_S"] = G.field([m.ring_pedersen_statement for m in all_m], "S")
@@ -517,6 +528,9 @@ class CollectBatch:
             self._points(st)
         if self.negs:
             self.negs.decide(msgs, joins, n, st["avail"], st["pdl"], st["rng"], st["sts"])
+            if self.negs.s3 is not None:
+                self._keep.append(self.negs.s3)
+                c.pdl_s3_neg = self.negs.s3.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
         self.nl = nl
         return self
 

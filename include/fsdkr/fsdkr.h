@@ -187,13 +187,20 @@ typedef struct fsdkr_collect_batch {
    *             panics in the challenge hash, Z shorter at check len(Z)
    *             (ring_pedersen_proof.rs:131-144); missing rows are placeholders.
    *  ck_lens    [R+J] lengths of dk_correctness_proof.sigma_vec (< 11 panics in
-   *             zk-paillier's verify); missing rows are placeholders. */
+   *             zk-paillier's verify); missing rows are placeholders.
+   *  pdl_s3_neg [R*n] nonzero: the pair's PDL s3 is negative and pdl_s3 holds |s3|.
+   *             commitment_unknown_order then raises h2^-1 to |s3|
+   *             (zk_pdl_with_slack.rs:177-184); the u3 check is evaluated as
+   *             h1^s1 == u3 * z^e * h2^|s3| (mod N~), equivalent when h2 is a unit.
+   *             The caller reports the pairs whose h2 is not a unit (mod_inv
+   *             unwrap panics) itself; their u3 bit here is meaningless. */
   const uint32_t* vss_len;
   const uint32_t* range_lens;
   uint32_t ckl;
   uint32_t recv_avail;
   const uint32_t* ped_lens;
   const uint32_t* ck_lens;
+  const uint8_t* pdl_s3_neg;
 } fsdkr_collect_batch;
 
 /* Verdicts (caller-allocated). 1 bits mean "check passed".  cap_* are the

@@ -166,12 +166,85 @@ def test_negative_dlog_response(joined, which):
     assert host_outcome(msgs, keys[1], [j2]) == want
 
 
+class _NegGamma:
+    """rng proxy for oracle.zk_pdl_with_slack.prove: its third sample_below (gamma,
+    below q^3 N~) comes back shifted by -2 q^3 N~, so s3 = e rho + gamma < 0 while
+    the proof stays valid (u3 = h1^alpha (h2^-1)^|gamma|, commitment_unknown_order)."""
+
+    def __init__(self, rng):
+        self.rng, self.k = rng, 0
+
+    def sample_below(self, bound):
+        v = self.rng.sample_below(bound)
+        self.k += 1
+        return v - 2 * bound if self.k == 3 else v
+
+    def __getattr__(self, name):
+        return getattr(self.rng, name)
+
+
+def dkr_negative_s3(t, n, seed, senders):
+    """_dkr with every PDL proof of the given senders (party indices) carrying a
+    negative s3 -- valid proofs the reference accepts (h2^-1 raised to |s3|)."""
+    from oracle import zk_pdl_with_slack as zpdl
+    rng = Rng(seed)
+    keys = protocol.simulate_keygen(t, n, rng, KB)
+    msgs, dks = [], []
+    orig = zpdl.prove
+    for key in keys:
+        if key.i in senders:
+            zpdl.prove = lambda x, r, st, g: orig(x, r, st, _NegGamma(g))
+        try:
+            m, dk = protocol.distribute(key.i, key, n, rng, KB)
+        finally:
+            zpdl.prove = orig
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks
+
+
+@pytest.fixture(scope="module")
+def neg_s3():
+    return dkr_negative_s3(1, 4, "neg-s3-t1n4", {1, 3})
+
+
+def test_negative_pdl_s3_valid(neg_s3):
+    """Negative s3 (an h2^-1 exponent, zk_pdl_with_slack.rs:177-184): the oracle
+    accepts; the batch packs |s3| and flags exactly those pairs (pdl_s3_neg),
+    with no host rule (every h2 is a unit)."""
+    from fsdkr.batch import CollectBatch
+    from fsdkr._native import limbs_to_ints
+    keys, msgs, dks = neg_s3
+    neg = [k * 4 + i for k in range(4) for i in range(4) if msgs[k].pdl_proof_vec[i].s3 < 0]
+    assert neg == [k * 4 + i for k in (0, 2) for i in range(4)]
+    assert oracle_outcome(msgs, keys[1], dks[1]) is None
+    b = CollectBatch(msgs, keys[1], [], 256, KB)
+    assert b.negs.s3.tolist() == [int(p in neg) for p in range(16)]
+    assert np.ctypeslib.as_array(b.c.pdl_s3_neg, shape=(16,)).tolist() == b.negs.s3.tolist()
+    s3 = limbs_to_ints(np.ctypeslib.as_array(b.c.pdl_s3, shape=(16, b.c.s3l)))
+    assert s3 == [abs(m.pdl_proof_vec[i].s3) for m in msgs for i in range(4)]
+    assert not b.negs.pdl
+    assert host_outcome(msgs, keys[1]) is None
+
+
+def test_negative_pdl_s3_h2_not_unit(neg_s3):
+    """h2 not a unit mod N~: mod_inv(h2).unwrap() panics at the first pair with a
+    negative s3 (sender 1 holds the first message: its pair to receiver 2 is the
+    first to reach u3 with h2 = N~)."""
+    keys, msgs, dks = neg_s3
+    key = keys[0].clone()
+    st = key.h1_h2_n_tilde_vec[2]
+    key.h1_h2_n_tilde_vec[2] = dataclasses.replace(st, ni=st.N)
+    assert oracle_outcome(msgs, key, dks[0]) == ("panic",)
+    assert host_outcome(msgs, key) == ("panic",)
+
+
 def test_negative_outside_the_rules_still_unsupported(dkr4):
-    """a negative PDL s3 is an h2^-1 exponent in the reference (a valid value, not a
-    panic): still UnsupportedInput for the batch"""
+    """a negative PDL z is hashed and reduced (z^e mod N~): still UnsupportedInput
+    for the batch"""
     from fsdkr.batch import CollectBatch, UnsupportedInput
     keys, msgs, dks = dkr4
-    m2 = _pdl(msgs, 0, 0, s3=lambda p: -p.s3)
+    m2 = _pdl(msgs, 0, 0, z=lambda p: -p.z)
     with pytest.raises(UnsupportedInput):
         CollectBatch(m2, keys[0], [], 256, KB)
 

@@ -16,7 +16,7 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from test_edge_outcomes_gpu import KB, _check, _dkr, _joins_setup  # noqa: E402
-from test_negative_operands import _alice, _pdl  # noqa: E402
+from test_negative_operands import _alice, _pdl, dkr_negative_s3  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -46,6 +46,34 @@ def test_negative_pdl_u2_u3(gpu_ctx, dkr5):
     ro = _check(gpu_ctx, _pdl(msgs, 4, 0, u3=lambda p: -p.u3, u2=lambda p: -p.u2), keys[0], dks[0],
                 expect="PDLwSlackProof")
     assert ro[1] == {"is_u1_eq": True, "is_u2_eq": False, "is_u3_eq": False}
+
+
+@pytest.fixture(scope="module")
+def neg_s3():
+    return dkr_negative_s3(2, 5, "neg-s3-gpu-t2n5", {2, 5})
+
+
+def test_negative_pdl_s3(gpu_ctx, neg_s3):
+    """s3 < 0 raises h2^-1 to |s3| (commitment_unknown_order,
+    zk_pdl_with_slack.rs:177-184): valid proofs from two senders -> Ok with the
+    oracle's LocalKey; a wrong u3 on such a pair -> a new challenge, all false; a sign-flipped
+    positive s3 -> u3 false; h2 not a unit -> the mod_inv unwrap panic."""
+    keys, msgs, dks = neg_s3
+    assert sum(p.s3 < 0 for m in msgs for p in m.pdl_proof_vec) == 10
+    for r in (0, 3):
+        assert _check(gpu_ctx, msgs, keys[r], dks[r]) is None
+    ro = _check(gpu_ctx, _pdl(msgs, 1, 3, u3=lambda p: p.u3 + 1), keys[0], dks[0], expect="PDLwSlackProof")
+    assert ro[1] == {"is_u1_eq": False, "is_u2_eq": False, "is_u3_eq": False}   # u3 is hashed into e
+    ro = _check(gpu_ctx, _pdl(msgs, 0, 2, s3=lambda p: -p.s3), keys[0], dks[0], expect="PDLwSlackProof")
+    assert ro[1] == {"is_u1_eq": True, "is_u2_eq": True, "is_u3_eq": False}
+    ro = _check(gpu_ctx, _pdl(msgs, 4, 1, s3=lambda p: -p.s3), keys[0], dks[0], expect="PDLwSlackProof")
+    assert ro[1] == {"is_u1_eq": True, "is_u2_eq": True, "is_u3_eq": False}
+    key = keys[0].clone()
+    st = key.h1_h2_n_tilde_vec[3]
+    key.h1_h2_n_tilde_vec[3] = dataclasses.replace(st, ni=0)
+    # the first message's s3 is positive: its u3 fails before any unwrap is reached
+    _check(gpu_ctx, msgs, key, dks[0], expect="PDLwSlackProof")
+    _check(gpu_ctx, _pdl(msgs, 0, 3, s3=lambda p: -p.s3), key, dks[0], expect="panic")
 
 
 def test_negative_alice_operands(gpu_ctx, dkr5):
@@ -102,13 +130,25 @@ def test_negative_dlog_response(gpu_ctx, which):
 def test_collect_many_negative_session_alone(gpu_ctx, dkr5):
     """collect_many: the session holding a negative s1 panics, the regular
     sessions around it succeed, each as the oracle says."""
+    keys, msgs, dks, _ = dkr5
+    m2 = _pdl(msgs, 4, 2, s1=lambda p: -p.s1)
+    sessions = [(msgs, 0), (m2, 1), (msgs, 2)]
+    _collect_many_like_oracle(gpu_ctx, keys, dks, sessions)
+
+
+def test_collect_many_negative_s3_session(gpu_ctx, neg_s3):
+    """collect_many: a session of valid negative-s3 proofs (packed on its own,
+    pdl_s3_neg) succeeds beside regular sessions; one with a broken u3 fails."""
+    keys, msgs, dks = neg_s3
+    m2 = _pdl(msgs, 1, 0, u3=lambda p: p.u3 + 1)
+    _collect_many_like_oracle(gpu_ctx, keys, dks, [(msgs, 0), (m2, 1), (msgs, 4)])
+
+
+def _collect_many_like_oracle(gpu_ctx, keys, dks, sessions):
     from fsdkr import refresh
     from test_edge_outcomes_gpu import _same_key
     from oracle import protocol
     from oracle.rng import Rng
-    keys, msgs, dks, _ = dkr5
-    m2 = _pdl(msgs, 4, 2, s1=lambda p: -p.s1)
-    sessions = [(msgs, 0), (m2, 1), (msgs, 2)]
     gk = [keys[p].clone() for _, p in sessions]
     out = refresh.collect_many([(copy.deepcopy(m), k, dks[p], []) for (m, p), k in zip(sessions, gk)],
                                ctx=gpu_ctx, key_bits=KB)
@@ -117,10 +157,14 @@ def test_collect_many_negative_session_alone(gpu_ctx, dkr5):
         try:
             protocol.collect(copy.deepcopy(m), ko, dks[p], [], Rng("a8"), KB)
             want = None
+        except protocol.FsDkrError as e:
+            want = (e.variant, e.fields)
         except Exception:
             want = "panic"
         if want is None:
             assert o is None, o
             _same_key(ko, k)
-        else:
+        elif want == "panic":
             assert isinstance(o, refresh.FsDkrPanic), o
+        else:
+            assert isinstance(o, refresh.FsDkrError) and (o.variant, o.fields) == want, (o, want)
