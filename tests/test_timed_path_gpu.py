@@ -131,7 +131,7 @@ def test_timed_path_config2_negative_operands(gpu_ctx, timed2):
     """VERDICT r4 item 8 at full size: one sender's negative PDL s1 -> that pair's
     panic (zk_pdl_with_slack.rs:139), no key written (the PDL loop precedes every
     write); s2 - N^2 in another pair (GA's base: the same residue) -> Ok, with the
-    LocalKey the clean batch gives."""
+    LocalKey the clean batch gives; a negative s3 -> that pair's u3 fails."""
     from fsdkr import refresh
     msgs, joins, lk, dk = timed2
     m2 = list(msgs)
@@ -150,6 +150,14 @@ def test_timed_path_config2_negative_operands(gpu_ctx, timed2):
     assert got is None, got
     ref, key0 = _collect(gpu_ctx, msgs, joins, lk, dk)
     assert (key3.x_i, key3.y, key3.pk_vec) == (key0.x_i, key0.y, key0.pk_vec)
+    # a sign-flipped s3 is an h2^-1 exponent (zk_pdl_with_slack.rs:177-184): the
+    # pair's u3 alone fails (pdl_s3_neg; |s3| into the prestarted comb tables)
+    m4 = list(msgs)
+    m = tamper._own(m4, 23)
+    p = m.pdl_proof_vec[11]
+    m.pdl_proof_vec[11] = dataclasses.replace(p, s3=-p.s3)
+    got, _ = _collect(gpu_ctx, m4, joins, lk, dk)
+    assert got == ("PDLwSlackProof", {"is_u1_eq": True, "is_u2_eq": True, "is_u3_eq": False}), got
 
 
 # ------------------------------------------------------------------ configs[3]
