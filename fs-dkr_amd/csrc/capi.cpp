@@ -17,7 +17,6 @@
 #include <string>
 #include <vector>
 
-#include "collect.hpp"
 #include "ctx.hpp"
 #include "kernels.h"
 #include "verify.h"
@@ -321,30 +320,6 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
                        uint32_t prio, uint32_t group, uint32_t desc_flags, const SplitArgs* split) {
   if (!st) st = c->stream;
   if (count == 0) return FSDKR_OK;
-  if (group == kCoopGroup) {   // the one-wave cooperative shape: d_consts are coop_constants rows
-    const uint32_t K = coop_digits(k32);
-    if (!K || c->ct || (split && split->lo_bit)) {
-      c->fail("the cooperative modexp shape takes whole public-exponent chains at 2048 / 4096 bits");
-      return FSDKR_E_ARG;
-    }
-    const uint32_t w = choose_slide_window(exp_bits ? exp_bits : 1);
-    const size_t entries = ((size_t)1 << (w - 1)) + 1;
-    uint32_t* d_table = (uint32_t*)c->buf(table_tag, sizeof(uint32_t) * (size_t)count * entries * K);
-    if (!d_table) {
-      c->fail("device allocation failed (%u instances, window %u)", count, w);
-      return FSDKR_E_OOM;
-    }
-    const size_t n8 = (size_t)count * 8, n4 = (size_t)count * 4;
-    CoopArgs a{reinterpret_cast<const uint64_t*>(d_desc), reinterpret_cast<const uint32_t*>(d_desc + 2 * n8),
-               reinterpret_cast<const uint64_t*>(d_desc + n8), reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + n4),
-               reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 2 * n4), d_consts, d_out,
-               (desc_flags & kDescOutIdx) ? reinterpret_cast<const uint32_t*>(d_desc + 2 * n8 + 4 * n4) : nullptr,
-               d_table, w, count, prio};
-    const size_t tm = c->tbeg("modexp", st);
-    int rc = c->hip_check(launch_modexp_coop(k32, a, st), "coop modexp launch");
-    c->tend(tm, st);
-    return rc;
-  }
   // sliding windows: the 4096-bit group shapes, public exponents, wave-uniform (caller)
   // a forced context setting wins (tuning, tests), except that the 32-lane shape
   // runs only where the caller asked for it (it prepared KD = 160 constants)
@@ -511,52 +486,6 @@ int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_ba
   return launch_modexp_job(c, job, d_consts, d_out, "generic", wide);
 }
 
-// The one-wave cooperative shape (coop.hip) on device-resident operands; the
-// moduli's constants are computed on the host (coop_constants).
-int run_modexp_coop(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
-                    uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* h_mods,
-                    uint32_t n_mod, uint32_t* d_out) {
-  const uint32_t K = coop_digits(k32);
-  std::vector<uint32_t> cons((size_t)n_mod * 4 * K);
-  parallel_for(n_mod, 1, [&](size_t m0, size_t m1) {
-    for (size_t m = m0; m < m1; ++m) coop_constants(h_mods + m * k32, k32, K, cons.data() + m * 4 * K);
-  });
-  const uint32_t w = choose_slide_window(exp_bits ? exp_bits : 1);
-  const size_t entries = ((size_t)1 << (w - 1)) + 1;
-  uint32_t* d_cons = (uint32_t*)c->buf("coop_consts", cons.size() * 4);
-  uint8_t* d_desc = (uint8_t*)c->buf("coop_desc", (size_t)count * 24);
-  uint32_t* d_table = (uint32_t*)c->buf("coop_table", sizeof(uint32_t) * (size_t)count * entries * K);
-  if (!d_cons || !d_desc || !d_table) {
-    c->fail("fsdkr_modexp_batch: device allocation failed (cooperative shape)");
-    return FSDKR_E_OOM;
-  }
-  std::vector<uint8_t> h((size_t)count * 24);
-  uint64_t* bp = reinterpret_cast<uint64_t*>(h.data());
-  uint64_t* ep = bp + count;
-  uint32_t* bl = reinterpret_cast<uint32_t*>(ep + count);
-  uint32_t* el = bl + count;
-  for (uint32_t i = 0; i < count; ++i) {
-    bp[i] = (uint64_t)(uintptr_t)(d_base + (size_t)i * k32);
-    ep[i] = (uint64_t)(uintptr_t)(d_exp + (size_t)i * exp_limbs);
-    bl[i] = k32;
-    el[i] = exp_limbs;
-  }
-  int rc;
-  if ((rc = c->hip_check(hipMemcpyAsync(d_cons, cons.data(), cons.size() * 4, hipMemcpyHostToDevice, c->stream),
-                         "H2D coop consts")) ||
-      (rc = c->hip_check(hipMemcpyAsync(d_desc, h.data(), h.size(), hipMemcpyHostToDevice, c->stream), "H2D coop desc")))
-    return rc;
-  CoopArgs a{reinterpret_cast<const uint64_t*>(d_desc), reinterpret_cast<const uint32_t*>(d_desc + (size_t)count * 16),
-             reinterpret_cast<const uint64_t*>(d_desc + (size_t)count * 8),
-             reinterpret_cast<const uint32_t*>(d_desc + (size_t)count * 20), d_mod_idx, d_cons, d_out, nullptr, d_table,
-             w, count, c->prio};
-  const size_t tm = c->tbeg("modexp", c->stream);
-  rc = c->hip_check(launch_modexp_coop(k32, a, c->stream), "coop modexp launch");
-  c->tend(tm, c->stream);
-  if (rc) return rc;
-  return c->sync();   // (the host vectors go out of scope)
-}
-
 }  // namespace fsdkr
 
 // ---------------------------------------------------------------- C ABI -------
@@ -643,9 +572,7 @@ const char* fsdkr_last_error(const fsdkr_ctx* ctx) {
 
 int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes) {
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
-  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64 &&
-             lanes != kCoopGroup))
-    return FSDKR_E_ARG;
+  if (!c || (lanes != 0 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)) return FSDKR_E_ARG;
   c->modexp_group = lanes;
   return FSDKR_OK;
 }
@@ -823,10 +750,7 @@ int fsdkr_modexp_batch(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const
                                         hipMemcpyHostToDevice, c->stream),
                          "H2D mods")))
     return rc;
-  if (c->modexp_group == kCoopGroup && !c->ct && coop_digits(mod_limbs))
-    rc = run_modexp_coop(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_idx, mods, n_mod, d_out);
-  else
-    rc = run_modexp_device(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_idx, d_mods, n_mod, d_out);
+  rc = run_modexp_device(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_idx, d_mods, n_mod, d_out);
   if (rc) return rc;
   if ((rc = c->hip_check(hipMemcpyAsync(out, d_out, nb, hipMemcpyDeviceToHost, c->stream), "D2H out"))) return rc;
   return c->sync();

@@ -520,17 +520,6 @@ inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
   return count <= 16384u ? 16 : 4;
 }
 
-// The one-wave cooperative shape (coop.hip: separated Montgomery, one chain per
-// wave) for a multi-GPU rank's GA, whose <= 1 024 4096-bit chains leave most
-// SIMDs idle in the lane-group shapes.  FSDKR_GA_COOP=1 / 0 forces it on / off.
-constexpr uint32_t kCoopChains = 1024;
-inline bool ga_coop(uint32_t count, uint32_t nn) {
-  if (nn != 128 || lanes_env("FSDKR_GA_LANES", nn)) return false;
-  const char* e = getenv("FSDKR_GA_COOP");
-  if (e) return atoi(e) != 0;
-  return false;
-}
-
 // J2 (c^e mod N^2, 256-bit exponents) lanes per instance, when the joint tail
 // does not absorb it
 inline uint32_t j2_lanes(size_t count, uint32_t nn) {

@@ -913,9 +913,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
                o_s = o_s2 + al((size_t)P * nl * 4), o_desc = o_s + al((size_t)P * nl * 4);
   // the lanes launch() would give GA: 32 lanes (KD = 160 constants) for the small
   // batches of a multi-GPU shard, where GA's chain latency is the critical path
-  // or the one-wave cooperative shape (ga_coop: a rank's small slice)
-  const bool coop = ga_coop(2 * P, nn);
-  const uint32_t group = coop ? kCoopGroup : ga_lanes(2 * P, nn), per_wave = group <= 64 ? 64 / group : 0;
+  const uint32_t group = ga_lanes(2 * P, nn), per_wave = group <= 64 ? 64 / group : 0;
   // descriptors with out_idx, for 2P chains + at most per_wave - 1 pads per receiver
   const size_t desc_bytes = ((size_t)2 * P + (size_t)n * (per_wave ? per_wave - 1 : 0)) * 36,
                o_out = o_desc + al(desc_bytes);
@@ -944,10 +942,8 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   uint32_t* S1 = reinterpret_cast<uint32_t*>(img + o_s);
   std::vector<uint32_t> rbits(n);
   std::vector<uint32_t> sess_of_recv(n);
-  const uint32_t coopK = coop ? coop_digits(nn) : 0;
-  std::vector<uint32_t> coop_cons((size_t)n * 4 * coopK);   // coop_constants of every N_i^2
   for (uint32_t k = 0; k < count; ++k) std::fill(sess_of_recv.begin() + ss[k].rbase, sess_of_recv.begin() + ss[k].rbase + ss[k].n, k);
-  parallel_for(n, coop ? 1 : 64, [&](size_t r0, size_t r1) {
+  parallel_for(n, 64, [&](size_t r0, size_t r1) {
     for (size_t r = r0; r < r1; ++r) {
       const GaPre::Sess& x = ss[sess_of_recv[r]];
       const uint32_t* Np = bs[sess_of_recv[r]].recv_n + (r - x.rbase) * x.nl;
@@ -955,7 +951,6 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
       hbn::store(hbn::mul(N, N), NN + r * nn, nn);
       memcpy(RN + r * nl, Np, (size_t)x.nl * 4);
       rbits[r] = hbn::bitlen(Np, x.nl);
-      if (coop) coop_constants(NN + r * nn, nn, coopK, coop_cons.data() + r * 4 * coopK);
     }
   });
   uint32_t recvn_max = 1;
@@ -1023,21 +1018,8 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   g.split = ga_split_ok(nn, group, flags);
   SplitArgs head;
   head.lo_bit = kGaSplit;
-  const uint32_t* ga_cons = cons;
-  if (coop) {   // whole chains on the cooperative shape, from its own constants
-    uint32_t* cc = (uint32_t*)c->buf("collect_ga_coop", coop_cons.size() * 4);
-    if (!cc) {
-      c->fail("fsdkr_collect_prestart: device allocation failed (cooperative constants)");
-      return FSDKR_E_OOM;
-    }
-    if ((rc = c->hip_check(hipMemcpyAsync(cc, coop_cons.data(), coop_cons.size() * 4, hipMemcpyHostToDevice, gs),
-                           "H2D coop constants")) ||
-        (rc = c->hip_check(hipStreamSynchronize(gs), "coop constants H2D")))   // (coop_cons goes out of scope)
-      return rc;
-    ga_cons = cc;
-  }
-  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, ga_cons, g.out, gs, "mxt_GApre", gprio,
-                               group, flags, g.split ? &head : nullptr)))
+  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", gprio, group,
+                               flags, g.split ? &head : nullptr)))
     return rc;
   g.ga_group = group;
   g.ga_flags = flags;

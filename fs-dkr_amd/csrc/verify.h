@@ -35,30 +35,6 @@ struct AliceHashArgs {      // H(N, N+1, c, z, u, w) == e
   uint32_t count;
 };
 
-// One-wave cooperative modexp (coop.hip): one instance per wave, separated
-// Montgomery over 28-bit digits (R = 2^(28 K), K = coop_digits(k32)), sliding
-// windows over the instance's exponent.  consts: [n_mod][4K] = N | R mod N |
-// R^2 mod N | -N^-1 mod R (coop_constants, host).
-struct CoopArgs {
-  const uint64_t* base_ptr;   // [count] K32 limbs (base_len of them)
-  const uint32_t* base_len;
-  const uint64_t* exp_ptr;    // [count]
-  const uint32_t* exp_len;
-  const uint32_t* mod_idx;    // [count] row of consts
-  const uint32_t* consts;
-  uint32_t* out;              // [count][K32] (row out_idx[i] when set)
-  const uint32_t* out_idx;
-  uint32_t* table;            // [count][2^(window-1) + 1][K] scratch
-  uint32_t window;
-  uint32_t count;
-  uint32_t prio;              // > 0: s_setprio(prio) (as ModexpArgs.prio)
-};
-constexpr uint32_t kCoopGroup = 256;   // fsdkr_ctx_set_modexp_group value selecting it
-uint32_t coop_digits(uint32_t k32);    // 0: no cooperative shape for this width
-hipError_t launch_modexp_coop(uint32_t k32, const CoopArgs& a, hipStream_t st);
-// the 4K constant words of one modulus (k32 little-endian limbs, odd)
-void coop_constants(const uint32_t* n, uint32_t k32, uint32_t K, uint32_t* out);
-
 struct InverseArgs {
   const uint64_t* y_ptr;    // value to invert (reduced, K32 limbs)
   const uint64_t* m_ptr;    // odd modulus (K32 limbs)

@@ -19,7 +19,7 @@ LIB = os.path.join(PKG, "libfsdkr.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["modexp.hip", "coop.hip", "coop_host.cpp", "fixedbase.hip", "comb.hip", "inverse.hip", "vhash.hip", "vmont.hip", "vec.hip", "pow2.hip",
+SOURCES = ["modexp.hip", "fixedbase.hip", "comb.hip", "inverse.hip", "vhash.hip", "vmont.hip", "vec.hip", "pow2.hip",
            "prime.hip", "capi.cpp", "keygen.cpp", "collect.cpp", "collect_prestart.cpp", "collect_prepare.cpp",
            "collect_launch.cpp", "recover.cpp", "standalone.cpp", "fixedbase_host.cpp"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
