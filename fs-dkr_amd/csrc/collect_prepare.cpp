@@ -474,6 +474,27 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   const size_t o_ps1 = field(&B::pdl_s1, R_pair, W_s1, s1l), o_ps2 = field(&B::pdl_s2, R_pair, W_nl, nl);
   const size_t o_ps3 = field(&B::pdl_s3, R_pair, W_s3, s3l);
   const size_t o_az = field(&B::rp_z, R_pair, W_nl, nl), o_ae = field(&B::rp_e, R_pair, W_el, el);
+  // negative z (fsdkr_collect_batch.z_neg): the rows hold |z| (hashed); z^e takes -|z| mod N~
+  std::vector<uint32_t> zneg_row(2 * (size_t)P, ~0u), ZR;
+  for (const Sess& x : pl.ss)
+    if (x.b->z_neg)
+      for (uint32_t lp = 0; lp < x.P; ++lp)
+        for (int which = 0; which < 2; ++which)
+          if (x.b->z_neg[lp] & (1u << which)) {
+            const uint32_t p = x.pbase + lp, r = recv_of_pair[p];
+            const uint32_t* zr = (which ? x.b->rp_z : x.b->pdl_z) + (size_t)lp * x.b->nl;
+            const hbn::Limbs Nt = hbn::from(x.b->recv_ntilde + (size_t)(r - x.rbase) * x.b->nl, x.b->nl);
+            const hbn::Limbs zm = hbn::mod(hbn::from(zr, x.b->nl), Nt);
+            const hbn::Limbs res = zm.empty() ? zm : hbn::sub(Nt, zm);
+            zneg_row[(size_t)which * P + p] = (uint32_t)(ZR.size() / nl);
+            ZR.resize(ZR.size() + nl);
+            hbn::store(res, ZR.data() + ZR.size() - nl, nl);
+          }
+  const size_t o_zr = ZR.empty() ? 0 : I.own(ZR);
+  auto z_off = [&](int which, uint32_t p, size_t o_raw) {   // image offset of z's row as J5's base
+    const uint32_t k = zneg_row[(size_t)which * P + p];
+    return k == ~0u ? o_raw + (size_t)p * nl * 4 : o_zr + (size_t)k * nl * 4;
+  };
   const size_t o_as = field(&B::rp_s, R_pair, W_nl, nl), o_as1 = field(&B::rp_s1, R_pair, W_s1, s1l);
   const size_t o_as2 = field(&B::rp_s2, R_pair, W_s3, s3l);
   const size_t o_vss = I.reserve((size_t)V * 64);
@@ -677,7 +698,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
           FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
           fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
         }
-        if (!pl.ch_hit) J5.add(DI(o_pz + (size_t)p * nl * 4), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
+        if (!pl.ch_hit) J5.add(DI(z_off(0, p, o_pz)), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
         if (!pl.fx_hit) {
@@ -685,7 +706,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
           fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
                               DX(x_J4 + slot * nl * 4)});
         }
-        if (!pl.ch_hit) J5.add(DI(o_az + (size_t)p * nl * 4), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
+        if (!pl.ch_hit) J5.add(DI(z_off(1, p, o_az)), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
       }
     }
   for (uint32_t p = 0; p < P; ++p)

@@ -16,11 +16,11 @@ check), a LocalKey with fewer keys than receivers (panic at the first pair
 past them, :334-339), an ek.n wider than the batch's moduli (its correct-key
 proof runs at its own width before ModuliTooSmall, :376-391), and negative
 BigInts where the reference's outcome for that instance is a panic, an error,
-a plain residue or an h2^-1 exponent (_Negatives: PDL s1 / u2 / u3 / s2 / s3,
-Alice s / s1 / s2 / e, ring-Pedersen Z, DLog y).  Still outside the
-representable set (UnsupportedInput): other negative fields (hashed AND reduced
-values such as c, z, A) and values wider than 3072 bits in a proof field (6144
-bits for ek.n / sigma)."""
+a plain residue, an h2^-1 exponent or a hashed-and-reduced value (_Negatives:
+PDL s1 / u2 / u3 / s2 / s3 / z, Alice s / s1 / s2 / e / z, ring-Pedersen Z,
+DLog y).  Still outside the representable set (UnsupportedInput): the other
+hashed-and-reduced fields (the ciphertext c, ring-Pedersen A) and values wider
+than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
 import ctypes
 import math
 import os
@@ -191,10 +191,13 @@ class _Negatives:
       s2 < 0 is the base of s2^N mod N^2: packed as s2 mod N^2; s3 < 0 raises
       h2^-1 to |s3| (commitment_unknown_order, :177-184): mod_inv(h2).unwrap()
       panics when h2 is not a unit mod N~, else |s3| is packed with the pair's
-      pdl_s3_neg flag and the device checks h1^s1 == u3 * z^e * h2^|s3|.
+      pdl_s3_neg flag and the device checks h1^s1 == u3 * z^e * h2^|s3|;
+      z < 0 hashes as |z| and is the base of z^e mod N~ (GMP reduces it): |z|
+      is packed with the pair's z_neg bit, the device raises -|z| mod N~.
     - Alice (range_proofs.rs:112-164): s1 > q^3 -> false first; e < 0 panics
       in z^e; z^e not invertible -> false; then s1 / s2 < 0 panic in h1^s1 /
-      h2^s2; s < 0 is the base of s^N mod N^2 (packed as s mod N^2).
+      h2^s2; s < 0 is the base of s^N mod N^2 (packed as s mod N^2); z < 0 as
+      PDL's z (z_neg bit 1).
     - ring-Pedersen (ring_pedersen_proof.rs:126-157): Z[i] < 0 panics at
       iteration i, after checks 0..i-1 -- exactly the short-Z mechanism
       (ped_lens: Z "ends" at its first negative entry).
@@ -208,6 +211,7 @@ class _Negatives:
         self.range = {}    # pair -> verdict (0 false, 2 panic)
         self.dlog = {}     # join -> "y1-panic" | "y1-false" | "y2"
         self.s3 = None     # [pairs] uint8 pdl_s3_neg flags (None: no negative s3)
+        self.z = None      # [pairs] uint8 z_neg flags: bit 0 PDL z, bit 1 Alice z
 
     def __bool__(self):
         return bool(self.rows)
@@ -230,6 +234,11 @@ class _Negatives:
         """the verdict rules, once every field is gathered"""
         for p in self.rows.get("pdl_s1", ()):
             self.pdl[p] = (8, 0xFF)
+        if self.rows.get("pdl_z") or self.rows.get("rp_z"):
+            self.z = np.zeros(len(pdl), np.uint8)
+            for name, bit in (("pdl_z", 1), ("rp_z", 2)):
+                for p in self.rows.get(name, ()):
+                    self.z[p] |= bit
         if self.rows.get("pdl_s3"):
             self.s3 = np.zeros(len(pdl), np.uint8)
             for p in self.rows["pdl_s3"]:
@@ -528,9 +537,10 @@ class CollectBatch:
             self._points(st)
         if self.negs:
             self.negs.decide(msgs, joins, n, st["avail"], st["pdl"], st["rng"], st["sts"])
-            if self.negs.s3 is not None:
-                self._keep.append(self.negs.s3)
-                c.pdl_s3_neg = self.negs.s3.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+            for arr, attr in ((self.negs.s3, "pdl_s3_neg"), (self.negs.z, "z_neg")):
+                if arr is not None:
+                    self._keep.append(arr)
+                    setattr(c, attr, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
         self.nl = nl
         return self
 
@@ -543,10 +553,10 @@ class CollectBatch:
         F, G, pdl, rng, n = st["F"], st["G"], st["pdl"], st["rng"], st["n"]
         neg = self.negs
         F["enc"] = G.field([m.points_encrypted_vec[i] for m in st["msgs"] for i in range(n)])
-        F["pdl_z"] = G.field(pdl, "z")
+        F["pdl_z"] = neg.field(G, "pdl_z", pdl, "z", _magnitude)
         for a in ("u2", "u3"):
             F["pdl_" + a] = neg.field(G, "pdl_" + a, pdl, a, _magnitude)
-        F["rp_z"] = G.field(rng, "z")
+        F["rp_z"] = neg.field(G, "rp_z", rng, "z", _magnitude)
         F["rp_e"] = neg.field(G, "rp_e", rng, "e", _zero)
         if st["joins"]:
             for name, attr in (("N", "N"), ("g", "g"), ("ni", "ni")):

@@ -193,7 +193,11 @@ typedef struct fsdkr_collect_batch {
    *             (zk_pdl_with_slack.rs:177-184); the u3 check is evaluated as
    *             h1^s1 == u3 * z^e * h2^|s3| (mod N~), equivalent when h2 is a unit.
    *             The caller reports the pairs whose h2 is not a unit (mod_inv
-   *             unwrap panics) itself; their u3 bit here is meaningless. */
+   *             unwrap panics) itself; their u3 bit here is meaningless.
+   *  z_neg      [R*n] bit 0: the pair's PDL z is negative, bit 1: its Alice z is;
+   *             pdl_z / rp_z then hold |z|.  The challenges hash |z| (curv to_bytes),
+   *             z^e takes the residue -|z| mod N~ (GMP mpz_powm reduces a negative
+   *             base; zk_pdl_with_slack.rs:151-157, range_proofs.rs:129). */
   const uint32_t* vss_len;
   const uint32_t* range_lens;
   uint32_t ckl;
@@ -201,6 +205,7 @@ typedef struct fsdkr_collect_batch {
   const uint32_t* ped_lens;
   const uint32_t* ck_lens;
   const uint8_t* pdl_s3_neg;
+  const uint8_t* z_neg;
 } fsdkr_collect_batch;
 
 /* Verdicts (caller-allocated). 1 bits mean "check passed".  cap_* are the

@@ -203,6 +203,59 @@ def dkr_negative_s3(t, n, seed, senders):
     return keys, msgs, dks
 
 
+def dkr_negative_z(t, n, seed, senders):
+    """_dkr with every PDL proof of the given senders carrying z - N~ (the same
+    residue, negative): the prover hashes the negative z (|z| through to_bytes),
+    so the proofs stay valid -- the reference reduces z in z^e mod N~."""
+    from oracle import zk_pdl_with_slack as zpdl
+    rng = Rng(seed)
+    keys = protocol.simulate_keygen(t, n, rng, KB)
+    msgs, dks = [], []
+    orig_prove, orig_cuo = zpdl.prove, zpdl.commitment_unknown_order
+
+    def prove(x, r, st, g):
+        first = [True]
+
+        def cuo(h1, h2, N, a, b):   # the prover's first commitment is z
+            v = orig_cuo(h1, h2, N, a, b)
+            if first[0]:
+                first[0] = False
+                return v - N
+            return v
+        zpdl.commitment_unknown_order = cuo
+        try:
+            return orig_prove(x, r, st, g)
+        finally:
+            zpdl.commitment_unknown_order = orig_cuo
+    for key in keys:
+        if key.i in senders:
+            zpdl.prove = prove
+        try:
+            m, dk = protocol.distribute(key.i, key, n, rng, KB)
+        finally:
+            zpdl.prove = orig_prove
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks
+
+
+def test_negative_z_packed_as_magnitude(dkr4):
+    """PDL / Alice z < 0 (hashed as |z|, reduced in z^e): |z| packed with the pair's
+    z_neg bit; valid negative-z proofs verify in the oracle."""
+    from fsdkr.batch import CollectBatch
+    from fsdkr._native import limbs_to_ints
+    keys, msgs, dks = dkr_negative_z(1, 4, "neg-z-t1n4", {2})
+    assert all(p.z < 0 for p in msgs[1].pdl_proof_vec)
+    assert oracle_outcome(msgs, keys[0], dks[0]) is None
+    m2 = _alice(msgs, 3, 2, z=lambda a: -a.z)
+    b = CollectBatch(m2, keys[0], [], 256, KB)
+    flags = np.ctypeslib.as_array(b.c.z_neg, shape=(16,)).tolist()
+    assert flags == [1 if k == 1 else 0 for k in range(4) for i in range(4)][:12] + [0, 0, 2, 0]
+    z = limbs_to_ints(np.ctypeslib.as_array(b.c.pdl_z, shape=(16, b.nl)))
+    assert z == [abs(m.pdl_proof_vec[i].z) for m in m2 for i in range(4)]
+    assert host_outcome(msgs, keys[0]) is None
+
+
 @pytest.fixture(scope="module")
 def neg_s3():
     return dkr_negative_s3(1, 4, "neg-s3-t1n4", {1, 3})
@@ -240,11 +293,12 @@ def test_negative_pdl_s3_h2_not_unit(neg_s3):
 
 
 def test_negative_outside_the_rules_still_unsupported(dkr4):
-    """a negative PDL z is hashed and reduced (z^e mod N~): still UnsupportedInput
-    for the batch"""
+    """a negative ciphertext is hashed and reduced (c^e mod N^2, the share's
+    decryption): still UnsupportedInput for the batch"""
     from fsdkr.batch import CollectBatch, UnsupportedInput
     keys, msgs, dks = dkr4
-    m2 = _pdl(msgs, 0, 0, z=lambda p: -p.z)
+    m2 = copy.deepcopy(msgs)
+    m2[0].points_encrypted_vec[1] = -m2[0].points_encrypted_vec[1]
     with pytest.raises(UnsupportedInput):
         CollectBatch(m2, keys[0], [], 256, KB)
 

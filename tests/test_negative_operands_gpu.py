@@ -16,7 +16,7 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from test_edge_outcomes_gpu import KB, _check, _dkr, _joins_setup  # noqa: E402
-from test_negative_operands import _alice, _pdl, dkr_negative_s3  # noqa: E402
+from test_negative_operands import _alice, _pdl, dkr_negative_s3, dkr_negative_z  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -74,6 +74,25 @@ def test_negative_pdl_s3(gpu_ctx, neg_s3):
     # the first message's s3 is positive: its u3 fails before any unwrap is reached
     _check(gpu_ctx, msgs, key, dks[0], expect="PDLwSlackProof")
     _check(gpu_ctx, _pdl(msgs, 0, 3, s3=lambda p: -p.s3), key, dks[0], expect="panic")
+
+
+def test_negative_z(gpu_ctx):
+    """z < 0 is hashed as |z| and reduced in z^e mod N~ (zk_pdl_with_slack.rs:114-122,
+    151-157; range_proofs.rs:129,150-157): valid PDL proofs carrying z - N~ -> Ok
+    with the oracle's LocalKey; a sign-flipped PDL / Alice z -> the oracle's outcome
+    (the same challenge, z^e off by (-1)^e: Ok for an even e); z = -N~ (residue 0,
+    no z^-1) -> the oracle's outcome."""
+    keys, msgs, dks = dkr_negative_z(2, 5, "neg-z-gpu-t2n5", {3})
+    assert all(p.z < 0 for p in msgs[2].pdl_proof_vec)
+    for r in (0, 2):
+        assert _check(gpu_ctx, msgs, keys[r], dks[r]) is None
+    # -z: the same hash, z^e times (-1)^e -- fails only for an odd challenge
+    outs = [_check(gpu_ctx, _pdl(msgs, k, i, z=lambda p: -p.z), keys[0], dks[0]) for k in (0, 1) for i in range(5)]
+    outs += [_check(gpu_ctx, _alice(msgs, k, i, z=lambda a: -a.z), keys[0], dks[0]) for k, i in ((1, 3), (3, 0), (4, 4))]
+    assert {o[0] for o in outs if o} == {"PDLwSlackProof", "RangeProof"}, outs
+    nt = keys[0].h1_h2_n_tilde_vec[1].N
+    _check(gpu_ctx, _pdl(msgs, 3, 1, z=lambda p: -nt), keys[0], dks[0])
+    _check(gpu_ctx, _alice(msgs, 4, 1, z=lambda a: -nt), keys[0], dks[0])
 
 
 def test_negative_alice_operands(gpu_ctx, dkr5):
@@ -134,6 +153,14 @@ def test_collect_many_negative_session_alone(gpu_ctx, dkr5):
     m2 = _pdl(msgs, 4, 2, s1=lambda p: -p.s1)
     sessions = [(msgs, 0), (m2, 1), (msgs, 2)]
     _collect_many_like_oracle(gpu_ctx, keys, dks, sessions)
+
+
+def test_collect_many_negative_z_session(gpu_ctx):
+    """collect_many: a session of valid negative-z proofs (its own batch, z_neg)
+    beside regular sessions of the same keys."""
+    keys, msgs, dks = dkr_negative_z(2, 5, "neg-z-many", {1})
+    m_ok = _pdl(msgs, 0, 0, z=lambda p: p.z)
+    _collect_many_like_oracle(gpu_ctx, keys, dks, [(msgs, 0), (m_ok, 3), (msgs, 4)])
 
 
 def test_collect_many_negative_s3_session(gpu_ctx, neg_s3):
