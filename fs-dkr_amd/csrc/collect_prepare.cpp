@@ -169,7 +169,9 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       const size_t lp = p - x.pbase;
       if (hash && !pdl_challenge(sha, b, lp, EPDL.data() + p * 8)) sha_fail = true;
       // a ciphertext at or above N^2 (GMP reduces it; the joint tail's inverse needs it reduced)
-      big_c[p] = hbn::cmp_raw(b->enc + lp * 2 * b->nl, 2 * b->nl, NN.data() + (size_t)recv_of_pair[p] * nn, nn) >= 0;
+      // (or a negative one, neg_bits bit 2: enc holds |c|, the arithmetic takes -|c| mod N^2)
+      big_c[p] = hbn::cmp_raw(b->enc + lp * 2 * b->nl, 2 * b->nl, NN.data() + (size_t)recv_of_pair[p] * nn, nn) >= 0 ||
+                 (b->neg_bits && (b->neg_bits[lp] & 4));
       const uint32_t* Np = b->recv_n + (size_t)(lp % x.n) * b->nl;
       const uint32_t* s1 = b->pdl_s1 + lp * b->s1l;
       // s1 < N -> (N+1)^s1 mod N^2 = 1 + s1*N  (binomial, bit-identical)
@@ -200,15 +202,21 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     mx.big_s1 = mx.big_s1 || t.big_s1;
   }
   clk.lap("pair scan + PDL challenges");
-  std::vector<uint32_t> RC;   // c mod N^2 of the ciphertexts at or above N^2 (joint tail only)
-  if (pl.joint && std::find(big_c.begin(), big_c.end(), 1) != big_c.end()) {
+  // c mod N^2 of the ciphertexts at or above N^2 (the joint tail's inverse needs it
+  // reduced) and -|c| mod N^2 of the negative ones (every use but the hashes)
+  std::vector<uint32_t> RC;
+  if (std::find(big_c.begin(), big_c.end(), 1) != big_c.end()) {
     RC.assign((size_t)P * nn, 0u);
     parallel_for(P, 64, [&](size_t b0, size_t b1) {
       for (size_t p = b0; p < b1; ++p) {
         if (!big_c[p]) continue;
         const Sess& x = pl.ss[sess_of_pair[p]];
-        const hbn::Limbs cc = hbn::from(x.b->enc + (p - x.pbase) * 2 * x.b->nl, 2 * x.b->nl);
-        hbn::store(hbn::mod(cc, hbn::from(NN.data() + (size_t)recv_of_pair[p] * nn, nn)), RC.data() + p * nn, nn);
+        const size_t lp = p - x.pbase;
+        const hbn::Limbs cc = hbn::from(x.b->enc + lp * 2 * x.b->nl, 2 * x.b->nl);
+        const hbn::Limbs NNr = hbn::from(NN.data() + (size_t)recv_of_pair[p] * nn, nn);
+        hbn::Limbs v = hbn::mod(cc, NNr);
+        if (x.b->neg_bits && (x.b->neg_bits[lp] & 4) && !v.empty()) v = hbn::sub(NNr, v);
+        hbn::store(v, RC.data() + p * nn, nn);
       }
     });
   }
@@ -474,13 +482,13 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   const size_t o_ps1 = field(&B::pdl_s1, R_pair, W_s1, s1l), o_ps2 = field(&B::pdl_s2, R_pair, W_nl, nl);
   const size_t o_ps3 = field(&B::pdl_s3, R_pair, W_s3, s3l);
   const size_t o_az = field(&B::rp_z, R_pair, W_nl, nl), o_ae = field(&B::rp_e, R_pair, W_el, el);
-  // negative z (fsdkr_collect_batch.z_neg): the rows hold |z| (hashed); z^e takes -|z| mod N~
+  // negative z (fsdkr_collect_batch.neg_bits): the rows hold |z| (hashed); z^e takes -|z| mod N~
   std::vector<uint32_t> zneg_row(2 * (size_t)P, ~0u), ZR;
   for (const Sess& x : pl.ss)
-    if (x.b->z_neg)
+    if (x.b->neg_bits)
       for (uint32_t lp = 0; lp < x.P; ++lp)
         for (int which = 0; which < 2; ++which)
-          if (x.b->z_neg[lp] & (1u << which)) {
+          if (x.b->neg_bits[lp] & (1u << which)) {
             const uint32_t p = x.pbase + lp, r = recv_of_pair[p];
             const uint32_t* zr = (which ? x.b->rp_z : x.b->pdl_z) + (size_t)lp * x.b->nl;
             const hbn::Limbs Nt = hbn::from(x.b->recv_ntilde + (size_t)(r - x.rbase) * x.b->nl, x.b->nl);
@@ -684,7 +692,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       if (!pl.ga_hit)
         J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
-      const uint64_t cp = DI(o_enc + (size_t)p * nn * 4);
+      const uint64_t cp = big_c[p] ? DI(o_rc + (size_t)p * nn * 4) : DI(o_enc + (size_t)p * nn * 4);
       if (pl.ch_hit || pl.joint) {   // (prestarted, or joined into GA's tail)
       } else if (which == 0) {
         J2.add(cp, nn, DI(o_epdl + (size_t)p * 32), 8, 256, r);

@@ -799,7 +799,7 @@ bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t coun
     const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
     if (b->nl != nl || b->el != el || b->s1l != s1l || x.n != ns || x.R != b->n_refresh || b->range_lens ||
         b->recv_avail || !b->enc || !b->pdl_z || !b->pdl_u1 || !b->pdl_u2 || !b->pdl_u3 || !b->commit || !b->rp_z ||
-        !b->rp_e || !b->pdl_s1 || !b->rp_s1 || !b->vss || vlen[k] != (b->vss_len ? 1u : 0u) || b->z_neg)
+        !b->rp_e || !b->pdl_s1 || !b->rp_s1 || !b->vss || vlen[k] != (b->vss_len ? 1u : 0u) || b->neg_bits)
       return false;   // (negative z: prepare's J5 takes residue rows)
     uint32_t vk = 0;
     for (uint32_t m = 0; m < x.R; ++m, ++q) {

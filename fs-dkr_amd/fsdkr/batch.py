@@ -17,10 +17,10 @@ past them, :334-339), an ek.n wider than the batch's moduli (its correct-key
 proof runs at its own width before ModuliTooSmall, :376-391), and negative
 BigInts where the reference's outcome for that instance is a panic, an error,
 a plain residue, an h2^-1 exponent or a hashed-and-reduced value (_Negatives:
-PDL s1 / u2 / u3 / s2 / s3 / z, Alice s / s1 / s2 / e / z, ring-Pedersen Z,
-DLog y).  Still outside the representable set (UnsupportedInput): the other
-hashed-and-reduced fields (the ciphertext c, ring-Pedersen A) and values wider
-than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
+PDL s1 / u2 / u3 / s2 / s3 / z, Alice s / s1 / s2 / e / z, the ciphertext c,
+ring-Pedersen Z, DLog y).  Still outside the representable set
+(UnsupportedInput): a negative ring-Pedersen A (hashed and reduced) and values
+wider than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
 import ctypes
 import math
 import os
@@ -193,11 +193,13 @@ class _Negatives:
       panics when h2 is not a unit mod N~, else |s3| is packed with the pair's
       pdl_s3_neg flag and the device checks h1^s1 == u3 * z^e * h2^|s3|;
       z < 0 hashes as |z| and is the base of z^e mod N~ (GMP reduces it): |z|
-      is packed with the pair's z_neg bit, the device raises -|z| mod N~.
+      is packed with the pair's neg_bits bit, the device raises -|z| mod N~;
+      the ciphertext c < 0 likewise (bit 2: |c| hashed by both proofs, -|c|
+      mod N^2 in c^e, c^-1 and, on the host, the share decryption).
     - Alice (range_proofs.rs:112-164): s1 > q^3 -> false first; e < 0 panics
       in z^e; z^e not invertible -> false; then s1 / s2 < 0 panic in h1^s1 /
       h2^s2; s < 0 is the base of s^N mod N^2 (packed as s mod N^2); z < 0 as
-      PDL's z (z_neg bit 1).
+      PDL's z (neg_bits bit 1).
     - ring-Pedersen (ring_pedersen_proof.rs:126-157): Z[i] < 0 panics at
       iteration i, after checks 0..i-1 -- exactly the short-Z mechanism
       (ped_lens: Z "ends" at its first negative entry).
@@ -211,7 +213,7 @@ class _Negatives:
         self.range = {}    # pair -> verdict (0 false, 2 panic)
         self.dlog = {}     # join -> "y1-panic" | "y1-false" | "y2"
         self.s3 = None     # [pairs] uint8 pdl_s3_neg flags (None: no negative s3)
-        self.z = None      # [pairs] uint8 z_neg flags: bit 0 PDL z, bit 1 Alice z
+        self.z = None      # [pairs] uint8 neg_bits flags: bit 0 PDL z, bit 1 Alice z, bit 2 c
 
     def __bool__(self):
         return bool(self.rows)
@@ -234,9 +236,9 @@ class _Negatives:
         """the verdict rules, once every field is gathered"""
         for p in self.rows.get("pdl_s1", ()):
             self.pdl[p] = (8, 0xFF)
-        if self.rows.get("pdl_z") or self.rows.get("rp_z"):
+        if self.rows.get("pdl_z") or self.rows.get("rp_z") or self.rows.get("enc"):
             self.z = np.zeros(len(pdl), np.uint8)
-            for name, bit in (("pdl_z", 1), ("rp_z", 2)):
+            for name, bit in (("pdl_z", 1), ("rp_z", 2), ("enc", 4)):
                 for p in self.rows.get(name, ()):
                     self.z[p] |= bit
         if self.rows.get("pdl_s3"):
@@ -537,7 +539,7 @@ class CollectBatch:
             self._points(st)
         if self.negs:
             self.negs.decide(msgs, joins, n, st["avail"], st["pdl"], st["rng"], st["sts"])
-            for arr, attr in ((self.negs.s3, "pdl_s3_neg"), (self.negs.z, "z_neg")):
+            for arr, attr in ((self.negs.s3, "pdl_s3_neg"), (self.negs.z, "neg_bits")):
                 if arr is not None:
                     self._keep.append(arr)
                     setattr(c, attr, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
@@ -552,7 +554,8 @@ class CollectBatch:
         st["late"] = True
         F, G, pdl, rng, n = st["F"], st["G"], st["pdl"], st["rng"], st["n"]
         neg = self.negs
-        F["enc"] = G.field([m.points_encrypted_vec[i] for m in st["msgs"] for i in range(n)])
+        F["enc"] = neg.field(G, "enc", [m.points_encrypted_vec[i] for m in st["msgs"] for i in range(n)], None,
+                             _magnitude)
         F["pdl_z"] = neg.field(G, "pdl_z", pdl, "z", _magnitude)
         for a in ("u2", "u3"):
             F["pdl_" + a] = neg.field(G, "pdl_" + a, pdl, a, _magnitude)

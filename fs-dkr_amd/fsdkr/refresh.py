@@ -420,10 +420,11 @@ def _speculative_launch(ctx, jobs):
             if nl is None:
                 raise FsDkrPanic("share recovery: decryption key wider than 6144 bits")
             # Paillier::mul / add / decrypt reduce their operands mod N^2 (powm and
-            # mulm mod NN), so a ciphertext c + k N^2 recovers like c: reduce here,
-            # the C ABI takes ciphertexts below 2^(64 nl) (fsdkr.h)
+            # mulm mod NN), so a ciphertext c + k N^2 -- or a negative one --
+            # recovers like its residue: reduce here, the C ABI takes ciphertexts in
+            # [0, 2^(64 nl)) (fsdkr.h)
             nn_ = (lk.paillier_dk.p * lk.paillier_dk.q) ** 2
-            cts = [c % nn_ if nn_ and c >= nn_ else c for c in plan["cts"]]   # p or q = 0: the GPU reports it
+            cts = [c % nn_ if nn_ and (c >= nn_ or c < 0) else abs(c) for c in plan["cts"]]   # p or q = 0: the GPU reports it
             if not decrypt:
                 todo.append(k)
                 cj.append(dict(nl=64, t_vss=plan["t_vss"], t_key=lk.t, old_index=plan["index"], cts=[0] *

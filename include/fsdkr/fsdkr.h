@@ -194,10 +194,13 @@ typedef struct fsdkr_collect_batch {
    *             h1^s1 == u3 * z^e * h2^|s3| (mod N~), equivalent when h2 is a unit.
    *             The caller reports the pairs whose h2 is not a unit (mod_inv
    *             unwrap panics) itself; their u3 bit here is meaningless.
-   *  z_neg      [R*n] bit 0: the pair's PDL z is negative, bit 1: its Alice z is;
-   *             pdl_z / rp_z then hold |z|.  The challenges hash |z| (curv to_bytes),
-   *             z^e takes the residue -|z| mod N~ (GMP mpz_powm reduces a negative
-   *             base; zk_pdl_with_slack.rs:151-157, range_proofs.rs:129). */
+   *  neg_bits   [R*n] bit 0: the pair's PDL z is negative, bit 1: its Alice z is,
+   *             bit 2: its ciphertext c is; pdl_z / rp_z / enc then hold the
+   *             magnitude.  The challenges hash |v| (curv to_bytes); the arithmetic
+   *             takes the residue -|v| mod N~ (z^e) or mod N^2 (c^e, c^-1), as GMP
+   *             reduces a negative base (zk_pdl_with_slack.rs:114-122,136-157;
+   *             range_proofs.rs:129-157).  The caller's share decryption reduces its
+   *             own ciphertexts (Paillier::mul / add work mod N^2, :221-234). */
   const uint32_t* vss_len;
   const uint32_t* range_lens;
   uint32_t ckl;
@@ -205,7 +208,7 @@ typedef struct fsdkr_collect_batch {
   const uint32_t* ped_lens;
   const uint32_t* ck_lens;
   const uint8_t* pdl_s3_neg;
-  const uint8_t* z_neg;
+  const uint8_t* neg_bits;
 } fsdkr_collect_batch;
 
 /* Verdicts (caller-allocated). 1 bits mean "check passed".  cap_* are the

@@ -241,7 +241,7 @@ def dkr_negative_z(t, n, seed, senders):
 
 def test_negative_z_packed_as_magnitude(dkr4):
     """PDL / Alice z < 0 (hashed as |z|, reduced in z^e): |z| packed with the pair's
-    z_neg bit; valid negative-z proofs verify in the oracle."""
+    neg_bits bit; valid negative-z proofs verify in the oracle."""
     from fsdkr.batch import CollectBatch
     from fsdkr._native import limbs_to_ints
     keys, msgs, dks = dkr_negative_z(1, 4, "neg-z-t1n4", {2})
@@ -249,7 +249,7 @@ def test_negative_z_packed_as_magnitude(dkr4):
     assert oracle_outcome(msgs, keys[0], dks[0]) is None
     m2 = _alice(msgs, 3, 2, z=lambda a: -a.z)
     b = CollectBatch(m2, keys[0], [], 256, KB)
-    flags = np.ctypeslib.as_array(b.c.z_neg, shape=(16,)).tolist()
+    flags = np.ctypeslib.as_array(b.c.neg_bits, shape=(16,)).tolist()
     assert flags == [1 if k == 1 else 0 for k in range(4) for i in range(4)][:12] + [0, 0, 2, 0]
     z = limbs_to_ints(np.ctypeslib.as_array(b.c.pdl_z, shape=(16, b.nl)))
     assert z == [abs(m.pdl_proof_vec[i].z) for m in m2 for i in range(4)]
@@ -292,13 +292,52 @@ def test_negative_pdl_s3_h2_not_unit(neg_s3):
     assert host_outcome(msgs, key) == ("panic",)
 
 
+def dkr_negative_c(t, n, seed, senders):
+    """_dkr with the given senders' ciphertexts replaced by c - N_i^2 (the same
+    residue, negative) BEFORE their PDL and Alice proofs are made over them, so
+    the proofs (which hash |c|) stay valid; the reference reduces c in c^e,
+    c^-1 and the share decryption."""
+    from oracle import paillier
+    rng = Rng(seed)
+    keys = protocol.simulate_keygen(t, n, rng, KB)
+    msgs, dks = [], []
+    orig = paillier.encrypt_with_chosen_randomness
+    for key in keys:
+        if key.i in senders:
+            paillier.encrypt_with_chosen_randomness = lambda ek, m, r: orig(ek, m, r) - ek.nn
+        try:
+            m, dk = protocol.distribute(key.i, key, n, rng, KB)
+        finally:
+            paillier.encrypt_with_chosen_randomness = orig
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks
+
+
+def test_negative_c_packed_as_magnitude():
+    """negative ciphertexts: |c| packed (both proofs hash it) with neg_bits bit 2,
+    valid in the oracle; the local party's own ciphertexts decrypt as residues"""
+    from fsdkr.batch import CollectBatch
+    from fsdkr._native import limbs_to_ints
+    keys, msgs, dks = dkr_negative_c(1, 4, "neg-c-t1n4", {3})
+    assert all(c < 0 for c in msgs[2].points_encrypted_vec)
+    assert oracle_outcome(msgs, keys[1], dks[1]) is None
+    b = CollectBatch(msgs, keys[1], [], 256, KB)
+    assert np.ctypeslib.as_array(b.c.neg_bits, shape=(16,)).tolist() == [4 if k == 2 else 0 for k in range(4)
+                                                                         for i in range(4)]
+    enc = limbs_to_ints(np.ctypeslib.as_array(b.c.enc, shape=(16, 2 * b.nl)))
+    assert enc == [abs(m.points_encrypted_vec[i]) for m in msgs for i in range(4)]
+    assert host_outcome(msgs, keys[1]) is None
+
+
 def test_negative_outside_the_rules_still_unsupported(dkr4):
-    """a negative ciphertext is hashed and reduced (c^e mod N^2, the share's
-    decryption): still UnsupportedInput for the batch"""
+    """a negative ring-Pedersen A is hashed and reduced: still UnsupportedInput
+    for the batch"""
     from fsdkr.batch import CollectBatch, UnsupportedInput
     keys, msgs, dks = dkr4
     m2 = copy.deepcopy(msgs)
-    m2[0].points_encrypted_vec[1] = -m2[0].points_encrypted_vec[1]
+    pf = m2[0].ring_pedersen_proof
+    m2[0].ring_pedersen_proof = dataclasses.replace(pf, A=tuple(-a if k == 3 else a for k, a in enumerate(pf.A)))
     with pytest.raises(UnsupportedInput):
         CollectBatch(m2, keys[0], [], 256, KB)
 

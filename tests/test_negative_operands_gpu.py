@@ -16,7 +16,7 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from test_edge_outcomes_gpu import KB, _check, _dkr, _joins_setup  # noqa: E402
-from test_negative_operands import _alice, _pdl, dkr_negative_s3, dkr_negative_z  # noqa: E402
+from test_negative_operands import _alice, _pdl, dkr_negative_c, dkr_negative_s3, dkr_negative_z  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -95,6 +95,27 @@ def test_negative_z(gpu_ctx):
     _check(gpu_ctx, _alice(msgs, 4, 1, z=lambda a: -nt), keys[0], dks[0])
 
 
+def test_negative_ciphertext(gpu_ctx):
+    """c < 0: both proofs hash |c| (zk_pdl_with_slack.rs:117, range_proofs.rs:153),
+    c^e, c^-1 and the share decryption reduce it (:136-142, range_proofs.rs:142,
+    refresh_message.rs:221-234).  Valid proofs over c - N^2 (one sender, the
+    local party's own ciphertext among them) -> Ok with the oracle's LocalKey;
+    a sign-flipped c and c = -N^2 -> the oracle's outcome."""
+    keys, msgs, dks = dkr_negative_c(2, 5, "neg-c-gpu-t2n5", {2})
+    assert all(c < 0 for c in msgs[1].points_encrypted_vec)
+    for r in (0, 1, 4):   # receiver 1 decrypts its own negative ciphertext
+        assert _check(gpu_ctx, msgs, keys[r], dks[r]) is None
+    outs = []
+    for k, i in ((0, 2), (3, 4), (4, 0), (2, 3)):
+        m2 = copy.deepcopy(msgs)
+        m2[k].points_encrypted_vec[i] = -m2[k].points_encrypted_vec[i]
+        outs.append(_check(gpu_ctx, m2, keys[0], dks[0]))
+    assert any(outs), outs
+    m3 = copy.deepcopy(msgs)
+    m3[3].points_encrypted_vec[2] = -keys[0].paillier_key_vec[2].n ** 2
+    _check(gpu_ctx, m3, keys[0], dks[0])
+
+
 def test_negative_alice_operands(gpu_ctx, dkr5):
     keys, msgs, dks, _ = dkr5
     _check(gpu_ctx, _alice(msgs, 1, 2, e=lambda a: -a.e), keys[0], dks[0], expect="panic")
@@ -156,11 +177,18 @@ def test_collect_many_negative_session_alone(gpu_ctx, dkr5):
 
 
 def test_collect_many_negative_z_session(gpu_ctx):
-    """collect_many: a session of valid negative-z proofs (its own batch, z_neg)
+    """collect_many: a session of valid negative-z proofs (its own batch, neg_bits)
     beside regular sessions of the same keys."""
     keys, msgs, dks = dkr_negative_z(2, 5, "neg-z-many", {1})
     m_ok = _pdl(msgs, 0, 0, z=lambda p: p.z)
     _collect_many_like_oracle(gpu_ctx, keys, dks, [(msgs, 0), (m_ok, 3), (msgs, 4)])
+
+
+def test_collect_many_negative_c_session(gpu_ctx):
+    keys, msgs, dks = dkr_negative_c(2, 5, "neg-c-many", {4})
+    m2 = copy.deepcopy(msgs)
+    m2[0].points_encrypted_vec[3] = -m2[0].points_encrypted_vec[3]
+    _collect_many_like_oracle(gpu_ctx, keys, dks, [(msgs, 0), (m2, 1), (msgs, 3)])
 
 
 def test_collect_many_negative_s3_session(gpu_ctx, neg_s3):
