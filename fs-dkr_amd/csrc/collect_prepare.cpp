@@ -516,6 +516,23 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     if (!tz_z) I.rows_at(o_pZ + (size_t)x.mbase * M * zl * 4, x.b->ped_Z, (size_t)x.Mt * M, x.b->zl, zl);
   }
   const size_t o_pS = I.own(PEDS);
+  // negative ring-Pedersen A (ped_a_neg): the rows hold |A| (hashed); the check takes -|A| mod N
+  std::vector<uint32_t> aneg_row((size_t)Mt * M, ~0u), AR;
+  for (const Sess& x : pl.ss)
+    if (x.b->ped_a_neg)
+      for (size_t q = 0; q < (size_t)x.Mt * M; ++q)
+        if (x.b->ped_a_neg[q]) {
+          const size_t lm = q / M;
+          const hbn::Limbs Nm = hbn::from(x.b->ped_N + lm * x.b->nl, x.b->nl);
+          const hbn::Limbs am = hbn::mod(hbn::from(x.b->ped_A + q * x.b->nl, x.b->nl), Nm);
+          aneg_row[(size_t)x.mbase * M + q] = (uint32_t)(AR.size() / nl);
+          AR.resize(AR.size() + nl);
+          hbn::store(am.empty() ? am : hbn::sub(Nm, am), AR.data() + AR.size() - nl, nl);
+        }
+  const size_t o_ar = AR.empty() ? 0 : I.own(AR);
+  auto a_off = [&](size_t q) {   // image offset of A_q's row in the checks (q = m * M + k)
+    return aneg_row[q] == ~0u ? o_pA + q * nl * 4 : o_ar + (size_t)aneg_row[q] * nl * 4;
+  };
   const size_t o_cks = I.reserve((size_t)Mt * CK_M2 * ckl * 4);
   for (const Sess& x : pl.ss)
     I.rows_at(o_cks + (size_t)x.mbase * CK_M2 * ckl * 4, x.b->ck_sigma, (size_t)x.Mt * CK_M2, x.ckl, ckl);
@@ -955,7 +972,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
             : tz_out ? (uint64_t)(uintptr_t)(tz_out + ((size_t)m * M + k) * nl)
                      : DX(x_RP + ((size_t)m * M + k) * nl * 4);
       e.b = DI(o_one);
-      e.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
+      e.c = DI(a_off((size_t)m * M + k));
       e.d = DI(o_pS + (size_t)m * nl * 4);
       e.a_len = e.b_len = e.c_len = e.d_len = nl;
       e.sel = m * MW * 32 + k;
@@ -1041,7 +1058,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       o.a_len = nl;
       o.ea = tz_z ? (uint64_t)(uintptr_t)(tz_z + ((size_t)m * M + k) * zl) : DI(o_pZ + ((size_t)m * M + k) * zl * 4);
       o.ea_len = zl;
-      o.c = DI(o_pA + ((size_t)m * M + k) * nl * 4);
+      o.c = DI(a_off((size_t)m * M + k));
       o.c_len = nl;
       o.d = DI(o_pSraw + (size_t)m * nl * 4);
       o.d_len = nl;

@@ -42,7 +42,7 @@ class CollectBatchC(ctypes.Structure):
                                     "dlog_x1", "dlog_x2", "dlog_y1", "dlog_y2")] + [("n_recv", ctypes.c_uint32)] + \
                [("vss_len", u32p), ("range_lens", u32p), ("ckl", ctypes.c_uint32), ("recv_avail", ctypes.c_uint32),
                 ("ped_lens", u32p), ("ck_lens", u32p), ("pdl_s3_neg", ctypes.POINTER(ctypes.c_uint8)),
-                ("neg_bits", ctypes.POINTER(ctypes.c_uint8))]
+                ("neg_bits", ctypes.POINTER(ctypes.c_uint8)), ("ped_a_neg", ctypes.POINTER(ctypes.c_uint8))]
 
 
 u8p = ctypes.POINTER(ctypes.c_uint8)

@@ -18,9 +18,10 @@ proof runs at its own width before ModuliTooSmall, :376-391), and negative
 BigInts where the reference's outcome for that instance is a panic, an error,
 a plain residue, an h2^-1 exponent or a hashed-and-reduced value (_Negatives:
 PDL s1 / u2 / u3 / s2 / s3 / z, Alice s / s1 / s2 / e / z, the ciphertext c,
-ring-Pedersen Z, DLog y).  Still outside the representable set
-(UnsupportedInput): a negative ring-Pedersen A (hashed and reduced) and values
-wider than 3072 bits in a proof field (6144 bits for ek.n / sigma)."""
+ring-Pedersen A / Z, DLog y).  Still outside the representable set
+(UnsupportedInput): negative statement fields (keys, N~, h1, h2, ring-Pedersen
+S / T / N, ek.n, sigma) and values wider than 3072 bits in a proof field (6144
+bits for ek.n / sigma)."""
 import ctypes
 import math
 import os
@@ -202,7 +203,8 @@ class _Negatives:
       PDL's z (neg_bits bit 1).
     - ring-Pedersen (ring_pedersen_proof.rs:126-157): Z[i] < 0 panics at
       iteration i, after checks 0..i-1 -- exactly the short-Z mechanism
-      (ped_lens: Z "ends" at its first negative entry).
+      (ped_lens: Z "ends" at its first negative entry); A[i] < 0 hashes as
+      |A[i]| and mod_mul reduces it: |A[i]| packed with its ped_a_neg flag.
     - composite DLog (zk-paillier, joins :417-424): y < 0 panics in g^y once the
       N > 2^128 and gcd checks pass (else false); proof 2 runs only if proof 1
       holds."""
@@ -214,6 +216,7 @@ class _Negatives:
         self.dlog = {}     # join -> "y1-panic" | "y1-false" | "y2"
         self.s3 = None     # [pairs] uint8 pdl_s3_neg flags (None: no negative s3)
         self.z = None      # [pairs] uint8 neg_bits flags: bit 0 PDL z, bit 1 Alice z, bit 2 c
+        self.a = None      # [(R+J) * M] uint8 ped_a_neg flags (None: no negative A)
 
     def __bool__(self):
         return bool(self.rows)
@@ -463,12 +466,23 @@ class CollectBatch:
         F["ped_S"] = G.field([m.ring_pedersen_statement for m in all_m], "S")
         rpp = [m.ring_pedersen_proof for m in all_m]
         short = any(len(r.A) < M or len(r.Z) < M for r in rpp)
+        a_rows = short
         if not short:   # the first M of every vector, flattened in C
-            F["ped_A"] = G.rows(rpp, "A", M)
+            try:
+                F["ped_A"] = G.rows(rpp, "A", M)
+            except UnsupportedInput:   # a negative A[i]: |A[i]| with its ped_a_neg flag
+                a_rows = True
             try:
                 F["ped_Z"] = G.rows(rpp, "Z", M)
             except UnsupportedInput:   # a negative Z[i]: Z "ends" there (see _Negatives)
                 short = True
+        if a_rows:   # short A vectors or a negative entry: zero-padded |A| rows
+            A = [list(r.A[:M]) for r in rpp]
+            neg_a = [[1 if isinstance(v, int) and v < 0 else 0 for v in row] + [0] * (M - len(row)) for row in A]
+            if any(map(any, neg_a)):
+                neg.a = np.array(neg_a, dtype=np.uint8).reshape(-1)
+                neg.rows["ped_A"] = [k for k, v in enumerate(neg.a) if v]
+            F["ped_A"] = G.field([abs(v) for row in A for v in row + [0] * (M - len(row))])
         if short:   # short vectors (or a negative Z entry): zero-padded rows
             Z = [list(r.Z[:M]) for r in rpp]
             zlen = [next((i for i, v in enumerate(row) if isinstance(v, int) and v < 0), len(row)) for row in Z]
@@ -476,9 +490,6 @@ class CollectBatch:
                 neg.rows["ped_Z"] = [m for m, (zl, row) in enumerate(zip(zlen, Z)) if zl < len(row)]
                 Z = [row[:zl] for zl, row in zip(zlen, Z)]
             c.ped_lens = k(np.array([[min(len(r.A), M), zl] for r, zl in zip(rpp, zlen)], dtype=np.uint32))
-            if "ped_A" not in F:
-                A = [list(r.A[:M]) for r in rpp]
-                F["ped_A"] = G.field([v for row in A for v in row + [0] * (M - len(row))])
             F["ped_Z"] = G.field([v for row in Z for v in row + [0] * (M - len(row))])
         c.s1l = _limbs_for(max(F["pdl_s1"][1], F["rp_s1"][1], 1))
         c.s3l = _limbs_for(max(F["pdl_s3"][1], F["rp_s2"][1], 1))
@@ -539,7 +550,7 @@ class CollectBatch:
             self._points(st)
         if self.negs:
             self.negs.decide(msgs, joins, n, st["avail"], st["pdl"], st["rng"], st["sts"])
-            for arr, attr in ((self.negs.s3, "pdl_s3_neg"), (self.negs.z, "neg_bits")):
+            for arr, attr in ((self.negs.s3, "pdl_s3_neg"), (self.negs.z, "neg_bits"), (self.negs.a, "ped_a_neg")):
                 if arr is not None:
                     self._keep.append(arr)
                     setattr(c, attr, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))

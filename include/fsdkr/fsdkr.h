@@ -200,7 +200,11 @@ typedef struct fsdkr_collect_batch {
    *             takes the residue -|v| mod N~ (z^e) or mod N^2 (c^e, c^-1), as GMP
    *             reduces a negative base (zk_pdl_with_slack.rs:114-122,136-157;
    *             range_proofs.rs:129-157).  The caller's share decryption reduces its
-   *             own ciphertexts (Paillier::mul / add work mod N^2, :221-234). */
+   *             own ciphertexts (Paillier::mul / add work mod N^2, :221-234).
+   *  ped_a_neg  [R+J][M] nonzero: ring-Pedersen A_k is negative and ped_A holds |A_k|:
+   *             the challenge hashes |A_k|, the check T^Z_k == A_k S^e_k (mod N)
+   *             takes -|A_k| mod N (BigInt::mod_mul reduces it;
+   *             ring_pedersen_proof.rs:130-153). */
   const uint32_t* vss_len;
   const uint32_t* range_lens;
   uint32_t ckl;
@@ -209,6 +213,7 @@ typedef struct fsdkr_collect_batch {
   const uint32_t* ck_lens;
   const uint8_t* pdl_s3_neg;
   const uint8_t* neg_bits;
+  const uint8_t* ped_a_neg;
 } fsdkr_collect_batch;
 
 /* Verdicts (caller-allocated). 1 bits mean "check passed".  cap_* are the

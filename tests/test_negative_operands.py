@@ -330,16 +330,59 @@ def test_negative_c_packed_as_magnitude():
     assert host_outcome(msgs, keys[1]) is None
 
 
+def dkr_negative_a(t, n, seed, senders):
+    """_dkr with the given senders' ring-Pedersen proofs made over A_k - N for
+    every third k (the same residues, negative): the challenge hashes |A_k|, the
+    check's mod_mul reduces A_k, so the proofs stay valid."""
+    from oracle import bigint, ring_pedersen
+    rng = Rng(seed)
+    keys = protocol.simulate_keygen(t, n, rng, KB)
+    msgs, dks = [], []
+    orig = ring_pedersen.prove
+
+    def prove(wit, st, M, g):   # ring_pedersen.prove with the shifted commitments
+        a = [g.sample_below(st.phi) for _ in range(M)]
+        A = [bigint.mod_pow(st.T, ai, st.N) - (st.N if k % 3 == 0 else 0) for k, ai in enumerate(a)]
+        bits = ring_pedersen.challenge_bits(A, M)
+        Z = [bigint.mod_add(a[i], bits[i] * wit.lam, st.phi) for i in range(M)]
+        return ring_pedersen.RingPedersenProof(tuple(A), tuple(Z))
+    for key in keys:
+        if key.i in senders:
+            ring_pedersen.prove = prove
+        try:
+            m, dk = protocol.distribute(key.i, key, n, rng, KB)
+        finally:
+            ring_pedersen.prove = orig
+        msgs.append(m)
+        dks.append(dk)
+    return keys, msgs, dks
+
+
+def test_negative_ring_pedersen_a_packed():
+    """negative A_k: |A_k| packed (the challenge hashes it) with ped_a_neg flags"""
+    from fsdkr.batch import CollectBatch
+    from fsdkr._native import limbs_to_ints
+    keys, msgs, dks = dkr_negative_a(1, 4, "neg-a-t1n4", {4})
+    assert oracle_outcome(msgs, keys[0], dks[0]) is None
+    b = CollectBatch(msgs, keys[0], [], 256, KB)
+    flags = np.ctypeslib.as_array(b.c.ped_a_neg, shape=(4, 256))
+    assert flags.tolist() == [[0] * 256] * 3 + [[1 if k % 3 == 0 else 0 for k in range(256)]]
+    A = limbs_to_ints(np.ctypeslib.as_array(b.c.ped_A, shape=(4 * 256, b.nl)))
+    assert A == [abs(a) for m in msgs for a in m.ring_pedersen_proof.A]
+    assert host_outcome(msgs, keys[0]) is None
+
+
 def test_negative_outside_the_rules_still_unsupported(dkr4):
-    """a negative ring-Pedersen A is hashed and reduced: still UnsupportedInput
-    for the batch"""
+    """a negative statement field (here the receiver's N~) is outside the
+    representable set: UnsupportedInput for the batch"""
     from fsdkr.batch import CollectBatch, UnsupportedInput
     keys, msgs, dks = dkr4
-    m2 = copy.deepcopy(msgs)
-    pf = m2[0].ring_pedersen_proof
-    m2[0].ring_pedersen_proof = dataclasses.replace(pf, A=tuple(-a if k == 3 else a for k, a in enumerate(pf.A)))
+    m2 = msgs
+    key = keys[0].clone()
+    st = key.h1_h2_n_tilde_vec[1]
+    key.h1_h2_n_tilde_vec[1] = dataclasses.replace(st, N=-st.N)
     with pytest.raises(UnsupportedInput):
-        CollectBatch(m2, keys[0], [], 256, KB)
+        CollectBatch(m2, key, [], 256, KB)
 
 
 def test_session_set_moves_negative_sessions_out(dkr4):

@@ -16,7 +16,8 @@ import pytest
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from test_edge_outcomes_gpu import KB, _check, _dkr, _joins_setup  # noqa: E402
-from test_negative_operands import _alice, _pdl, dkr_negative_c, dkr_negative_s3, dkr_negative_z  # noqa: E402
+from test_negative_operands import (_alice, _pdl, dkr_negative_a, dkr_negative_c, dkr_negative_s3,  # noqa: E402
+                                    dkr_negative_z)
 
 pytestmark = pytest.mark.gpu
 
@@ -114,6 +115,25 @@ def test_negative_ciphertext(gpu_ctx):
     m3 = copy.deepcopy(msgs)
     m3[3].points_encrypted_vec[2] = -keys[0].paillier_key_vec[2].n ** 2
     _check(gpu_ctx, m3, keys[0], dks[0])
+
+
+def test_negative_ring_pedersen_a(gpu_ctx):
+    """A_k < 0: the challenge hashes |A_k|, mod_mul reduces it (ring_pedersen_proof.rs:
+    130-153).  Valid proofs over A_k - N (one sender) -> Ok with the oracle's
+    LocalKey; a sign-flipped A_k (the same challenge, the check against -A_k)
+    -> the oracle's RingPedersenProofError; both beside a negative Z (panic)."""
+    keys, msgs, dks = dkr_negative_a(2, 5, "neg-a-gpu-t2n5", {5})
+    assert sum(a < 0 for a in msgs[4].ring_pedersen_proof.A) == 86
+    for r in (0, 3):
+        assert _check(gpu_ctx, msgs, keys[r], dks[r]) is None
+    m2 = copy.deepcopy(msgs)
+    pf = m2[1].ring_pedersen_proof
+    m2[1].ring_pedersen_proof = dataclasses.replace(pf, A=tuple(-a if k == 17 else a for k, a in enumerate(pf.A)))
+    _check(gpu_ctx, m2, keys[0], dks[0], expect="RingPedersenProofError")
+    m3 = copy.deepcopy(msgs)
+    pf = m3[4].ring_pedersen_proof
+    m3[4].ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(-z if k == 200 else z for k, z in enumerate(pf.Z)))
+    _check(gpu_ctx, m3, keys[0], dks[0], expect="panic")
 
 
 def test_negative_alice_operands(gpu_ctx, dkr5):
