@@ -18,7 +18,7 @@ proof runs at its own width before ModuliTooSmall, :376-391), and negative
 BigInts where the reference's outcome for that instance is a panic, an error,
 a plain residue, an h2^-1 exponent or a hashed-and-reduced value (_Negatives:
 PDL s1 / u2 / u3 / s2 / s3 / z, Alice s / s1 / s2 / e / z, the ciphertext c,
-ring-Pedersen A / Z, DLog y).  Still outside the representable set
+ring-Pedersen A / Z, DLog x / y).  Still outside the representable set
 (UnsupportedInput): negative statement fields (keys, N~, h1, h2, ring-Pedersen
 S / T / N, ek.n, sigma) and values wider than 3072 bits in a proof field (6144
 bits for ek.n / sigma)."""
@@ -207,13 +207,15 @@ class _Negatives:
       |A[i]| and mod_mul reduces it: |A[i]| packed with its ped_a_neg flag.
     - composite DLog (zk-paillier, joins :417-424): y < 0 panics in g^y once the
       N > 2^128 and gcd checks pass (else false); proof 2 runs only if proof 1
-      holds."""
+      holds; x < 0 (hashed as |x|) never equals mod_mul(g^y, ni^e) >= 0: that
+      proof is false unless its y panics first."""
 
     def __init__(self):
         self.rows = {}     # field -> rows packed with a stand-in
         self.pdl = {}      # pair -> (or-bits, and-mask)
         self.range = {}    # pair -> verdict (0 false, 2 panic)
         self.dlog = {}     # join -> "y1-panic" | "y1-false" | "y2"
+        self.dlogx = {}    # join -> DLog verdict bits a negative x clears (1: proof 1, 2: proof 2)
         self.s3 = None     # [pairs] uint8 pdl_s3_neg flags (None: no negative s3)
         self.z = None      # [pairs] uint8 neg_bits flags: bit 0 PDL z, bit 1 Alice z, bit 2 c
         self.a = None      # [(R+J) * M] uint8 ped_a_neg flags (None: no negative A)
@@ -269,6 +271,9 @@ class _Negatives:
                 self.range[p] = 0
             else:                   # s1 or s2 < 0
                 self.range[p] = 2
+        for name, bit in (("dlog_x1", 1), ("dlog_x2", 2)):   # x < 0 never equals mod_mul(..) >= 0
+            for j in self.rows.get(name, ()):
+                self.dlogx[j] = self.dlogx.get(j, 0) | bit
         for j in sorted(set(self.rows.get("dlog_y1", ())) | set(self.rows.get("dlog_y2", ()))):
             st = joins[j].dlog_statement
             if joins[j].composite_dlog_proof_base_h1.y < 0:
@@ -283,6 +288,8 @@ class _Negatives:
             pdl[p] = (pdl[p] & a) | o
         for p, v in self.range.items():
             rng[p] = v
+        for j, bits in self.dlogx.items():   # before the y rules: g^y's panic comes first
+            dlog[j] &= ~bits & 0xFF
         for j, rule in self.dlog.items():
             if rule == "y1-panic" or (rule == "y2" and dlog[j] & 1):
                 dlog[j] = 4
@@ -577,8 +584,7 @@ class CollectBatch:
                 F["dlog_" + name] = G.field([j.dlog_statement for j in st["joins"]], attr)
             for name, which, attr in (("x1", 1, "x"), ("x2", 2, "x"), ("y1", 1, "y"), ("y2", 2, "y")):
                 pf = [getattr(j, f"composite_dlog_proof_base_h{which}") for j in st["joins"]]
-                F["dlog_" + name] = neg.field(G, "dlog_" + name, pf, attr, _zero) if attr == "y" else \
-                    G.field(pf, attr)
+                F["dlog_" + name] = neg.field(G, "dlog_" + name, pf, attr, _zero)
 
     def _points(self, st):
         """secp256k1 points: the shares' commitments Q, PDL u1 and the VSS commitments"""

@@ -154,6 +154,21 @@ def test_negative_bases_packed_as_residues(dkr4):
     assert host_outcome(m2, key) is None
 
 
+@pytest.mark.parametrize("case", ["x1", "x2", "x1_y1", "x2_y2", "x1_y2"])
+def test_negative_dlog_commitment(joined, case):
+    """x < 0: that proof is false (mod_mul(g^y, ni^e) >= 0), unless its y < 0
+    panics first in g^y; proof 2 only after proof 1"""
+    keys, msgs, dks, jm = joined
+    j2 = copy.deepcopy(jm)
+    for part in case.split("_"):
+        attr = "composite_dlog_proof_base_h1" if part[1] == "1" else "composite_dlog_proof_base_h2"
+        p = getattr(j2, attr)
+        setattr(j2, attr, dataclasses.replace(p, **{part[0]: -getattr(p, part[0])}))
+    want = oracle_outcome(msgs, keys[1], dks[1], [j2])
+    assert want is not None
+    assert host_outcome(msgs, keys[1], [j2]) == want
+
+
 @pytest.mark.parametrize("which", ["y1", "y2"])
 def test_negative_dlog_response(joined, which):
     keys, msgs, dks, jm = joined

@@ -173,6 +173,17 @@ def test_negative_ring_pedersen_z(gpu_ctx, dkr5):
     _check(gpu_ctx, m3, keys[0], dks[0], expect="RingPedersenProofError")
 
 
+@pytest.mark.parametrize("case", ["x1", "x2", "x1_y1", "x2_y2", "x1_y2"])
+def test_negative_dlog_commitment(gpu_ctx, case):
+    keys, msgs, dks, jm, _ = _joins_setup("neg-dlog-x")
+    j2 = copy.deepcopy(jm)
+    for part in case.split("_"):
+        attr = "composite_dlog_proof_base_h1" if part[1] == "1" else "composite_dlog_proof_base_h2"
+        p = getattr(j2, attr)
+        setattr(j2, attr, dataclasses.replace(p, **{part[0]: -getattr(p, part[0])}))
+    assert _check(gpu_ctx, msgs, keys[1], dks[1], [j2]) is not None
+
+
 @pytest.mark.parametrize("which", ["y1", "y2"])
 def test_negative_dlog_response(gpu_ctx, which):
     keys, msgs, dks, jm, _ = _joins_setup("neg-dlog")
