@@ -57,6 +57,44 @@ def kernel_issued(kd, g, ebits):
     return ((1 << w) - 1 + (nwin - 1) + 1) * mul + (nwin - 1) * w * sqr
 
 
+def slide_window(ebits):
+    """capi.cpp choose_slide_window: 2^(w-1) odd powers + ebits/(w+1) products, fewest."""
+    return min(range(1, 8), key=lambda w: (1 << (w - 1)) + ebits / (w + 1))
+
+
+def slide_products(e, w):
+    """(squarings, multiplies) modexp_slide_kernel runs for exponent e: the odd-power
+    table (x*R^2, x^2, 2^(w-1) - 1 products), the window scan from the top bit (the
+    first window is a table load) and the exit product."""
+    bits = bin(e)[2:][::-1]
+    bit = lambda i: bits[i] == "1"
+    sq, mul = 1, 1 + (1 << (w - 1)) - 1 + 1
+    i = len(bits) - 1
+    j = max(i - w + 1, 0)
+    while not bit(j):
+        j += 1
+    i = j - 1
+    while i >= 0:
+        if not bit(i):
+            sq, i = sq + 1, i - 1
+            continue
+        j = max(i - w + 1, 0)
+        while not bit(j):
+            j += 1
+        sq, mul, i = sq + i - j + 1, mul + 1, j - 1
+    return sq, mul
+
+
+def slide_issued(kd, g, exps):
+    """kernel_issued for modexp_slide_kernel, averaged over the launch's exponents."""
+    w = slide_window(max(e.bit_length() for e in exps))
+    L = kd // g
+    mul = kd * g * 2 * L
+    sqr = kd * g * ((L + 1) // 2 if L % 2 else L // 2 + 1) + kd * g * L
+    tot = [slide_products(e, w) for e in exps]
+    return sum(q * sqr + m * mul for q, m in tot) / len(tot)
+
+
 def proofs_of(R, J, n):
     return 2 * R * n + (R + J) + (R + J) + 2 * J
 
@@ -247,8 +285,11 @@ def keygen_bench(ctx, count=64, bits=2048, seed=77):
             "what": "keypairs + correct-key proofs per batched call; single = one keypair (distribute path)"}
 
 
-def modexp_roofline(ctx, count, reps, seed=1234):
-    """The dominant kernel on the metric-2 shape: base^N mod N^2, N 2048-bit."""
+def modexp_roofline(ctx, count, reps, seed=1234, keyed=True):
+    """The dominant kernel on the metric-2 shape: base^N mod N^2, N 2048-bit.
+    keyed: fsdkr_modexp_keyed_device (exponent N per key, waves regrouped by key,
+    sliding windows: modexp_slide_kernel); else fsdkr_modexp_batch_device with a
+    per-instance exponent row (fixed windows: modexp_kernel)."""
     import random
     import torch
     from fsdkr._native import ints_to_limbs
@@ -260,7 +301,7 @@ def modexp_roofline(ctx, count, reps, seed=1234):
     rng = np.random.default_rng(seed)
     base = rng.integers(0, 2 ** 32, size=(count, 128), dtype=np.uint64).astype(np.uint32)
     base[:, -1] >>= 1
-    E = ints_to_limbs([Ns[i] for i in idx], 64)
+    E = ints_to_limbs(Ns if keyed else [Ns[i] for i in idx], 64)
     Mo = ints_to_limbs(mods, 128)
     dev = torch.device("cuda", torch.cuda.current_device())
     d_b = torch.from_numpy(base.view(np.int32)).to(dev)
@@ -271,9 +312,11 @@ def modexp_roofline(ctx, count, reps, seed=1234):
     torch.cuda.synchronize()
     L = ctx._lib
 
+    fn = L.fsdkr_modexp_keyed_device if keyed else L.fsdkr_modexp_batch_device
+
     def once():
-        ctx.check(L.fsdkr_modexp_batch_device(ctx.handle, 128, count, d_b.data_ptr(), d_e.data_ptr(), 64, 2048,
-                                              d_i.data_ptr(), d_m.data_ptr(), nmod, d_o.data_ptr()))
+        ctx.check(fn(ctx.handle, 128, count, d_b.data_ptr(), d_e.data_ptr(), 64, 2048, d_i.data_ptr(), d_m.data_ptr(),
+                     nmod, d_o.data_ptr()))
     once()
     ctx.set_timing(True)
     ctx.kernel_time_reset()
@@ -289,19 +332,21 @@ def modexp_roofline(ctx, count, reps, seed=1234):
         b = int.from_bytes(base[i].tobytes(), "little")
         assert int.from_bytes(out[i].tobytes(), "little") == pow(b, Ns[idx[i]], mods[idx[i]]), "modexp parity"
     W = count * w_modexp(128, 2048)
-    g = 4 if count * 4 > 256 * 4 * 3 * 64 else 8   # modexp.hip pick_group for 128 limbs
+    cap = 256 * 4 * 3 * 64   # modexp.hip pick_group / capi.cpp run_modexp_keyed for 128 limbs
+    g = 16 if count * 16 <= cap else 8 if count * 8 <= cap else 4
+    issued = slide_issued(144, g, Ns) if keyed else kernel_issued(144, g, 2048)
     return {"count": count, "kernel_ms": ms, "wall_ms": wall * 1e3, "modexp_per_s": count / (ms * 1e-3),
-            "achieved_mac_per_s": W / (ms * 1e-3), "group": g,
-            "issued_mac_per_s": count * kernel_issued(144, g, 2048) / (ms * 1e-3)}
+            "achieved_mac_per_s": W / (ms * 1e-3), "group": g, "keyed": keyed,
+            "issued_mac_per_s": count * issued / (ms * 1e-3)}
 
 
-def pmc_traffic(count):
+def pmc_traffic(count, pattern="r*_pmc_modexp4096_keyed.json"):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3
     --pmc passes (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 per the
     gfx950 correction + WRITE_SIZE, one pass each), scaled to `count`
     instances.  PMC cannot be collected inside the timed run."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_modexp4096.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", pattern), recursive=True))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -588,6 +633,7 @@ def main():
     ctx.set_cu_split(0)   # a shard slice may have split the CUs; the single-GPU figures below use the whole chip
     batch, verd, ph = phases(ctx, msgs, lk, joins, a.key_bits)
     roof = modexp_roofline(ctx, a.modexp_count, 3)
+    roof_rows = modexp_roofline(ctx, a.modexp_count, 3, keyed=False)
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         try:
@@ -615,11 +661,15 @@ def main():
         "phases_ms": ph,
         "device_pipeline_proofs_per_s": proofs / (ph["device_pipeline_ms"] * 1e-3),
         "modexp_4096_per_s": roof["modexp_per_s"],
+        "modexp_4096_per_s_exponent_rows": {
+            "value": roof_rows["modexp_per_s"], "kernel_ms": roof_rows["kernel_ms"], "lanes": roof_rows["group"],
+            "what": "fsdkr_modexp_batch_device: a per-instance exponent row, fixed 5-bit windows (modexp_kernel)"},
         "roofline": {"bound": "valu-int", "achieved": roof["achieved_mac_per_s"] / 1e12, "peak": PEAK_MAC / 1e12,
                      "unit": "T u32-MAC/s", "frac": roof["achieved_mac_per_s"] / PEAK_MAC, "traffic": traffic,
                      "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
                      "algorithmic_bytes": roof["count"] * (512 + 256 + 512),
-                     "kernel": "modexp_kernel (4096-bit modulus N^2, 2048-bit exponent N)",
+                     "kernel": "modexp_slide_kernel (4096-bit modulus N^2, 2048-bit exponent N shared per key: "
+                               "fsdkr_modexp_keyed_device, 16 keys x 4096 instances, sliding windows w = 7)",
                      "per_launch": f"{roof['count']} instances x {w_modexp(128, 2048) / 1e6:.2f} M MACs in "
                                    f"{roof['kernel_ms']:.2f} ms (HIP events)",
                      "accounting": "achieved = SURVEY §8d MACs (32-bit limbs, 2k^2+k per modmul); issued = the "

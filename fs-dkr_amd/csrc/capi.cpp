@@ -414,7 +414,7 @@ void ModexpJob::pack(std::vector<uint8_t>& dst) const {
 
 // Upload a modexp descriptor set and launch it against prepared constants.
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
-                      uint32_t group) {
+                      uint32_t group, uint32_t desc_flags) {
   const uint32_t count = (uint32_t)job.size();
   if (count == 0) return FSDKR_OK;
   std::string dname = std::string("mxdesc_") + tag;
@@ -432,7 +432,7 @@ int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, ui
   rc = c->hip_check(hipStreamSynchronize(c->stream), "sync desc");
   if (rc) return rc;
   return launch_modexp_desc(c, job.k32, count, job.exp_bits, d_desc, d_consts, d_out, nullptr, "mxtable", c->prio,
-                            group);
+                            group, desc_flags);
 }
 
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
@@ -484,6 +484,44 @@ int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_ba
   rc = c->hip_check(hipStreamSynchronize(c->stream), "sync");
   if (rc) return rc;
   return launch_modexp_job(c, job, d_consts, d_out, "generic", wide);
+}
+
+// Exponent per modulus (key): d_exp is [n_mod][exp_limbs].  The instances are
+// regrouped by key so the instances of every wave share their exponent (runs
+// padded to whole waves with copies that rewrite their own row), which lets the
+// 4096-bit shapes run sliding windows (modexp_slide_kernel: 2048-bit exponent at
+// w = 6, ~2042 squarings + ~300 products against 2043 + 440 with fixed 5-bit
+// windows).  Other widths, or a constant-time context, keep fixed windows.
+int run_modexp_keyed(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
+                     uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,
+                     uint32_t n_mod, uint32_t* d_out) {
+  if (count == 0) return FSDKR_OK;
+  uint32_t* d_consts = nullptr;
+  int rc = setup_moduli(c, k32, d_mods, n_mod, &d_consts, "keyed", 0);
+  if (rc) return rc;
+  std::vector<uint32_t> idx(count);
+  rc = c->hip_check(hipMemcpyAsync(idx.data(), d_mod_idx, sizeof(uint32_t) * count, hipMemcpyDeviceToHost, c->stream),
+                    "D2H mod_idx");
+  if (rc) return rc;
+  if ((rc = c->hip_check(hipStreamSynchronize(c->stream), "sync"))) return rc;
+  ModexpJob job;
+  job.k32 = k32;
+  for (uint32_t i = 0; i < count; ++i) {
+    if (idx[i] >= n_mod) {
+      c->fail("fsdkr_modexp_keyed_device: mod_idx[%u] = %u out of range (%u moduli)", i, idx[i], n_mod);
+      return FSDKR_E_ARG;
+    }
+    job.add((uint64_t)(uintptr_t)(d_base + (size_t)i * k32), k32, (uint64_t)(uintptr_t)(d_exp + (size_t)idx[i] * exp_limbs),
+            exp_limbs, exp_bits, idx[i]);
+  }
+  job.exp_bits = exp_bits;
+  // lanes per instance as the generic 4096-bit launch picks them (modexp.hip
+  // pick_group): the widest shape whose lanes fit the resident-wave capacity
+  constexpr uint64_t kLaneCapacity = 256ull * 4 * 3 * 64;
+  const uint32_t G = (uint64_t)count * 16 <= kLaneCapacity ? 16u : (uint64_t)count * 8 <= kLaneCapacity ? 8u : 4u;
+  uint32_t flags = 0;   // the regrouped job carries out_idx (the caller's rows)
+  if (k32 == 128 && !c->ct && group_by_exponent(job, 64 / G, kPadSelf)) flags = kDescOutIdx | kDescSlide;
+  return launch_modexp_job(c, job, d_consts, d_out, "keyed", (flags & kDescSlide) ? G : 0u, flags);
 }
 
 }  // namespace fsdkr
@@ -777,6 +815,22 @@ int fsdkr_modexp_batch_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count
     return FSDKR_E_ARG;
   }
   int rc = run_modexp_device(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_mod_idx, d_mods, n_mod, d_out);
+  if (rc) return rc;
+  return c->sync();
+}
+
+int fsdkr_modexp_keyed_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* d_base,
+                              const uint32_t* d_exp, uint32_t exp_limbs, uint32_t exp_bits,
+                              const uint32_t* d_mod_idx, const uint32_t* d_mods, uint32_t n_mod, uint32_t* d_out) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!d_base || !d_exp || !d_mod_idx || !d_mods || !d_out || n_mod == 0 || exp_limbs == 0 ||
+      exp_bits > 32u * exp_limbs) {
+    c->fail("fsdkr_modexp_keyed_device: bad argument");
+    return FSDKR_E_ARG;
+  }
+  int rc = run_modexp_keyed(c, mod_limbs, count, d_base, d_exp, exp_limbs, exp_bits, d_mod_idx, d_mods, n_mod, d_out);
   if (rc) return rc;
   return c->sync();
 }

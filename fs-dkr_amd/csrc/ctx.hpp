@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -178,6 +179,62 @@ uint32_t choose_window(uint32_t ebits);
 // the instances of every wave share their exponent (sliding windows)
 constexpr uint32_t kDescOutIdx = 1, kDescSlide = 2;
 
+// J1 (s2^N_i | s^N_i mod N_i^2) regrouped so the instances of every wave share
+// their exponent N_i: stable order by exponent address (receiver), out_idx = the
+// original row.  With a scratch output row (pad_row != kNoPad) every run of one
+// exponent is padded to whole waves of `per_wave` instances with copies of its
+// last chain writing pad_row (at most per_wave - 1 per receiver); returns whether
+// every wave is then uniform (the launch may use sliding windows: kDescSlide).
+// pad_row == kPadSelf: a pad copy writes its chain's own row (the same value
+// twice, no scratch row needed)
+constexpr uint32_t kNoPad = 0xffffffffu, kPadSelf = 0xfffffffeu;
+inline bool group_by_exponent(ModexpJob& J, uint32_t per_wave, uint32_t pad_row) {
+  const size_t cnt = J.size();
+  // stable order by exponent address: a counting sort over the few distinct
+  // addresses (a comparison sort of 131k instances cost ~10 ms at n = 256)
+  std::vector<uint64_t> keys(J.exp_ptr);
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  std::vector<uint32_t> kid(cnt), start(keys.size() + 1, 0), ord(cnt);
+  for (size_t k = 0; k < cnt; ++k) {
+    kid[k] = (uint32_t)(std::lower_bound(keys.begin(), keys.end(), J.exp_ptr[k]) - keys.begin());
+    ++start[kid[k] + 1];
+  }
+  for (size_t q = 1; q < start.size(); ++q) start[q] += start[q - 1];
+  for (size_t k = 0; k < cnt; ++k) ord[start[kid[k]]++] = (uint32_t)k;
+  auto same = [&](uint32_t x, uint32_t y) {
+    return J.exp_ptr[x] == J.exp_ptr[y] && J.exp_len[x] == J.exp_len[y] && J.ebits[x] == J.ebits[y];
+  };
+  bool aligned = per_wave > 0;
+  for (size_t s = 0; s < cnt && aligned && pad_row == kNoPad;) {   // unpadded: every run whole waves
+    size_t e = s;
+    while (e < cnt && same(ord[e], ord[s])) ++e;
+    aligned = (e - s) % per_wave == 0;
+    s = e;
+  }
+  ModexpJob G;
+  G.k32 = J.k32;
+  for (auto* v : {&G.base_len, &G.exp_len, &G.mod_idx, &G.ebits, &G.out_idx}) v->reserve(cnt + cnt / 8);
+  G.base_ptr.reserve(cnt + cnt / 8);
+  G.exp_ptr.reserve(cnt + cnt / 8);
+  auto put = [&](uint32_t k, uint32_t row) {
+    G.add(J.base_ptr[k], J.base_len[k], J.exp_ptr[k], J.exp_len[k], J.ebits[k], J.mod_idx[k]);
+    if (G.out_idx.size() == G.size()) G.out_idx.back() = row;   // add() extended a non-empty out_idx
+    else G.out_idx.push_back(row);
+  };
+  for (size_t s = 0; s < cnt;) {
+    size_t e = s;
+    while (e < cnt && same(ord[e], ord[s])) ++e;
+    for (size_t q = s; q < e; ++q) put(ord[q], J.out_idx.empty() ? ord[q] : J.out_idx[ord[q]]);
+    if (aligned && pad_row != kNoPad)
+      for (size_t q = e - s; q % per_wave; ++q)
+        put(ord[e - 1], pad_row != kPadSelf ? pad_row : J.out_idx.empty() ? ord[e - 1] : J.out_idx[ord[e - 1]]);
+    s = e;
+  }
+  G.exp_bits = J.exp_bits;
+  J = std::move(G);
+  return aligned;
+}
 // RingPedersenProof::verify outcome from the per-index equalities and the
 // challenge-length word of ped_hash (ring_pedersen_proof.rs:136-153): checks run
 // in index order, so a failing check before the BitVec index panic is an error,
@@ -192,7 +249,7 @@ void free_collect_plan(Ctx* c);
 void free_recover(Ctx* c);
 void free_ga_pre(Ctx* c);
 int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, uint32_t* d_out, const char* tag,
-                      uint32_t group = 0);
+                      uint32_t group = 0, uint32_t desc_flags = 0);
 // A split sliding-window launch (ModexpArgs lo_bit / tail, modexp.hip): the head
 // runs the exponent bits >= lo_bit, the tail (same descriptors, group and
 // table_tag) the rest, jointly with base2^exp2 when d_desc2 (per instance:

@@ -130,6 +130,8 @@ def lib():
     L.fsdkr_modexp_batch_device.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
                                             ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp]
     L.fsdkr_modexp_batch_device.restype = ctypes.c_int
+    L.fsdkr_modexp_keyed_device.argtypes = L.fsdkr_modexp_batch_device.argtypes
+    L.fsdkr_modexp_keyed_device.restype = ctypes.c_int
     L.fsdkr_kernel_time.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_uint32)]
     L.fsdkr_kernel_time.restype = ctypes.c_int

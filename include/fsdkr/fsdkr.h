@@ -109,6 +109,18 @@ int fsdkr_modexp_batch_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count
                               const uint32_t* d_mod_idx, const uint32_t* d_mods, uint32_t n_mod,
                               uint32_t* d_out);
 
+/* fsdkr_modexp_batch_device with ONE exponent per modulus (key): d_exp is
+ * [n_mod][exp_limbs], instance i computes d_base[i]^d_exp[mod_idx[i]] mod
+ * d_mods[mod_idx[i]] -- the r^N mod N^2 of Paillier encryption under key N
+ * (paillier EncryptWithChosenRandomness behind the reference's
+ * Paillier::encrypt_with_chosen_randomness calls, refresh_message.rs:75-81).
+ * The instances are regrouped by key so each wave shares its exponent and the
+ * 4096-bit launch runs sliding windows; results land in the caller's order. */
+int fsdkr_modexp_keyed_device(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const uint32_t* d_base,
+                              const uint32_t* d_exp, uint32_t exp_limbs, uint32_t exp_bits,
+                              const uint32_t* d_mod_idx, const uint32_t* d_mods, uint32_t n_mod,
+                              uint32_t* d_out);
+
 /* ---- Key generation: batched Miller–Rabin -------------------
  * verdict[i] = 1 iff cand[i] is a strong probable prime to base bases[i]:
  * with cand - 1 = d 2^s, b^d == 1 or b^(d 2^j) == cand - 1 for some j < s

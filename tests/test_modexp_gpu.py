@@ -152,3 +152,78 @@ def test_modexp_joint_split_chains(gpu_ctx, group):
     want = [pow(b, exps[i], mods[i]) * pow(y, f, mods[i]) % mods[i] for b, y, f, i in zip(bases, bases2, e2, idx)]
     bad = [k for k in range(count) if got[k] != want[k]]
     assert not bad, f"G={group}: {len(bad)} mismatches, first at {bad[0]}"
+
+
+def _keyed(ctx, bases, exps, mods, idx, limbs, exp_limbs):
+    """fsdkr_modexp_keyed_device on device-resident operands (exps: one per modulus),
+    staged through the HIP runtime libfsdkr already loaded (hipMalloc / hipMemcpy)."""
+    import ctypes
+    import numpy as np
+    from fsdkr._native import ints_to_limbs, limbs_to_ints
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    held = []
+
+    def put(a):
+        a = np.ascontiguousarray(a, dtype=np.uint32)
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), max(a.nbytes, 4)) == 0
+        held.append(p)
+        assert hip.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0   # hipMemcpyHostToDevice
+        return p.value
+
+    try:
+        out = np.full((len(bases), limbs), 0xffffffff, dtype=np.uint32)
+        d_o = put(out)
+        ebits = max(1, max(e.bit_length() for e in exps))
+        ctx.check(ctx._lib.fsdkr_modexp_keyed_device(ctx.handle, limbs, len(bases), put(ints_to_limbs(bases, limbs)),
+                                                     put(ints_to_limbs(exps, exp_limbs)), exp_limbs, ebits,
+                                                     put(np.asarray(idx, dtype=np.uint32)),
+                                                     put(ints_to_limbs(mods, limbs)), len(mods), d_o))
+        assert hip.hipMemcpy(out.ctypes.data, d_o, out.nbytes, 2) == 0   # hipMemcpyDeviceToHost
+        return limbs_to_ints(out)
+    finally:
+        for p in held:
+            hip.hipFree(p)
+
+
+@pytest.mark.parametrize("count", [150, 3000, 30000])
+def test_modexp_keyed_sliding_windows(gpu_ctx, count):
+    """One exponent per modulus (fsdkr_modexp_keyed_device, the r^N mod N^2 shape of
+    Paillier encryption): instances regrouped by key into waves that share their
+    exponent, ragged runs padded with copies that rewrite their own row, sliding
+    windows.  Counts cover the 16-, 8- and 4-lane launches; shuffled key order, a key
+    with one instance, an exponent of 0 and one of 1, bases above N^2."""
+    rnd = random.Random(5150 + count)
+    Ns = [_odd(rnd, 2048) for _ in range(5)]
+    mods = [n * n for n in Ns] + [_odd(rnd, 4096), _odd(rnd, 4001)]
+    exps = Ns + [0, 1]
+    idx = [rnd.choice([0, 0, 1, 2, 3, 5, 6]) for _ in range(count)]
+    idx[rnd.randrange(count)] = 4                    # the only instance of key 4
+    bases = [rnd.getrandbits(4096) for _ in range(count)]
+    got = _keyed(gpu_ctx, bases, exps, mods, idx, 128, 64)
+    # Python's pow takes ~0.1 s per 4096-bit chain: a sample of the full chains,
+    # the single-instance key, and every exponent-0 / exponent-1 instance
+    check = sorted(set(rnd.sample(range(count), 30)) | {idx.index(4)} | {k for k in range(count) if idx[k] >= 5})
+    bad = [k for k in check if got[k] != pow(bases[k], exps[idx[k]], mods[idx[k]])]
+    assert not bad, f"{len(bad)} mismatches, first at {bad[0]}"
+
+
+@pytest.mark.parametrize("limbs", [64, 192])
+def test_modexp_keyed_other_widths(gpu_ctx, limbs):
+    """Widths without a sliding-window shape keep fixed windows (per-instance exponent
+    pointers into the per-key rows); out-of-range key indices are refused."""
+    from fsdkr._native import FsdkrError
+    rnd = random.Random(limbs)
+    bits = 32 * limbs
+    mods = [_odd(rnd, bits) for _ in range(3)]
+    exps = [rnd.getrandbits(bits) for _ in range(3)]
+    idx = [rnd.randrange(3) for _ in range(100)]
+    bases = [rnd.getrandbits(bits) for _ in range(100)]
+    got = _keyed(gpu_ctx, bases, exps, mods, idx, limbs, limbs)
+    assert got == [pow(b, exps[i], mods[i]) for b, i in zip(bases, idx)]
+    idx[7] = 3
+    with pytest.raises(FsdkrError):
+        _keyed(gpu_ctx, bases, exps, mods, idx, limbs, limbs)

@@ -21,7 +21,7 @@ def mmacs(k32, ebits):
     return (ebits + (ebits + 4) // 5) * (2 * k32 * k32 + k32)
 
 
-def run(ctx, k32, count, nmod, reps, seed):
+def run(ctx, k32, count, nmod, reps, seed, keyed=False):
     rng = np.random.default_rng(seed)
     import random
     rnd = random.Random(seed)
@@ -38,7 +38,8 @@ def run(ctx, k32, count, nmod, reps, seed):
     idx = (np.arange(count) % nmod).astype(np.uint32)
     base = rng.integers(0, 2**32, size=(count, k32), dtype=np.uint64).astype(np.uint32)
     base[:, -1] >>= 1  # < 2^(32k-1) <= N^2 for top-bit-set moduli (uniform below that bound)
-    E = ints_to_limbs([exps_int[i] for i in idx], (ebits_nominal + 31) // 32)
+    # keyed: one exponent row per modulus (fsdkr_modexp_keyed_device, sliding windows)
+    E = ints_to_limbs(exps_int if keyed else [exps_int[i] for i in idx], (ebits_nominal + 31) // 32)
     M = ints_to_limbs(mods, k32)
     dev = torch.device("cuda")
     d_base = torch.from_numpy(base.view(np.int32)).to(dev)
@@ -48,9 +49,10 @@ def run(ctx, k32, count, nmod, reps, seed):
     d_out = torch.empty((count, k32), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     L = ctx._lib
+    fn = L.fsdkr_modexp_keyed_device if keyed else L.fsdkr_modexp_batch_device
 
     def once():
-        ctx.check(L.fsdkr_modexp_batch_device(ctx.handle, k32, count, d_base.data_ptr(), d_exp.data_ptr(),
+        ctx.check(fn(ctx.handle, k32, count, d_base.data_ptr(), d_exp.data_ptr(),
                                               E.shape[1], ebits_nominal, d_idx.data_ptr(), d_mod.data_ptr(),
                                               nmod, d_out.data_ptr()))
     once()
@@ -81,12 +83,14 @@ if __name__ == "__main__":
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--widths", default="128,64")
     ap.add_argument("--groups", default="0", help="lanes per instance to force (0 = automatic), comma list")
+    ap.add_argument("--keyed", action="store_true", help="fsdkr_modexp_keyed_device (exponent per modulus)")
     a = ap.parse_args()
     ctx = Context(timing=True)
     for k in [int(x) for x in a.widths.split(",")]:
         for g in [int(x) for x in a.groups.split(",")]:
             ctx.set_modexp_group(g)
-            r = run(ctx, k, a.count, 16, a.reps, 1234 + k)
+            r = run(ctx, k, a.count, 16, a.reps, 1234 + k, a.keyed)
             r["group"] = g
+            r["keyed"] = a.keyed
             print(json.dumps(r), flush=True)
     ctx.set_modexp_group(0)

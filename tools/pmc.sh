@@ -1,7 +1,8 @@
 #!/bin/bash
 # PMC passes over the metric-2 modexp launch (65 536 x 4096-bit modexp, exponent N,
 # modulus N^2), one rocprofv3 run per counter group (gfx950 slot limits: FETCH_SIZE
-# and WRITE_SIZE never share a pass).  Usage (via gpurun): bash tools/pmc.sh TAG
+# and WRITE_SIZE never share a pass).  Usage (via gpurun): bash tools/pmc.sh TAG [--keyed]
+# (--keyed: the exponent-per-key launch, modexp_slide_kernel)
 set -o pipefail
 TAG=${1:-pmc}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -9,7 +10,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-CMD="python3 $R/tools/bench_modexp.py --count 65536 --reps 1 --widths 128"
+CMD="python3 $R/tools/bench_modexp.py --count 65536 --reps 1 --widths 128 $2"
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || echo "counter listing failed rc=$?"
 pass() {
   local name=$1; shift
