@@ -810,6 +810,15 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
     qs_env = (e && e[0] == '0') ? 0 : 1;
   }
   const bool qs = qs_env == 1;
+  // the 4-lane throughput shapes run quotient-scaled rows too (no v_mul_lo_u32
+  // per row: metric 2 -1.5 % keyed, -0.9 % per-instance exponents, interleaved,
+  // profiles/r05/r05qs4_*); FSDKR_QS4=0 keeps them plain (A/B)
+  static int qs4_env = -1;
+  if (qs4_env < 0) {
+    const char* e = getenv("FSDKR_QS4");
+    qs4_env = (e && e[0] == '0') ? 0 : 1;
+  }
+  const bool qs4 = qs && qs4_env == 1;
   if (a.slide) {   // shared exponent per wave: the 4096-bit shapes of GA
     if (k32 != 128 || a.ct || a.group == kWaveGroup) return hipErrorInvalidValue;
     if (a.group == kWideGroup) {   // 32 lanes (KD = 160 constants, the caller's): small launches
@@ -823,14 +832,15 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
                                : (qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st));
         case 8: return a.tail ? (qs ? launch_modexp_tail<144, 8, 128, true>(a, st) : launch_modexp_tail<144, 8, 128, false>(a, st))
                               : (qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st));
-        case 4: return a.tail ? launch_modexp_tail<144, 4, 128, false>(a, st) : launch_modexp_slide<144, 4, 128, false>(a, st);
+        case 4: return a.tail ? (qs4 ? launch_modexp_tail<144, 4, 128, true>(a, st) : launch_modexp_tail<144, 4, 128, false>(a, st))
+                              : (qs4 ? launch_modexp_slide<144, 4, 128, true>(a, st) : launch_modexp_slide<144, 4, 128, false>(a, st));
         default: return hipErrorInvalidValue;
       }
     }
     switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
       case 16: return qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st);
       case 8: return qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st);
-      default: return launch_modexp_slide<144, 4, 128, false>(a, st);
+      default: return qs4 ? launch_modexp_slide<144, 4, 128, true>(a, st) : launch_modexp_slide<144, 4, 128, false>(a, st);
     }
   }
   switch (k32) {
@@ -840,10 +850,10 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
     case 64:
       switch (pick_group(a.count, (int)a.group, {2, 4, 8}, 4)) {
         case 8: return qs ? launch_modexp<72, 8, 64, false, true>(a, st) : launch_modexp<72, 8, 64>(a, st);
-        case 4: return launch_modexp<72, 4, 64>(a, st);
+        case 4: return qs4 ? launch_modexp<72, 4, 64, false, true>(a, st) : launch_modexp<72, 4, 64>(a, st);
         default: return launch_modexp<72, 2, 64>(a, st);
       }
-    case 96: return launch_modexp<108, 4, 96>(a, st);
+    case 96: return qs4 ? launch_modexp<108, 4, 96, false, true>(a, st) : launch_modexp<108, 4, 96>(a, st);
     case 128:
       // 32 lanes only on explicit request: it needs KD = 160 constants (mod_setup_g)
       if (a.group == kWideGroup)
@@ -854,12 +864,12 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
       switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
         case 16: return qs ? launch_modexp<144, 16, 128, false, true>(a, st) : launch_modexp<144, 16, 128>(a, st);
         case 8: return qs ? launch_modexp<144, 8, 128, false, true>(a, st) : launch_modexp<144, 8, 128>(a, st);
-        default: return launch_modexp<144, 4, 128>(a, st);
+        default: return qs4 ? launch_modexp<144, 4, 128, false, true>(a, st) : launch_modexp<144, 4, 128>(a, st);
       }
     case 192:
       if (pick_group(a.count, (int)a.group, {4, 8}, 4) == 8)
         return qs ? launch_modexp<216, 8, 192, false, true>(a, st) : launch_modexp<216, 8, 192>(a, st);
-      return launch_modexp<216, 4, 192>(a, st);
+      return qs4 ? launch_modexp<216, 4, 192, false, true>(a, st) : launch_modexp<216, 4, 192>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

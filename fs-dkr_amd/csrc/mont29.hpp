@@ -295,8 +295,8 @@ struct Mont29 {
     const uint32_t a2 = (SQ && !USE_B2) ? ai << 1 : 0u;
     if constexpr (ORDERED) {
       mac_ab<R, SQ, 0>(acc, b, b2, ai, a2);
-      static_assert(!QS, "quotient-scaled rows: group shapes of 8-32 lanes");
-      uint32_t m = (uint32_t)acc[s0] * ninv;
+      // QS: the retiring column is the quotient (no v_mul_lo_u32)
+      uint32_t m = QS ? (uint32_t)acc[s0] : (uint32_t)acc[s0] * ninv;
       __builtin_amdgcn_sched_barrier(0);
       mac_ab_rest<R, SQ>(acc, b, b2, ai, a2, std::make_integer_sequence<int, L - 1>{});
       __builtin_amdgcn_sched_barrier(0);
