@@ -72,6 +72,7 @@ int collect_launch_impl(Ctx* c) {
   //             challenges come from prepare's host pass)
   //   side 2  :                    J2 (nn, 256-bit challenges) -> nn inverses
   //   side 5  :                    pdl_u1 (secp256k1)
+  //   side 7  :                    Alice's hash prefix (alice_prefix)
   std::vector<hipEvent_t> done;
   // issue-priority levels of the serial chains: GA, FB tables, GD/GC, J5 (measured)
   uint32_t prio[4] = {3, 3, 2, 1};
@@ -237,6 +238,23 @@ int collect_launch_impl(Ctx* c) {
     }
     if (rc || (rc = join_later(ss))) return rc;
   }
+  // Alice's hash prefix H(N, N+1, c, z) (inputs only) beside the exponentiations:
+  // the pipeline's last kernel, alice_hash, then absorbs only u and w
+  // (FSDKR_AH_PREFIX=0: the whole hash at the end, A/B; read per call)
+  const char* ahp_env = getenv("FSDKR_AH_PREFIX");
+  const bool ahp = P && !(ahp_env && ahp_env[0] == '0');
+  uint32_t* ah_state = ahp ? (uint32_t*)c->buf("alice_state", (size_t)P * 32 * 4) : nullptr;
+  if (ahp && !ah_state) {
+    c->fail("fsdkr_collect_launch: device allocation failed (alice hash state)");
+    return FSDKR_E_OOM;
+  }
+  if (ahp) {
+    hipStream_t ss = c->side_stream(7);
+    (void)hipStreamWaitEvent(ss, ready, 0);
+    AliceHashArgs a{(const uint64_t*)(dev + pl.d_ahn), (const uint64_t*)(dev + pl.d_ahc), PI(pl.o_az), PX(pl.x_u),
+                    PX(pl.x_w), PI(pl.o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + pl.x_rng), P, ah_state};
+    if ((rc = c->hip_check(launch_alice_prefix(a, ss), "alice_prefix")) || (rc = join_later(ss))) return rc;
+  }
   if (!pl.ch_hit) {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
     hipStream_t ss = c->side_stream(5);
     (void)hipStreamWaitEvent(ss, ready, 0);
@@ -293,7 +311,7 @@ int collect_launch_impl(Ctx* c) {
   }
   {
     AliceHashArgs a{(const uint64_t*)(dev + pl.d_ahn), (const uint64_t*)(dev + pl.d_ahc), PI(pl.o_az), PX(pl.x_u),
-                    PX(pl.x_w), PI(pl.o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + pl.x_rng), P};
+                    PX(pl.x_w), PI(pl.o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + pl.x_rng), P, ah_state};
     c->mark("alice_hash", true);
     rc = c->hip_check(launch_alice_hash(a, st), "alice_hash");
     c->mark("alice_hash", false);

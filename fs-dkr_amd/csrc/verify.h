@@ -33,6 +33,7 @@ struct AliceHashArgs {      // H(N, N+1, c, z, u, w) == e
   uint32_t n_len, c_len, z_len, e_len;
   uint8_t* verdict;         // in: host pre-checks, out: AND hash equality
   uint32_t count;
+  uint32_t* state;          // [count][32] SHA-256 state after H(N, N+1, c, z) (alice_prefix), or null
 };
 
 struct InverseArgs {
@@ -147,6 +148,7 @@ struct EcMsmArgs {          // out[o] = sum_j scalars[o][j] * P[o][j]
 hipError_t launch_binom(const BinomArgs& a, hipStream_t st);
 hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st);
 hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st);
+hipError_t launch_alice_prefix(const AliceHashArgs& a, hipStream_t st);
 hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);
 // lane-cooperative Pornin inverse (inverse.hip): registers + DPP
 hipError_t launch_inverse_coop(uint32_t k32, const InverseArgs& a, hipStream_t st);

@@ -160,14 +160,9 @@ __global__ __launch_bounds__(64) void ped_hash_kernel(const PedHashArgs a) {
     if ((be[i >> 3] >> (i & 7)) & 1u) bits[i >> 5] |= 1u << (i & 31);
 }
 
-// e' = H(N, N+1, c, z, u, w) == e  ->  verdict bit (AND-ed with the host's pre-checks)
-__global__ void alice_hash_kernel(const AliceHashArgs a) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.count) return;
+// the inputs-only prefix of Alice's hash: N, N + 1, c, z (range_proofs.rs:150-154)
+__device__ __forceinline__ void alice_absorb_prefix(Sha256& h, const AliceHashArgs& a, uint32_t p) {
   const uint32_t* N = P32(a.n_ptr[p]);
-  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
-  Sha256 h;
-  h.init(sha_w + threadIdx.x * 16);
   h.bigint(N, a.n_len);
   // N + 1, streamed limb by limb from the top: compute the carry chain first
   {
@@ -187,6 +182,47 @@ __global__ void alice_hash_kernel(const AliceHashArgs a) {
   }
   h.bigint(P32(a.c_ptr[p]), a.c_len);
   h.bigint(a.z + (size_t)p * a.z_len, a.z_len);
+}
+
+// The SHA-256 state after the prefix, per proof: launched early beside the
+// exponentiations, so the pipeline's last kernel (alice_hash) absorbs only u and
+// w (12 of ~32 blocks at 2048-bit keys).  [h0..h7 | nbuf | total lo, hi | w0..w15]
+__global__ void alice_prefix_kernel(const AliceHashArgs a) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.count) return;
+  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
+  Sha256 h;
+  h.init(sha_w + threadIdx.x * 16);
+  alice_absorb_prefix(h, a, p);
+  uint32_t* s = a.state + (size_t)p * 32;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = h.h[i];
+  s[8] = h.nbuf;
+  s[9] = (uint32_t)h.total;
+  s[10] = (uint32_t)(h.total >> 32);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[11 + i] = h.w[i];
+}
+
+// e' = H(N, N+1, c, z, u, w) == e  ->  verdict bit (AND-ed with the host's pre-checks);
+// with a.state the prefix comes from alice_prefix_kernel
+__global__ void alice_hash_kernel(const AliceHashArgs a) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.count) return;
+  __shared__ uint32_t sha_w[64 * 16];  // launch blocks are 64 threads
+  Sha256 h;
+  h.init(sha_w + threadIdx.x * 16);
+  if (a.state) {
+    const uint32_t* s = a.state + (size_t)p * 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h.h[i] = s[i];
+    h.nbuf = s[8];
+    h.total = (uint64_t)s[9] | ((uint64_t)s[10] << 32);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) h.w[i] = s[11 + i];
+  } else {
+    alice_absorb_prefix(h, a, p);
+  }
   h.bigint(a.u + (size_t)p * a.c_len, a.c_len);
   h.bigint(a.w + (size_t)p * a.z_len, a.z_len);
   uint32_t d[8];
@@ -213,6 +249,12 @@ hipError_t launch_ped_hash(const PedHashArgs& a, hipStream_t st) {
 hipError_t launch_alice_hash(const AliceHashArgs& a, hipStream_t st) {
   if (!a.count) return hipSuccess;
   hipLaunchKernelGGL(alice_hash_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_alice_prefix(const AliceHashArgs& a, hipStream_t st) {
+  if (!a.count) return hipSuccess;
+  if (!a.state) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(alice_prefix_kernel, dim3(blocks_for(a.count, 64)), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 
