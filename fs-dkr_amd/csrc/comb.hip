@@ -107,12 +107,15 @@ __global__ __launch_bounds__(64 * COMB_SCHED_IPB) void comb_sched_kernel(const C
 
 // base^e from the instance's tables: acc = G[0][u_0], then per step a product by
 // G[j][u] (a squaring first at every j = 0 after the first column), lockstep.
-template <int KD, int G, int K32>
+// QS: quotient-scaled rows (the chain modulo N' = N (-N^-1 mod 2^29), exit modulo N;
+// the tables' residues mod N are valid inputs, as in modexp_kernel QS)
+template <int KD, int G, int K32, bool QS>
 __global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs args) {
   using MT = Mont29<KD, G>;
   constexpr int L = MT::L;
   constexpr int IPB = BLOCK / G;
   constexpr int STRIDE = cons_stride(KD);
+  static_assert(!QS || scaled_ok(KD, K32), "quotient-scaled chains: N' within R/4");
   __shared__ uint32_t lds[IPB * KD];
   const int g = threadIdx.x % G;
   const int li = threadIdx.x / G;
@@ -126,7 +129,8 @@ __global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs args)
   else if (args.prio == 2) __builtin_amdgcn_s_setprio(2);
   else if (args.prio == 1) __builtin_amdgcn_s_setprio(1);
   uint32_t* stream = lds + li * KD;
-  const uint32_t* C = args.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  const uint32_t* C0 = args.consts + (size_t)a.mod_idx[inst] * STRIDE;
+  const uint32_t* C = QS ? C0 + cons_scaled(KD) : C0;
   MT M;
   M.init_lane(g);
 #pragma unroll
@@ -149,16 +153,23 @@ __global__ __launch_bounds__(BLOCK) void comb_exp_kernel(const CombExpArgs args)
 #pragma unroll
       for (int k = 0; k < L; ++k) stream[g * L + k] = acc[k];
       __builtin_amdgcn_wave_barrier();
-      M.sqr(acc, acc, stream);
+      if constexpr (QS) M.sqr_s(acc, acc, stream);
+      else M.sqr(acc, acc, stream);
     }
     const uint32_t* P = tab + ((size_t)j * TS + S[st]) * KD;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int k = 0; k < L; ++k) stream[k * G + g] = P[k * G + g];   // coalesced over the group
     __builtin_amdgcn_wave_barrier();
-    M.mul(acc, acc, stream);
+    if constexpr (QS) M.mul_s(acc, acc, stream);
+    else M.mul(acc, acc, stream);
   }
-  // leave Montgomery form: acc * 1 / R, then exact reduction
+  // leave Montgomery form: acc * 1 / R, then exact reduction (modulo N itself)
+  if constexpr (QS) {
+#pragma unroll
+    for (int k = 0; k < L; ++k) M.n[k] = C0[g * L + k];
+    M.ninv = C0[3 * KD];
+  }
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int k = 0; k < L; ++k) stream[g * L + k] = (g == 0 && k == 0) ? 1u : 0u;
@@ -190,7 +201,7 @@ static hipError_t build_launch(const CombBuildArgs& a, hipStream_t st) {
   }
   return hipGetLastError();
 }
-template <int KD, int G, int K32>
+template <int KD, int G, int K32, bool QS>
 static hipError_t exp_launch(CombExpArgs& a, hipStream_t st) {
   uint64_t lanes = 0;
   for (uint32_t k = 0; k < a.ngroups; ++k) lanes += (uint64_t)a.g[k].count * G;
@@ -201,7 +212,7 @@ static hipError_t exp_launch(CombExpArgs& a, hipStream_t st) {
     blocks += (a.g[k].count + ipb - 1) / ipb;
   }
   if (!blocks) return hipSuccess;
-  hipLaunchKernelGGL((comb_exp_kernel<KD, G, K32>), dim3(blocks), dim3(bs), 0, st, a);
+  hipLaunchKernelGGL((comb_exp_kernel<KD, G, K32, QS>), dim3(blocks), dim3(bs), 0, st, a);
   return hipGetLastError();
 }
 
@@ -225,9 +236,22 @@ hipError_t launch_comb_exp(uint32_t k32, CombExpArgs& a, int group, hipStream_t 
   if (a.ngroups == 0 || a.ngroups > (uint32_t)kCombGroups) return hipErrorInvalidValue;
   for (uint32_t k = 0; k < a.ngroups; ++k)
     if (!a.g[k].steps) return hipErrorInvalidValue;
+  // quotient-scaled rows by default (no v_mul_lo_u32 per row); FSDKR_COMB_QS=0: plain (A/B)
+  static int qs_env = -1;
+  if (qs_env < 0) {
+    const char* e = getenv("FSDKR_COMB_QS");
+    qs_env = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (qs_env) {
+    switch (k32) {
+      case 64: return group == 8 ? exp_launch<72, 8, 64, true>(a, st) : exp_launch<72, 4, 64, true>(a, st);
+      case 96: return exp_launch<108, 4, 96, true>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (k32) {
-    case 64: return group == 8 ? exp_launch<72, 8, 64>(a, st) : exp_launch<72, 4, 64>(a, st);
-    case 96: return exp_launch<108, 4, 96>(a, st);
+    case 64: return group == 8 ? exp_launch<72, 8, 64, false>(a, st) : exp_launch<72, 4, 64, false>(a, st);
+    case 96: return exp_launch<108, 4, 96, false>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

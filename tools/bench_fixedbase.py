@@ -33,8 +33,11 @@ def main():
         ctx.fixed_base_modexp(bases, list(range(a.bases)), mods, bidx, exps, 64)
     tt, nt = ctx.kernel_time("fb_table")
     te, ne = ctx.kernel_time("fb_exp")
+    tc, nc = ctx.kernel_time("comb_exp")
     print(json.dumps({"bases": a.bases, "per_base": a.per_base, "bits": a.bits, "fb_table_ms": tt / max(nt, 1),
-                      "fb_exp_ms": te / max(ne, 1), "table_us_per_square": tt / max(nt, 1) * 1e3 / a.bits}))
+                      "fb_exp_ms": te / max(ne, 1), "comb_exp_ms": tc / max(nc, 1), "comb_launches": nc,
+                      "comb_qs": os.environ.get("FSDKR_COMB_QS", "1"),
+                      "table_us_per_square": tt / max(nt, 1) * 1e3 / a.bits}))
 
 
 if __name__ == "__main__":
