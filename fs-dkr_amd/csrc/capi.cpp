@@ -329,10 +329,7 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
   if (c->ct) grp = 0;   // the regular-access kernels have one shape per width
   // sliding windows: the 4096-bit 4/8/16/32-lane shapes, public exponents, waves of
   // `group` lanes uniform (caller), so only at the caller's lane count
-  // FSDKR_SLIDE=0: fixed windows (A/B; n = 64 and n = 256 whole calls within
-  // noise of each other, profiles/r04/r04h_*: fewer products, more control flow)
-  static const bool slide_off = getenv("FSDKR_SLIDE") && atoi(getenv("FSDKR_SLIDE")) == 0;
-  const bool slide = !slide_off && (desc_flags & kDescSlide) && (desc_flags & kDescOutIdx) && k32 == 128 && !c->ct &&
+  const bool slide = (desc_flags & kDescSlide) && (desc_flags & kDescOutIdx) && k32 == 128 && !c->ct &&
                      grp == group && (grp == 4 || grp == 8 || grp == 16 || grp == kWideGroup);
   const int KD = table_digits(k32, grp);
   if (!KD) {
@@ -555,7 +552,8 @@ int fsdkr_ctx_create(const fsdkr_cfg* cfg, fsdkr_ctx** out) {
     (void)hipGetDevice(&dev);
   }
   c->device = dev;
-  c->timing = cfg && (cfg->flags & FSDKR_CFG_TIMING);
+  c->flags = cfg ? cfg->flags : 0u;
+  c->timing = (c->flags & FSDKR_CFG_TIMING) != 0;
   if (!(c->stream = make_stream(c, 0))) {
     delete c;
     return FSDKR_E_HIP;
@@ -643,6 +641,16 @@ int fsdkr_ctx_set_timing(fsdkr_ctx* ctx, int on) {
   if (!c) return FSDKR_E_ARG;
   int rc = c->sync();   // fold events of launches made under the old setting
   c->timing = on != 0;
+  c->flags = on ? (c->flags | FSDKR_CFG_TIMING) : (c->flags & ~FSDKR_CFG_TIMING);
+  return rc;
+}
+
+int fsdkr_ctx_set_flags(fsdkr_ctx* ctx, uint32_t flags) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  int rc = c->sync();
+  c->flags = flags;
+  c->timing = (flags & FSDKR_CFG_TIMING) != 0;
   return rc;
 }
 
@@ -691,7 +699,7 @@ int fsdkr_mod_inverse(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t count, const 
   // simultaneous inversion, inverse_batch_kernel) where the width has that shape
   std::vector<uint32_t> order(count), gstart;
   for (uint32_t i = 0; i < count; ++i) order[i] = i;
-  const size_t kd = batch_inv_on() ? inverse_batch_scratch_words(mod_limbs) : 0;
+  const size_t kd = batch_inv_on(c) ? inverse_batch_scratch_words(mod_limbs) : 0;
   if (kd) {
     auto row = [&](uint32_t i) { return m + (size_t)i * mod_limbs; };
     std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y2) {

@@ -25,13 +25,9 @@ void free_ga_pre(Ctx* c) {
   if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
   if (g && g->fb_setup) (void)hipEventDestroy(g->fb_setup);
-  if (g && g->fx_done) (void)hipEventDestroy(g->fx_done);
   if (g && g->ck_done) (void)hipEventDestroy(g->ck_done);
   if (g && g->tz_done) (void)hipEventDestroy(g->tz_done);
   if (g && g->comb_done) (void)hipEventDestroy(g->comb_done);
-  if (g)
-    for (hipEvent_t e : g->ch_ev)
-      if (e) (void)hipEventDestroy(e);
   delete g;
   c->ga_pre = nullptr;
 }

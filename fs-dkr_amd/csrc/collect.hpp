@@ -14,11 +14,13 @@
 #include "evp_sha.hpp"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -139,6 +141,8 @@ struct HostSha {
     return ok;
   }
 };
+
+using RowsSha = std::array<uint8_t, 32>;
 
 // PDL challenge e = H(G, Q, c, z, u1, u2, u3) of pair lp of batch b as 8 little-endian
 // limbs (zk_pdl_with_slack.rs:114-122; every value as curv's to_bytes)
@@ -331,10 +335,6 @@ struct CollectPlan {
   // equalities read them once tz_done has fired
   bool tz_hit = false;
   hipEvent_t tz_done = nullptr;
-  // the challenge jobs (J2, J5, their inverses, pdl_u1, Feldman) computed by the
-  // prestart (ch_hit): the pipeline waits for ch_ev before its equalities
-  bool ch_hit = false;
-  hipEvent_t ch_ev[3] = {};
   // GA's joint tail (ga_split_ok): J2 is not run; GA computes s2^N c^-e_pdl | s^N c^-e_A,
   // the nn inverse is c's own (unit flags of c); job slot 2 then holds J9
   bool joint = false;
@@ -346,10 +346,7 @@ struct CollectPlan {
     uint32_t count = 0, bits = 0, group = 0, flags = 0;
   } ga_tail;
   std::vector<uint8_t> ae_zero;        // Alice e == 0: c^0 = 1 whatever c is
-  // the fixed-base exponents computed by the prestart (fx_hit): J3 / J4 / RP rows there
-  bool fx_hit = false;
-  hipEvent_t fx_done = nullptr;
-  // device words finish reads back (the plan's output region, or the prestart's)
+  // device words finish reads back (the plan's output region)
   const void *r_unn = nullptr, *r_uzA = nullptr, *r_uzp = nullptr, *r_pdlv = nullptr, *r_fel = nullptr;
   FbJob fb;
   size_t d_FB = 0;
@@ -409,48 +406,24 @@ struct GaPre {
   const uint32_t* fb_cons = nullptr;
   // ring-Pedersen T_m^Z_{m,k} of every message (fsdkr_collect_prestart_rp): the
   // fixed-base exponents behind the prestarted T tables, rows m*M + k at width nl;
-  // prepare drops them from its fixed-base job when tz_digest and the T rows match
+  // prepare drops them from its fixed-base job when the T rows and the Z rows' SHA-256 match
   bool tz_valid = false;
   uint32_t tz_Mt = 0, tz_M = 0;
-  uint64_t tz_digest = 0;
+  std::vector<RowsSha> tz_sha;             // SHA-256 of the Z rows, per block of kShaRows rows
   uint32_t* tz_out = nullptr;
   const uint32_t* tz_z = nullptr;        // the device copy of the Z rows [Mt*M][tz_zl]
   uint32_t tz_zl = 0;
   hipEvent_t tz_done = nullptr;
-  // device rows the later prestart jobs read: N_i^2 (GA's image, n x nn) and N~_i (the
-  // table chains' moduli, n x nl)
-  const uint32_t* nn_rows = nullptr;
-  const uint32_t* nt_rows = nullptr;
-  // the challenge jobs (prestart_chal, once stage 1c packed their fields): PDL challenges
-  // (host), J2 = c^e_pdl | c^e_A mod N_i^2, J5 = z^e_pdl | zA^e_A mod N~_i, the inverses
-  // and unit flags, pdl_u1, Feldman.  ch_host keeps the rows they read (prepare's match).
-  bool ch_valid = false;
-  uint32_t ch_P = 0, ch_V = 0, ch_el = 0, ch_s1l = 0, ch_n_inv_nn = 0;
-  const uint8_t* ch_host = nullptr;
-  struct ChRows {   // offsets of the compared fields in ch_host (rows at the session widths)
-    size_t enc, pz, pu1, pu2, pu3, Q, az, ae, ps1, as1, vss, vlen, rn, rt;
-  } ch_off{};
-  std::vector<uint32_t> ch_epdl;          // [P][8]
-  std::vector<uint32_t> ch_cpdl_extra;    // pairs whose c unit test is an extra nn inverse
-  uint32_t *ch_J2 = nullptr, *ch_J5 = nullptr, *ch_invc = nullptr, *ch_invz = nullptr;
-  uint32_t *ch_unn = nullptr, *ch_uzA = nullptr, *ch_uzp = nullptr;
-  uint8_t *ch_pdlv = nullptr, *ch_fel = nullptr;
-  hipEvent_t ch_ev[3] = {};
-  // the fixed-base exponents (prestart_fbx, when stage 1b packed the exponents): h1^s1 |
-  // h1^s1A -> J3 slots, h2^s3 | h2^s2A -> J4 slots, T_m^Z_k -> RP rows, as combs over the
-  // prestarted tables; fx_host keeps the exponent rows for prepare's match
-  bool fx_valid = false;
-  uint32_t fx_s1l = 0, fx_s3l = 0, fx_zl = 0;
-  const uint8_t* fx_host = nullptr;
-  size_t fx_ps1 = 0, fx_as1 = 0, fx_ps3 = 0, fx_as2 = 0, fx_z = 0;   // offsets in fx_host
-  uint32_t *fx_J3 = nullptr, *fx_J4 = nullptr, *fx_RP = nullptr;
-  hipEvent_t fx_done = nullptr;
 };
 
-// width-independent 64-bit digest of `rows` rows of `w` words (trailing zero
-// words ignored), order-dependent, computed in parallel (prestart and prepare
-// compare the ring-Pedersen Z rows with it)
-uint64_t rows_digest(const uint32_t* p, size_t rows, uint32_t w, uint64_t row0);
+// SHA-256 of a sequence of rows, one digest per block of kShaRows consecutive rows
+// (computed in parallel, one block per task).  A row enters as its length in words
+// without trailing zero words (u32) and those words, so rows of equal value hash
+// alike at any packed width and the encoding is injective.  Prestart and prepare
+// compare the ring-Pedersen Z rows with it: equal digest vectors mean equal rows
+// up to a SHA-256 collision.  `row(r)` returns {pointer, width} of global row r.
+constexpr size_t kShaRows = 2048;
+std::vector<RowsSha> rows_sha256(size_t rows, const std::function<std::pair<const uint32_t*, uint32_t>(size_t)>& row);
 
 // collect()'s fixed-base tables, base order [h1_i | T_m | h2_i] (FbJob::finalize
 // sizes: one entry per w exponent bits, at least one)
@@ -504,18 +477,7 @@ inline void ped_modulus(const fsdkr_collect_batch* b, uint32_t m, uint32_t M, ui
 // 4-lane shape wins: n = 256 (131 072 chains) 592 ms per call at 8 lanes, 571 ms
 // at 4, 628 ms at 16 (profiles/r04/r04e_ab_n256_lanes_v*).  Used by the prestart
 // and by launch().
-// FSDKR_GA_LANES / FSDKR_J2_LANES (4, 8, 16; 32 and 64 at 4096 bits) override the
-// choice (A/B runs).
-inline uint32_t lanes_env(const char* name, uint32_t nn) {
-  const char* e = getenv(name);
-  if (!e) return 0;
-  const uint32_t g = (uint32_t)atoi(e);
-  if (g == 4 || g == 8 || g == 16) return g;
-  if (nn == 128 && (g == kWideGroup || g == kWaveGroup)) return g;
-  return 0;
-}
 inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
-  if (uint32_t e = lanes_env("FSDKR_GA_LANES", nn)) return e;
   if (nn != 128) return (uint64_t)count * 16 <= 65536u ? 16 : 8;
   return count <= 16384u ? 16 : 4;
 }
@@ -523,7 +485,6 @@ inline uint32_t ga_lanes(uint32_t count, uint32_t nn) {
 // J2 (c^e mod N^2, 256-bit exponents) lanes per instance, when the joint tail
 // does not absorb it
 inline uint32_t j2_lanes(size_t count, uint32_t nn) {
-  if (uint32_t e = lanes_env("FSDKR_J2_LANES", nn)) return e;
   return nn == 128 ? (count <= 1024 ? kWaveGroup : count <= 16384 ? 16 : 8) : 8;
 }
 
@@ -536,19 +497,13 @@ inline uint32_t ga_desc_flags(bool aligned_for, uint32_t group) {
 // GA's joint tail (modexp.hip modexp_tail_kernel): the chains s2^N | s^N mod N^2 run
 // as a head over N's bits >= kGaSplit and a tail that multiplies c^-e_pdl | c^-e_A in
 // along its squarings (e < 2^256), so no separate c^e chain (J2) runs.  For the
-// sliding-window GA shapes (4096-bit, 4 / 8 / 16 / 32 lanes); FSDKR_JOINT=0 keeps J2
-// (A/B).  Read per call.
+// sliding-window GA shapes (4096-bit, 4 / 8 / 16 / 32 lanes): n = 64 -0.8 ms,
+// configs[3] -8 % against a separate J2 (profiles/r05/r05e_*, r05f_*)
 constexpr uint32_t kGaSplit = 256;
-// GA's issue priority (s_setprio of the prestarted chains and of the joint tail);
-// FSDKR_GA_PRIO overrides it (A/B)
-inline uint32_t ga_prio() {
-  const char* e = getenv("FSDKR_GA_PRIO");
-  return e ? (uint32_t)std::min(3, std::max(0, atoi(e))) : 2u;
-}
+// GA's issue priority (s_setprio of the prestarted chains and of the joint tail;
+// priority 3 measured 0.5-1 ms slower at n = 64, profiles/r04/r04g_*)
+inline uint32_t ga_prio() { return 2u; }
 inline bool ga_split_ok(uint32_t nn, uint32_t group, uint32_t flags) {
-  const char* j = getenv("FSDKR_JOINT");
-  const char* s = getenv("FSDKR_SLIDE");
-  if ((j && atoi(j) == 0) || (s && atoi(s) == 0)) return false;
   return nn == 128 && (flags & kDescSlide) && (flags & kDescOutIdx) &&
          (group == 4 || group == 8 || group == 16 || group == kWideGroup);
 }
@@ -560,8 +515,6 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
 int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 bool ga_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
-bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
-bool fbx_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_prepare.cpp
 int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count);
 // collect_launch.cpp

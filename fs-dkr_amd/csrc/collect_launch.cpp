@@ -104,7 +104,7 @@ int collect_launch_impl(Ctx* c) {
   auto pair_inverse = [&](uint32_t k32, const uint64_t* y, const uint64_t* m, uint32_t* out, uint32_t* unit,
                           uint32_t count, hipStream_t s, const char* scratch_tag, const char* what) -> int {
     const size_t kd = inverse_batch_scratch_words(k32);
-    if (batch_inv_on() && kd && count == P && pl.binv_ngroups) {
+    if (batch_inv_on(c) && kd && count == P && pl.binv_ngroups) {
       uint32_t* scr = (uint32_t*)c->buf(scratch_tag, (size_t)count * kd * 4);
       if (!scr) {
         c->fail("device allocation failed (inverse scratch)");
@@ -184,7 +184,7 @@ int collect_launch_impl(Ctx* c) {
     }
     if ((rc = join_later(ss))) return rc;
   }
-  if (!pl.ch_hit) {  // Feldman share checks (inputs only; one Horner chain per pair; else prestarted)
+  {  // Feldman share checks (inputs only; one Horner chain per pair)
     hipStream_t ss = c->side_stream(6);
     // one Horner chain of t+1 small-scalar steps per pair on one thread: ~2 % of
     // GA's work at n = 256, but a long serial chain; at the default priority it
@@ -224,12 +224,12 @@ int collect_launch_impl(Ctx* c) {
   }
   hipEvent_t ready;
   if ((rc = fork(st, &ready))) return rc;
-  {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses (prestarted on a chal hit)
+  {  // J2: c^e (4096-bit, 256-bit challenges) -> nn inverses
     hipStream_t ss = c->side_stream(2);
     (void)hipStreamWaitEvent(ss, ready, 0);
     // (joint: slot 2 holds J9, (N+1)^s1 for s1 >= N, at the generic lane count)
     if ((rc = launch_group(2, ss, 0, pl.joint ? 0u : j2_group, cons_nn))) return rc;
-    if (!pl.ch_hit && !pl.joint) {
+    if (!pl.joint) {
       InverseArgs a{(const uint64_t*)(dev + pl.d_iynn), (const uint64_t*)(dev + pl.d_imnn), PX(pl.x_invc),
                     PX(pl.x_unn), nullptr, pl.n_inv_nn};
       c->mark("inverse", true, ss);
@@ -239,10 +239,9 @@ int collect_launch_impl(Ctx* c) {
     if (rc || (rc = join_later(ss))) return rc;
   }
   // Alice's hash prefix H(N, N+1, c, z) (inputs only) beside the exponentiations:
-  // the pipeline's last kernel, alice_hash, then absorbs only u and w
-  // (FSDKR_AH_PREFIX=0: the whole hash at the end, A/B; read per call)
-  const char* ahp_env = getenv("FSDKR_AH_PREFIX");
-  const bool ahp = P && !(ahp_env && ahp_env[0] == '0');
+  // the pipeline's last kernel, alice_hash, then absorbs only u and w (device span
+  // -0.5 ms at n = 64 against the whole hash at the end, profiles/r05/r05ahp_ab/)
+  const bool ahp = P != 0;
   uint32_t* ah_state = ahp ? (uint32_t*)c->buf("alice_state", (size_t)P * 32 * 4) : nullptr;
   if (ahp && !ah_state) {
     c->fail("fsdkr_collect_launch: device allocation failed (alice hash state)");
@@ -255,7 +254,7 @@ int collect_launch_impl(Ctx* c) {
                     PX(pl.x_w), PI(pl.o_ae), nl, nn, nl, pl.el, (uint8_t*)(out_base + pl.x_rng), P, ah_state};
     if ((rc = c->hip_check(launch_alice_prefix(a, ss), "alice_prefix")) || (rc = join_later(ss))) return rc;
   }
-  if (!pl.ch_hit) {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
+  {  // PDL u1 on secp256k1 (one Shamir ladder per pair, latency-bound) off the main chain
     hipStream_t ss = c->side_stream(5);
     (void)hipStreamWaitEvent(ss, ready, 0);
     PdlU1Args u{PI(pl.o_ps1), PI(pl.o_epdl), PI(pl.o_Q), PI(pl.o_pu1), pl.s1l, (uint8_t*)(out_base + pl.x_pdlv), P};
@@ -268,7 +267,7 @@ int collect_launch_impl(Ctx* c) {
   (void)hipEventDestroy(consts_ready);
   (void)hipEventDestroy(ready);
   if (inv_done) (void)hipEventDestroy(inv_done);
-  if (!pl.ch_hit) {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses (else prestarted)
+  {  // J5: z^e (2048-bit, 256-bit challenges) -> nl inverses
     hipStream_t js = st;
     if ((rc = launch_group(3, js, prio[3], j5_group, cons_nl))) return rc;
     c->mark("inverse", true, js);
@@ -286,9 +285,6 @@ int collect_launch_impl(Ctx* c) {
   }
   if (pl.ga_hit) (void)hipStreamWaitEvent(st, pl.ga_done, 0);   // the prestarted s^N rows
   if (pl.tz_hit) (void)hipStreamWaitEvent(st, pl.tz_done, 0);   // the prestarted ring-Pedersen T^Z rows
-  if (pl.fx_hit) (void)hipStreamWaitEvent(st, pl.fx_done, 0);   // the prestarted fixed-base exponents
-  if (pl.ch_hit)   // the prestarted challenge jobs (J2, J5 -> inverses; pdl_u1 -> Feldman)
-    for (hipEvent_t ev : pl.ch_ev) (void)hipStreamWaitEvent(st, ev, 0);
   // exact products (first: the negative-s3 pairs' u3 check reads rows of x_w), equality checks
   {
     Prod3Args pa{(const Prod3Operand*)(dev + pl.d_p3nn), PI(pl.d_p3m), cons_nn, PX(pl.x_u), P};

@@ -113,23 +113,15 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     pl.pre_cons_wide = gpre->wide;
     gpre->valid = false;   // consumed (the buffer lives until the next prestart)
   }
-  // prestarted challenge jobs of this batch (stage 1c): J2, J5, their inverses,
-  // pdl_u1 and Feldman are not launched again, the PDL challenges not hashed again
   // GA's joint tail: the prestart ran the split head (gpre->split), or prepare's own GA
-  // (J1 alone, padded to whole waves) takes a sliding-window shape; the challenge
-  // prestart's c^e rows are then not used
+  // (J1 alone, padded to whole waves) takes a sliding-window shape
   {
     const uint32_t g0 = ga_lanes(2 * P, nn);
     pl.joint = pl.ga_hit ? gpre->split : ga_split_ok(nn, g0, ga_desc_flags(true, g0));
   }
-  pl.ch_hit = !pl.joint && chal_pre_matches(c, bs, count) && gpre->ch_P == P;
   if (pl.joint && pl.ga_hit)
     pl.ga_tail = CollectPlan::GaTail{gpre->ga_desc, gpre->cons, gpre->out, gpre->ga_count, gpre->ga_bits, gpre->ga_group,
                                      gpre->ga_flags};
-  if (pl.ch_hit) {
-    for (int k = 0; k < 3; ++k) pl.ch_ev[k] = gpre->ch_ev[k];
-    gpre->ch_valid = false;   // consumed
-  }
   clk.lap("shapes");
 
   // ---------------- host pre-pass (O(n) + O(P) scans, no big exponentiations; threaded)
@@ -156,9 +148,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   // PDL challenges e = H(G, Q, c, z, u1, u2, u3) (zk_pdl_with_slack.rs:114-122) on the
   // host threads of this scan: J2 (c^e), J5 (z^e) and pdl_u1 can start with the pipeline
   std::vector<uint32_t>& EPDL = pl.e_pdl;
-  if (pl.ch_hit) EPDL = gpre->ch_epdl;
-  else EPDL.assign((size_t)P * 8, 0u);
-  const bool hash = !pl.ch_hit;
+  EPDL.assign((size_t)P * 8, 0u);
   std::atomic<bool> sha_fail{false};
   parallel_for(P, 256, [&](size_t b0, size_t b1) {
     Maxes mx;
@@ -167,7 +157,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       const Sess& x = pl.ss[sess_of_pair[p]];
       const fsdkr_collect_batch* b = x.b;
       const size_t lp = p - x.pbase;
-      if (hash && !pdl_challenge(sha, b, lp, EPDL.data() + p * 8)) sha_fail = true;
+      if (!pdl_challenge(sha, b, lp, EPDL.data() + p * 8)) sha_fail = true;
       // a ciphertext at or above N^2 (GMP reduces it; the joint tail's inverse needs it reduced)
       // (or a negative one, neg_bits bit 2: enc holds |c|, the arithmetic takes -|c| mod N^2)
       big_c[p] = hbn::cmp_raw(b->enc + lp * 2 * b->nl, 2 * b->nl, NN.data() + (size_t)recv_of_pair[p] * nn, nn) >= 0 ||
@@ -429,13 +419,15 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       for (uint32_t k = x.b->nl; k < nl && tz_hit; ++k) tz_hit = a[k] == 0;
     }
   }
-  if (tz_hit) {
-    uint64_t d = 0;
-    for (uint32_t s = 0; s < count; ++s) {
-      const Sess& x = pl.ss[s];
-      d += rows_digest(x.b->ped_Z, (size_t)x.Mt * M, x.b->zl, (size_t)x.mbase * M);
-    }
-    tz_hit = d == gtz->tz_digest;
+  if (tz_hit) {   // the Z rows themselves: SHA-256 per block of rows, as the prestart hashed them
+    std::vector<size_t> zrow0(count + 1, 0);
+    for (uint32_t s = 0; s < count; ++s) zrow0[s + 1] = zrow0[s] + (size_t)pl.ss[s].Mt * M;
+    const std::vector<RowsSha> sha = rows_sha256(zrow0[count], [&](size_t r) {
+      const size_t s = (size_t)(std::upper_bound(zrow0.begin(), zrow0.end(), r) - zrow0.begin()) - 1;
+      const fsdkr_collect_batch* b = pl.ss[s].b;
+      return std::make_pair(b->ped_Z + (r - zrow0[s]) * b->zl, b->zl);
+    });
+    tz_hit = !sha.empty() && sha == gtz->tz_sha;
   }
   if (tz_hit) {
     pl.tz_hit = true;
@@ -670,13 +662,6 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
               same_rows(gp->h2, x.rbase, x.b->recv_h2, x.n, x.b->nl) &&
               same_rows(gp->T, x.mbase, x.b->ped_T, x.Mt, x.b->nl);
   }
-  // the fixed-base exponents of a prestart (stage 1b's exponent rows, the same tables):
-  // h1 / h2 / T^Z instances are not launched again
-  pl.fx_hit = fb_cand && fbx_pre_matches(c, bs, count);
-  if (pl.fx_hit) {
-    pl.fx_done = gp->fx_done;
-    reinterpret_cast<GaPre*>(c->ga_pre)->fx_valid = false;   // consumed
-  }
   // ---------------- modexp jobs (descriptors addressed into the image)
   ModexpJob J1, J2, J5, J7, J8, J9, GC;
   J1.k32 = J2.k32 = J9.k32 = nn;
@@ -710,7 +695,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
         J1.add(which == 0 ? DI(o_ps2 + (size_t)p * nl * 4) : DI(o_as + (size_t)p * nl * 4), nl, Ni, nl, recvn_max, r);
       // J2: c^e (PDL :136-142 via the cross-multiplied check) | c^e (Alice :142)
       const uint64_t cp = big_c[p] ? DI(o_rc + (size_t)p * nn * 4) : DI(o_enc + (size_t)p * nn * 4);
-      if (pl.ch_hit || pl.joint) {   // (prestarted, or joined into GA's tail)
+      if (pl.joint) {   // (joined into GA's tail)
       } else if (which == 0) {
         J2.add(cp, nn, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
@@ -719,19 +704,15 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       // fixed bases (FB): h1^s1 -> J3 slot | h2^s3 (s2 for Alice) -> J4 slot;  J5: z^e
       const size_t slot = (size_t)which * P + p;
       if (which == 0) {
-        if (!pl.fx_hit) {
-          FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
-          fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
-        }
-        if (!pl.ch_hit) J5.add(DI(z_off(0, p, o_pz)), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
+        FB.add(fb_h1[r], DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, DX(x_J3 + slot * nl * 4));
+        fb_later.push_back({fb_h2[r], DI(o_ps3 + (size_t)p * s3l * 4), s3l, mx.s3, DX(x_J4 + slot * nl * 4)});
+        J5.add(DI(z_off(0, p, o_pz)), nl, DI(o_epdl + (size_t)p * 32), 8, 256, r);
       } else {
         const bool use = alice_pre[p];
-        if (!pl.fx_hit) {
-          FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
-          fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
-                              DX(x_J4 + slot * nl * 4)});
-        }
-        if (!pl.ch_hit) J5.add(DI(z_off(1, p, o_az)), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
+        FB.add(fb_h1[r], DI(o_as1 + (size_t)p * s1l * 4), use ? s1l : 0, mx.as1, DX(x_J3 + slot * nl * 4));
+        fb_later.push_back({fb_h2[r], DI(o_as2 + (size_t)p * s3l * 4), use ? s3l : 0, mx.as2,
+                            DX(x_J4 + slot * nl * 4)});
+        J5.add(DI(z_off(1, p, o_az)), nl, DI(o_ae + (size_t)p * el * 4), use ? el : 0, mx.ae, r);
       }
     }
   for (uint32_t p = 0; p < P; ++p)
@@ -741,7 +722,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
       J9.add(DI(o_NP1 + (size_t)r * nn * 4), nn, DI(o_ps1 + (size_t)p * s1l * 4), s1l, mx.s1, r);
     }
   clk.lap("desc pairs");
-  if (!tz_hit && !pl.fx_hit) {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
+  if (!tz_hit) {  // ring-Pedersen T^Z_k mod N (ring_pedersen_proof.rs:144): Mt*M instances, filled in parallel
     const size_t o = FB.grow((size_t)Mt * M);
     for (uint32_t m = 0; m < Mt; ++m) FB.b_bits[fb_T[m]] = std::max(FB.b_bits[fb_T[m]], std::max(z_max, 1u));
     parallel_for(Mt, 16, [&](size_t m0, size_t m1) {
@@ -858,7 +839,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   }
   // Lim-Lee combs per base class when they beat BGMW (comb.hip), over the
   // prestart's comb tables when it built them for the same classes
-  FB.plan_comb(comb_mem_cap(c), pl.fb_hit && gp ? &gp->comb_pre : nullptr);
+  FB.plan_comb(comb_mode(c), comb_mem_cap(c), pl.fb_hit && gp ? &gp->comb_pre : nullptr);
   if (pl.fb_hit && gp) pl.fb_pre.comb_ready = gp->comb_done;
   clk.lap("desc fb finalize");
   FB.pack(desc);   // FbJob offsets are positions in `desc`, i.e. relative to desc_base
@@ -880,17 +861,16 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     inv_y_nn.push_back(big_c[p] ? DI(o_rc + (size_t)p * nn * 4) : DI(o_enc + (size_t)p * nn * 4));
     inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
   }
-  for (uint32_t p = 0; p < P && !pl.ch_hit && !pl.joint; ++p) {
+  for (uint32_t p = 0; p < P && !pl.joint; ++p) {
     inv_y_nn.push_back(DX(x_J2 + ((size_t)P + p) * nn * 4));
     inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
   }
-  for (uint32_t p = 0; p < P && !pl.ch_hit && !pl.joint; ++p)
+  for (uint32_t p = 0; p < P && !pl.joint; ++p)
     if (ae_bits[p] == 0 || !alice_pre[p]) {  // c^eA does not witness c's unit-ness
       inv_y_nn.push_back(DX(x_J2 + (size_t)p * nn * 4));
       inv_m_nn.push_back(DI(o_NN + (size_t)recv_of_pair[p] * nn * 4));
       cpdl_extra.push_back(p);
     }
-  if (pl.ch_hit) cpdl_extra = gpre->ch_cpdl_extra;
   for (uint32_t p = 0; p < P; ++p) {  // zA^eA (value) then z^e_pdl (unit test)
     const uint64_t mt = DI(o_rt + (size_t)recv_of_pair[p] * nl * 4);
     inv_y_nl[p] = DX(x_J5 + ((size_t)P + p) * nl * 4);
@@ -916,21 +896,11 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
     pl.d_binv_order = put(order.data(), order.size() * 4);
     pl.d_binv_gstart = put(gstart.data(), gstart.size() * 4);
   }
-  // the fixed-base rows (J3, J4, RP): the prestart's (fx_hit) or this plan's outputs
-  const GaPre* gfx = reinterpret_cast<const GaPre*>(c->ga_pre);
-  auto J3_row = [&](size_t k) {
-    return pl.fx_hit ? (uint64_t)(uintptr_t)(gfx->fx_J3 + k * nl) : DX(x_J3 + k * nl * 4);
-  };
-  auto J4_row = [&](size_t k) {
-    return pl.fx_hit ? (uint64_t)(uintptr_t)(gfx->fx_J4 + k * nl) : DX(x_J4 + k * nl * 4);
-  };
-  // the rows of J2 / J5 and the inverses: the prestart's (ch_hit) or this plan's outputs
-  auto J2_row = [&](size_t k) {
-    return pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_J2 + k * nn) : DX(x_J2 + k * nn * 4);
-  };
-  auto J5_row = [&](size_t k) {
-    return pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_J5 + k * nl) : DX(x_J5 + k * nl * 4);
-  };
+  // the rows of the fixed-base (J3, J4) and challenge (J2, J5) outputs
+  auto J3_row = [&](size_t k) { return DX(x_J3 + k * nl * 4); };
+  auto J4_row = [&](size_t k) { return DX(x_J4 + k * nl * 4); };
+  auto J2_row = [&](size_t k) { return DX(x_J2 + k * nn * 4); };
+  auto J5_row = [&](size_t k) { return DX(x_J5 + k * nl * 4); };
   // eq_check descriptors
   clk.lap("desc fb/binom/inv");
   std::vector<EqOperand> eq_nn(P), eq_nl, eq_ck;
@@ -968,9 +938,8 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   for (uint32_t m = 0; m < Mt; ++m)
     for (uint32_t k = 0; k < M; ++k) {  // RP: T^Z_k == A_k * S^(e_k)  (mod N; the odd part here)
       EqOperand e;
-      e.a = pl.fx_hit   ? (uint64_t)(uintptr_t)(gfx->fx_RP + ((size_t)m * M + k) * nl)
-            : tz_out ? (uint64_t)(uintptr_t)(tz_out + ((size_t)m * M + k) * nl)
-                     : DX(x_RP + ((size_t)m * M + k) * nl * 4);
+      e.a = tz_out ? (uint64_t)(uintptr_t)(tz_out + ((size_t)m * M + k) * nl)
+                   : DX(x_RP + ((size_t)m * M + k) * nl * 4);
       e.b = DI(o_one);
       e.c = DI(a_off((size_t)m * M + k));
       e.d = DI(o_pS + (size_t)m * nl * 4);
@@ -1019,12 +988,11 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   std::vector<Prod3Operand> p3_nn(P), p3_nl(P);
   for (uint32_t p = 0; p < P; ++p) {
     p3_nn[p] = {DX(x_gs1 + (size_t)p * nn * 4), pl.ga_hit ? J1_at((size_t)P + p) : DX(x_J1 + ((size_t)P + p) * nn * 4),
-                pl.joint    ? DI(o_one)   // joint: b = s^N c^-e_A already
-                : pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invc + (size_t)p * nn)
-                            : DX(x_invc + (size_t)p * nn * 4),
+                pl.joint ? DI(o_one)   // joint: b = s^N c^-e_A already
+                         : DX(x_invc + (size_t)p * nn * 4),
                 nn, nn, nn, 0};
     p3_nl[p] = {J3_row((size_t)P + p), J4_row((size_t)P + p),
-                pl.ch_hit ? (uint64_t)(uintptr_t)(gpre->ch_invz + (size_t)p * nl) : DX(x_invz + (size_t)p * nl * 4),
+                DX(x_invz + (size_t)p * nl * 4),
                 nl, nl, nl, 0};
   }
   std::vector<uint32_t> p3_nl_mod;
@@ -1155,18 +1123,17 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   pl.d_p3mnl = d_p3mnl;
   pl.n_p3nl = (uint32_t)(P + K3);
   pl.d_alpre = d_alpre;
-  pl.n_inv_nn = pl.ch_hit && !pl.joint ? gpre->ch_n_inv_nn : (uint32_t)inv_y_nn.size();
-  pl.r_unn = pl.ch_hit ? (const void*)gpre->ch_unn : out_base + x_unn;
-  pl.r_uzA = pl.ch_hit ? (const void*)gpre->ch_uzA : out_base + x_uzA;
-  pl.r_uzp = pl.ch_hit ? (const void*)gpre->ch_uzp : out_base + x_uzp;
-  pl.r_pdlv = pl.ch_hit ? (const void*)gpre->ch_pdlv : out_base + x_pdlv;
-  pl.r_fel = pl.ch_hit ? (const void*)gpre->ch_fel : out_base + x_fel;
+  pl.n_inv_nn = (uint32_t)inv_y_nn.size();
+  pl.r_unn = out_base + x_unn;
+  pl.r_uzA = out_base + x_uzA;
+  pl.r_uzp = out_base + x_uzp;
+  pl.r_pdlv = out_base + x_pdlv;
+  pl.r_fel = out_base + x_fel;
   pl.n_eq_nn = (uint32_t)eq_nn.size();
   pl.n_eq_nl = (uint32_t)eq_nl.size();
   pl.n_eq_ck = (uint32_t)eq_ck.size();
   for (Sess& x : pl.ss) x.b = nullptr;   // the caller's buffers are not used after prepare
-  c->reuse_mask = (pl.ga_hit ? 1u : 0u) | (pl.fb_hit ? 2u : 0u) | (pl.ck_hit ? 4u : 0u) | (pl.tz_hit ? 8u : 0u) |
-                  (pl.ch_hit ? 16u : 0u) | (pl.fx_hit ? 32u : 0u);
+  c->reuse_mask = (pl.ga_hit ? 1u : 0u) | (pl.fb_hit ? 2u : 0u) | (pl.ck_hit ? 4u : 0u) | (pl.tz_hit ? 8u : 0u);
   c->plan = plan.release();
   return FSDKR_OK;
 }

@@ -83,12 +83,12 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
   };
   std::vector<PreRun> runs;
   size_t comb_bytes = 0, comb_desc = 0;
-  if (comb_mode() != 0 && (nl == 64 || nl == 96)) {
+  if (comb_mode(c) != 0 && (nl == 64 || nl == 96)) {
     for (const auto& r : base_runs(bbits.data(), L.h.data(), nb)) {
       double tot = 0;
       for (uint32_t b = r.first; b < r.second; ++b) tot += bcnt[b];
       const uint32_t nbr = r.second - r.first;
-      const CombParams p = comb_choose(bbits[r.first], w, L.h[r.first], comb_mode() == 2 ? 1e9 : tot / nbr, nbr,
+      const CombParams p = comb_choose(bbits[r.first], w, L.h[r.first], comb_mode(c) == 2 ? 1e9 : tot / nbr, nbr,
                                        (size_t)KD * 4, comb_mem_cap(c));
       if (!p.h) continue;
       runs.push_back(PreRun{r.first, r.second, CombJob()});
@@ -178,7 +178,6 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
     return rc;
   g.fb_table = reinterpret_cast<uint32_t*>(dev + o_tab);
   g.fb_cons = cons;
-  g.nt_rows = reinterpret_cast<const uint32_t*>(dev + o_mod);
   auto U64 = [&](size_t o) { return reinterpret_cast<const uint64_t*>(dev + o); };
   auto U32 = [&](size_t o) { return reinterpret_cast<const uint32_t*>(dev + o); };
   FbTableArgs tall{U64(o_bp), U32(o_bl), U32(o_bm), U32(o_bt), U32(o_bh), cons, g.fb_table, w, nb, 3};
@@ -301,527 +300,6 @@ static int prestart_ck(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, Ga
 }
 
 
-// The fixed-base exponents of a batch whose stage 1b packed the exponents (PDL s1, s3;
-// Alice s1, s2; ring-Pedersen Z): h1_i^s1 | h1_i^s1A (zk_pdl_with_slack.rs:144-157,
-// range_proofs.rs:129-137: the J3 slots), h2_i^s3 | h2_i^s2A (J4), T_m^Z_k
-// (ring_pedersen_proof.rs:144: RP rows), in prepare's instance order, as combs over the
-// prestarted tables (or BGMW over the chains), on the pipeline's fixed-base stream: the
-// schedules run at once, the exponents as soon as the tables exist.  Alice instances
-// run with their full exponents (prepare gives a rejected proof exponent 0; the
-// results then differ, but that proof's verdict is false either way: its w is never
-// compared).  prepare takes the rows when the exponent rows and the tables match (fx_hit).
-static int prestart_fbx(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, GaPre& g) {
-  if (!g.fb_valid || g.sess.size() != count || g.fb_bptr.size() != 2 * (size_t)g.n + g.Mt || !g.fb_table) return FSDKR_OK;
-  const uint32_t nl = g.nl, n = g.n, Mt = g.Mt, M = bs[0].m_security;
-  uint32_t s1l = 0, s3l = 0, zl = 0, P = 0;
-  for (uint32_t k = 0; k < count; ++k) {
-    const fsdkr_collect_batch* b = bs + k;
-    if (b->nl != nl || !b->pdl_s1 || !b->rp_s1 || !b->pdl_s3 || !b->rp_s2 || !b->ped_Z || !b->s1l || !b->s3l ||
-        !b->zl || b->ped_lens || b->range_lens || b->m_security != M || (k && (b->s1l != s1l || b->s3l != s3l || b->zl != zl)))
-      return FSDKR_OK;
-    s1l = b->s1l;
-    s3l = b->s3l;
-    zl = b->zl;
-    if (g.sess[k].pbase != P) return FSDKR_OK;
-    P += g.sess[k].R * g.sess[k].n;
-  }
-  const size_t rows_z = (size_t)Mt * M;
-  // host image: the exponent rows (uploaded, kept for the match)
-  auto al = Img::al;
-  const size_t o_ps1 = 0, o_as1 = al((size_t)P * s1l * 4), o_ps3 = o_as1 + al((size_t)P * s1l * 4),
-               o_as2 = o_ps3 + al((size_t)P * s3l * 4), o_z = o_as2 + al((size_t)P * s3l * 4),
-               o_rows_end = o_z + al(rows_z * zl * 4);
-  // outputs: J3 [2P], J4 [2P], RP [Mt M] rows at nl
-  const size_t o_J3 = o_rows_end, o_J4 = o_J3 + al((size_t)2 * P * nl * 4), o_RP = o_J4 + al((size_t)2 * P * nl * 4),
-               o_desc = o_RP + al(rows_z * nl * 4);
-  uint8_t* dev0 = (uint8_t*)c->buf("collect_fx_pre", o_desc);   // rows + outputs (descriptors: their own buffer)
-  uint8_t* img = c->host_buf("collect_fx_img", o_rows_end);
-  if (!dev0 || !img) {
-    c->fail("fsdkr_collect_prestart: fixed-base exponent allocation failed");
-    return FSDKR_E_OOM;
-  }
-  auto DI = [&](size_t off) { return (uint64_t)(uintptr_t)(dev0 + off); };
-  {
-    struct Cp {
-      uint8_t* dst;
-      const void* src;
-      size_t bytes;
-    };
-    std::vector<Cp> cps;
-    auto add = [&](size_t dst, const void* src, size_t bytes) {
-      constexpr size_t kChunk = 1u << 20;
-      for (size_t q = 0; q < bytes; q += kChunk)
-        cps.push_back(Cp{img + dst + q, (const uint8_t*)src + q, std::min(kChunk, bytes - q)});
-    };
-    size_t zrow = 0;
-    for (uint32_t k = 0; k < count; ++k) {
-      const fsdkr_collect_batch* b = bs + k;
-      const size_t pb = g.sess[k].pbase, cnt = (size_t)g.sess[k].R * g.sess[k].n;
-      const size_t zr = (size_t)(b->n_refresh + b->n_join) * M;
-      add(o_ps1 + pb * s1l * 4, b->pdl_s1, cnt * s1l * 4);
-      add(o_as1 + pb * s1l * 4, b->rp_s1, cnt * s1l * 4);
-      add(o_ps3 + pb * s3l * 4, b->pdl_s3, cnt * s3l * 4);
-      add(o_as2 + pb * s3l * 4, b->rp_s2, cnt * s3l * 4);
-      add(o_z + zrow * zl * 4, b->ped_Z, zr * zl * 4);
-      zrow += zr;
-    }
-    if (zrow != rows_z) return FSDKR_OK;
-    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
-      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].bytes);
-    });
-  }
-  // the job, as prepare builds it: bases [h1_i | T_m | h2_i], instances [h1 | T | h2]
-  std::vector<uint32_t> sess_of_pair(P);
-  for (uint32_t k = 0; k < count; ++k)
-    std::fill(sess_of_pair.begin() + g.sess[k].pbase, sess_of_pair.begin() + g.sess[k].pbase + g.sess[k].R * g.sess[k].n, k);
-  FbJob FX;
-  FX.k32 = nl;
-  for (uint32_t r = 0; r < n; ++r) FX.add_base(g.fb_bptr[r], nl, r);
-  for (uint32_t m = 0; m < Mt; ++m) FX.add_base(g.fb_bptr[n + m], nl, n + m);
-  for (uint32_t r = 0; r < n; ++r) FX.add_base(g.fb_bptr[n + Mt + r], nl, r);
-  for (int which = 0; which < 2; ++which)
-    for (uint32_t p = 0; p < P; ++p) {
-      const GaPre::Sess& x = g.sess[sess_of_pair[p]];
-      const uint32_t r = (uint32_t)(x.rbase + (p - x.pbase) % x.n);
-      FX.add(r, DI((which == 0 ? o_ps1 : o_as1) + (size_t)p * s1l * 4), s1l, 1,
-             DI(o_J3 + ((size_t)which * P + p) * nl * 4));
-    }
-  {
-    const size_t o = FX.grow(rows_z);
-    for (uint32_t m = 0; m < Mt; ++m)
-      for (uint32_t k = 0; k < M; ++k) {
-        const size_t i = o + (size_t)m * M + k, z = (size_t)m * M + k;
-        FX.e_ptr[i] = DI(o_z + z * zl * 4);
-        FX.e_len[i] = zl;
-        FX.e_base[i] = n + m;
-        FX.e_mod[i] = n + m;
-        FX.o_ptr[i] = DI(o_RP + z * nl * 4);
-      }
-  }
-  for (int which = 0; which < 2; ++which)
-    for (uint32_t p = 0; p < P; ++p) {
-      const GaPre::Sess& x = g.sess[sess_of_pair[p]];
-      const uint32_t r = (uint32_t)(x.rbase + (p - x.pbase) % x.n);
-      FX.add(n + Mt + r, DI((which == 0 ? o_ps3 : o_as2) + (size_t)p * s3l * 4), s3l, 1,
-             DI(o_J4 + ((size_t)which * P + p) * nl * 4));
-    }
-  // the prestart's table layout (sized by its exponent bounds)
-  for (uint32_t r = 0; r < n; ++r) {
-    FX.b_bits[r] = g.bits_h1;
-    FX.b_bits[n + Mt + r] = g.bits_h2;
-  }
-  for (uint32_t m = 0; m < Mt; ++m) FX.b_bits[n + m] = g.bits_z;
-  FX.finalize();
-  const FbLayout L = fb_layout(n, Mt, FX.w, g.bits_h1, g.bits_h2, g.bits_z);
-  bool same = FX.w == g.fb_w && L.entries == g.fb_entries;
-  for (uint32_t k = 0; k < FX.bases() && same; ++k)
-    same = FX.b_h[k] == L.h[k] && FX.b_toff[k] == L.toff[k] && FX.b_mod[k] == L.mod[k];
-  if (!same) return FSDKR_OK;
-  FX.plan_comb(comb_mem_cap(c), &g.comb_pre);
-  std::vector<uint8_t> desc;
-  FX.pack(desc);
-  const size_t o_sched = al(desc.size()), o_nst = o_sched + al(FX.sched_bytes()),
-               o_comb = o_nst + al(FX.nsteps_bytes()), dtotal = o_comb + al(FX.comb_scratch + 256);
-  uint8_t* dd = (uint8_t*)c->buf("collect_fx_desc", dtotal);
-  if (!dd) {
-    c->fail("fsdkr_collect_prestart: fixed-base exponent allocation failed");
-    return FSDKR_E_OOM;
-  }
-  hipStream_t fs = c->side_stream(1);   // launch()'s fixed-base stream
-  int rc;
-  if ((rc = c->hip_check(hipMemcpyAsync(dev0, img, o_rows_end, hipMemcpyHostToDevice, fs), "prestart fbx H2D")) ||
-      (rc = c->hip_check(hipMemcpyAsync(dd, desc.data(), desc.size(), hipMemcpyHostToDevice, fs), "prestart fbx desc")) ||
-      (rc = c->hip_check(hipStreamSynchronize(fs), "prestart fbx desc sync")))   // desc is pageable and local
-    return rc;
-  FbDev fd{dd, g.fb_table, reinterpret_cast<uint16_t*>(dd + o_sched), reinterpret_cast<uint32_t*>(dd + o_nst),
-           FX.cgroups.empty() ? nullptr : dd + o_comb};
-  FbPre pre{g.fb_table, g.fb_entries, g.fb_done, g.comb_done};
-  if ((rc = fb_launch(c, FX, fd, g.fb_cons, fs, "fb prestart", nullptr, &pre))) return rc;
-  if (!g.fx_done && (rc = c->hip_check(hipEventCreateWithFlags(&g.fx_done, hipEventDisableTiming), "event")))
-    return rc;
-  if ((rc = c->hip_check(hipEventRecord(g.fx_done, fs), "event record"))) return rc;
-  g.fx_host = img;
-  g.fx_s1l = s1l;
-  g.fx_s3l = s3l;
-  g.fx_zl = zl;
-  g.fx_ps1 = o_ps1;
-  g.fx_as1 = o_as1;
-  g.fx_ps3 = o_ps3;
-  g.fx_as2 = o_as2;
-  g.fx_z = o_z;
-  g.fx_J3 = reinterpret_cast<uint32_t*>(dev0 + o_J3);
-  g.fx_J4 = reinterpret_cast<uint32_t*>(dev0 + o_J4);
-  g.fx_RP = reinterpret_cast<uint32_t*>(dev0 + o_RP);
-  g.fx_valid = true;
-  return FSDKR_OK;
-}
-
-// do the prestarted fixed-base exponents read these sessions' exponent rows?
-// (the bases, moduli and tables are prepare's fb_cand check)
-bool fbx_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
-  const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
-  if (!g || !g->fx_valid || !g->fx_host || g->sess.size() != count) return false;
-  const uint32_t s1l = g->fx_s1l, s3l = g->fx_s3l, zl = g->fx_zl;
-  auto at = [&](size_t off) { return reinterpret_cast<const uint32_t*>(g->fx_host + off); };
-  size_t zrow = 0;
-  for (uint32_t k = 0; k < count; ++k) {
-    const fsdkr_collect_batch* b = bs + k;
-    const GaPre::Sess& x = g->sess[k];
-    const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
-    if (b->s1l != s1l || b->s3l != s3l || b->zl != zl || b->ped_lens || b->range_lens || x.n != ns ||
-        x.R != b->n_refresh || !b->pdl_s1 || !b->rp_s1 || !b->pdl_s3 || !b->rp_s2 || !b->ped_Z)
-      return false;
-    const size_t pb = x.pbase, cnt = (size_t)x.R * x.n, zr = (size_t)(b->n_refresh + b->n_join) * b->m_security;
-    if (!words_equal(at(g->fx_ps1) + pb * s1l, b->pdl_s1, cnt * s1l) ||
-        !words_equal(at(g->fx_as1) + pb * s1l, b->rp_s1, cnt * s1l) ||
-        !words_equal(at(g->fx_ps3) + pb * s3l, b->pdl_s3, cnt * s3l) ||
-        !words_equal(at(g->fx_as2) + pb * s3l, b->rp_s2, cnt * s3l) ||
-        !words_equal(at(g->fx_z) + zrow * zl, b->ped_Z, zr * zl))
-      return false;
-    zrow += zr;
-  }
-  return true;
-}
-
-
-// The challenge jobs of a batch whose stage 1c packed their fields: everything the
-// PDL / Alice / Feldman checks compute without an exponent table.
-//  - PDL challenges e = H(G, Q, c, z, u1, u2, u3) (zk_pdl_with_slack.rs:114-122) on the
-//    host threads;
-//  - J2 = c^e_pdl | c^e_A mod N_i^2 -> inverse_coop of every c^e_A (Alice's u needs the
-//    value, range_proofs.rs:140-148) and of c^e_pdl where e_A does not witness c's
-//    unit-ness (the PDL panic, zk_pdl_with_slack.rs:180);
-//  - J5 = z^e_pdl | zA^e_A mod N~_i -> the inverses of zA^e_A (Alice's w, :129-137) and
-//    the unit test of z^e_pdl;
-//  - pdl_u1 (G s1 + Q (q - e) on secp256k1), then Feldman (refresh_message.rs:147-191);
-// on their own streams beside GA, ~10 ms before prepare would start them.  The image
-// (and the rows that only the challenges read) stays in a pinned host buffer:
-// prepare compares the batch with it and takes these results on a match (ch_hit).
-static int prestart_chal(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, GaPre& g) {
-  if (g.sess.size() != count || !g.fb_valid || !g.fb_cons || !g.fb_setup || !g.nn_rows || !g.nt_rows || !g.cons)
-    return FSDKR_OK;
-  const uint32_t nl = g.nl, nn = 2 * nl;
-  uint32_t el = 0, s1l = 0, P = 0, V = 0;
-  for (uint32_t k = 0; k < count; ++k) {
-    const fsdkr_collect_batch* b = bs + k;
-    if (b->nl != nl || !b->enc || !b->pdl_z || !b->pdl_u1 || !b->pdl_u2 || !b->pdl_u3 || !b->commit || !b->rp_z ||
-        !b->rp_e || !b->pdl_s1 || !b->rp_s1 || !b->vss || !b->el || !b->s1l || b->range_lens || b->recv_avail ||
-        (k && (b->el != el || b->s1l != s1l)))
-      return FSDKR_OK;   // prepare computes them (one width per field here)
-    el = b->el;
-    s1l = b->s1l;
-    const GaPre::Sess& x = g.sess[k];
-    if (x.nl != nl || x.pbase != P) return FSDKR_OK;
-    P += x.R * x.n;
-    for (uint32_t m = 0; m < x.R; ++m) V += ncoef_of(b, m);
-  }
-  if (!P) return FSDKR_OK;
-  std::vector<uint32_t> sess_of_pair(P);
-  for (uint32_t k = 0; k < count; ++k)
-    std::fill(sess_of_pair.begin() + g.sess[k].pbase, sess_of_pair.begin() + g.sess[k].pbase + g.sess[k].R * g.sess[k].n, k);
-  auto recv_of = [&](uint32_t p) {
-    const GaPre::Sess& x = g.sess[sess_of_pair[p]];
-    return (uint32_t)(x.rbase + (p - x.pbase) % x.n);
-  };
-  // ---- host: PDL challenges, Alice pre-checks (as prepare's pair scan)
-  g.ch_epdl.assign((size_t)P * 8, 0u);
-  std::vector<uint8_t> alice_pre(P);
-  std::vector<uint32_t> ae_bits(P);
-  std::vector<uint32_t> ae_max(host_threads() + 1, 1);
-  std::atomic<uint32_t> slot{0};
-  std::atomic<bool> sha_fail{false};
-  const hbn::Limbs& q3 = q_cubed();
-  parallel_for(P, 128, [&](size_t b0, size_t b1) {
-    HostSha sha;
-    uint32_t mx = 1;
-    for (size_t p = b0; p < b1; ++p) {
-      const GaPre::Sess& x = g.sess[sess_of_pair[p]];
-      const fsdkr_collect_batch* b = bs + sess_of_pair[p];
-      const size_t lp = p - x.pbase;
-      if (!pdl_challenge(sha, b, lp, g.ch_epdl.data() + p * 8)) sha_fail = true;
-      ae_bits[p] = hbn::bitlen(b->rp_e + lp * el, el);
-      const bool s1_ok = hbn::cmp_raw(b->rp_s1 + lp * s1l, s1l, q3.data(), q3.size()) <= 0;
-      alice_pre[p] = (s1_ok && ae_bits[p] <= 256) ? 1 : 0;
-      if (alice_pre[p]) mx = std::max(mx, ae_bits[p]);
-    }
-    ae_max[slot++ % ae_max.size()] = mx;
-  });
-  if (sha_fail) {
-    c->fail("fsdkr_collect_prestart: SHA-256 (OpenSSL EVP) failed");
-    return FSDKR_E_ARG;
-  }
-  uint32_t mx_ae = 1;
-  for (uint32_t v : ae_max) mx_ae = std::max(mx_ae, v);
-  // ---- layout: [device image | rows only the host reads] in one pinned buffer
-  auto al = Img::al;
-  size_t o = 0;
-  auto take = [&](size_t bytes) {
-    const size_t at = o;
-    o = al(o + bytes);
-    return at;
-  };
-  GaPre::ChRows& R = g.ch_off;
-  R.enc = take((size_t)P * nn * 4);
-  R.pz = take((size_t)P * nl * 4);
-  R.az = take((size_t)P * nl * 4);
-  R.ae = take((size_t)P * el * 4);
-  const size_t o_ep = take((size_t)P * 32);
-  R.ps1 = take((size_t)P * s1l * 4);
-  R.Q = take((size_t)P * 64);
-  R.pu1 = take((size_t)P * 64);
-  R.vss = take((size_t)V * 64);
-  const size_t o_fi = take((size_t)P * sizeof(FeldmanInfo));
-  // descriptors: J2, J5 (2P each), inverse operand addresses (nn: <= 2P, nl: 2P)
-  ModexpJob J2, J5;
-  J2.k32 = nn;
-  J5.k32 = nl;
-  const size_t o_dJ2 = take((size_t)2 * P * 32), o_dJ5 = take((size_t)2 * P * 32);
-  const size_t o_iynn = take((size_t)2 * P * 8), o_imnn = take((size_t)2 * P * 8);
-  const size_t o_iynl = take((size_t)2 * P * 8), o_imnl = take((size_t)2 * P * 8);
-  const size_t dev_in = o;
-  // host-only rows of the match: u2, u3 (hashed), Alice s1 (pre-check), the receivers
-  R.pu2 = take((size_t)P * nn * 4);
-  R.pu3 = take((size_t)P * nl * 4);
-  R.as1 = take((size_t)P * s1l * 4);
-  R.vlen = take((size_t)count * 4 + (size_t)P * 4);
-  R.rn = take((size_t)g.n * nl * 4);
-  R.rt = take((size_t)g.n * nl * 4);
-  const size_t host_bytes = o;
-  // device outputs after the image
-  size_t od = dev_in;
-  auto out = [&](size_t bytes) {
-    const size_t at = od;
-    od = al(od + bytes);
-    return at;
-  };
-  const size_t x_J2 = out((size_t)2 * P * nn * 4), x_J5 = out((size_t)2 * P * nl * 4);
-  const size_t x_invc = out((size_t)2 * P * nn * 4), x_invz = out((size_t)P * nl * 4);
-  const size_t x_unn = out((size_t)2 * P * 4), x_uzA = out((size_t)P * 4), x_uzp = out((size_t)P * 4);
-  const size_t x_pdlv = out(P), x_fel = out(P);
-  uint8_t* dev = (uint8_t*)c->buf("collect_ch_pre", od);
-  uint8_t* img = c->host_buf("collect_ch_img", host_bytes);
-  if (!dev || !img) {
-    c->fail("fsdkr_collect_prestart: allocation of %zu device / %zu pinned bytes failed", od, host_bytes);
-    return FSDKR_E_OOM;
-  }
-  auto DI = [&](size_t off) { return (uint64_t)(uintptr_t)(dev + off); };
-  // ---- rows (per session, contiguous at the shared widths)
-  {
-    struct Cp {
-      uint8_t* dst;
-      const void* src;
-      size_t bytes;
-    };
-    std::vector<Cp> cps;
-    auto add = [&](size_t dst, const void* src, size_t bytes) {
-      constexpr size_t kChunk = 1u << 20;
-      for (size_t q = 0; q < bytes; q += kChunk)
-        cps.push_back(Cp{img + dst + q, (const uint8_t*)src + q, std::min(kChunk, bytes - q)});
-    };
-    size_t voff = 0;
-    for (uint32_t k = 0; k < count; ++k) {
-      const fsdkr_collect_batch* b = bs + k;
-      const GaPre::Sess& x = g.sess[k];
-      const size_t pb = x.pbase, cnt = (size_t)x.R * x.n;
-      uint32_t vk = 0;
-      for (uint32_t m = 0; m < x.R; ++m) vk += ncoef_of(b, m);
-      add(R.enc + pb * nn * 4, b->enc, cnt * nn * 4);
-      add(R.pz + pb * nl * 4, b->pdl_z, cnt * nl * 4);
-      add(R.az + pb * nl * 4, b->rp_z, cnt * nl * 4);
-      add(R.ae + pb * el * 4, b->rp_e, cnt * el * 4);
-      add(R.ps1 + pb * s1l * 4, b->pdl_s1, cnt * s1l * 4);
-      add(R.Q + pb * 64, b->commit, cnt * 64);
-      add(R.pu1 + pb * 64, b->pdl_u1, cnt * 64);
-      add(R.vss + voff * 64, b->vss, (size_t)vk * 64);
-      add(R.pu2 + pb * nn * 4, b->pdl_u2, cnt * nn * 4);
-      add(R.pu3 + pb * nl * 4, b->pdl_u3, cnt * nl * 4);
-      add(R.as1 + pb * s1l * 4, b->rp_s1, cnt * s1l * 4);
-      add(R.rn + x.rbase * nl * 4, b->recv_n, (size_t)x.n * nl * 4);
-      add(R.rt + x.rbase * nl * 4, b->recv_ntilde, (size_t)x.n * nl * 4);
-      voff += vk;
-    }
-    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
-      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].bytes);
-    });
-  }
-  // commitment counts (the match): [count] zeros for the regular shape, then per message
-  uint32_t* vlen = reinterpret_cast<uint32_t*>(img + R.vlen);
-  memset(vlen, 0, (size_t)count * 4 + (size_t)P * 4);
-  {
-    size_t q = count;
-    for (uint32_t k = 0; k < count; ++k) {
-      vlen[k] = bs[k].vss_len ? 1u : 0u;
-      for (uint32_t m = 0; m < bs[k].n_refresh; ++m) vlen[q++] = ncoef_of(bs + k, m);
-    }
-  }
-  memcpy(img + o_ep, g.ch_epdl.data(), (size_t)P * 32);
-  auto* finfo = reinterpret_cast<FeldmanInfo*>(img + o_fi);
-  for (uint32_t k = 0, voff = 0; k < count; ++k) {
-    const GaPre::Sess& x = g.sess[k];
-    for (uint32_t m = 0; m < x.R; ++m) {
-      const uint32_t nc = ncoef_of(bs + k, m);
-      for (uint32_t i = 0; i < x.n; ++i) finfo[x.pbase + (size_t)m * x.n + i] = {voff, nc, i + 1, 0};
-      voff += nc;
-    }
-  }
-  // J2 / J5 in prepare's instance order; inverse operands as prepare builds them
-  g.ch_cpdl_extra.clear();
-  auto* iynn = reinterpret_cast<uint64_t*>(img + o_iynn);
-  auto* imnn = reinterpret_cast<uint64_t*>(img + o_imnn);
-  auto* iynl = reinterpret_cast<uint64_t*>(img + o_iynl);
-  auto* imnl = reinterpret_cast<uint64_t*>(img + o_imnl);
-  for (int which = 0; which < 2; ++which)
-    for (uint32_t p = 0; p < P; ++p) {
-      const uint32_t r = recv_of(p);
-      const uint64_t cp = DI(R.enc + (size_t)p * nn * 4);
-      if (which == 0) {
-        J2.add(cp, nn, DI(o_ep + (size_t)p * 32), 8, 256, r);
-        J5.add(DI(R.pz + (size_t)p * nl * 4), nl, DI(o_ep + (size_t)p * 32), 8, 256, r);
-      } else {
-        J2.add(cp, nn, DI(R.ae + (size_t)p * el * 4), el, mx_ae, r);
-        J5.add(DI(R.az + (size_t)p * nl * 4), nl, DI(R.ae + (size_t)p * el * 4), alice_pre[p] ? el : 0, mx_ae, r);
-      }
-    }
-  uint32_t n_inv_nn = 0;
-  for (uint32_t p = 0; p < P; ++p) {   // Alice c^eA: the value and c's unit test
-    iynn[n_inv_nn] = DI(x_J2 + ((size_t)P + p) * nn * 4);
-    imnn[n_inv_nn++] = (uint64_t)(uintptr_t)(g.nn_rows + (size_t)recv_of(p) * nn);
-  }
-  for (uint32_t p = 0; p < P; ++p)
-    if (ae_bits[p] == 0 || !alice_pre[p]) {   // c^eA does not witness c's unit-ness: test c^e_pdl
-      iynn[n_inv_nn] = DI(x_J2 + (size_t)p * nn * 4);
-      imnn[n_inv_nn++] = (uint64_t)(uintptr_t)(g.nn_rows + (size_t)recv_of(p) * nn);
-      g.ch_cpdl_extra.push_back(p);
-    }
-  for (uint32_t p = 0; p < P; ++p) {   // zA^eA (value) then z^e_pdl (unit test)
-    const uint64_t mt = (uint64_t)(uintptr_t)(g.nt_rows + (size_t)recv_of(p) * nl);
-    iynl[p] = DI(x_J5 + ((size_t)P + p) * nl * 4);
-    imnl[p] = mt;
-    iynl[P + p] = DI(x_J5 + (size_t)p * nl * 4);
-    imnl[P + p] = mt;
-  }
-  {
-    std::vector<uint8_t> d2, d5;
-    J2.pack(d2);
-    J5.pack(d5);
-    memcpy(img + o_dJ2, d2.data(), d2.size());
-    memcpy(img + o_dJ5, d5.data(), d5.size());
-  }
-  // ---- upload on the J2 stream, then the three chains
-  hipStream_t s2 = c->side_stream(2), s5 = c->side_stream(5), s6 = c->side_stream(6);
-  int rc;
-  // an earlier prestart's chains that nobody consumed may still read the image on
-  // the other two streams: the upload waits for them
-  for (int k = 1; k < 3; ++k)
-    if (g.ch_ev[k]) (void)hipStreamWaitEvent(s2, g.ch_ev[k], 0);
-  if ((rc = c->hip_check(hipMemcpyAsync(dev, img, dev_in, hipMemcpyHostToDevice, s2), "prestart chal H2D")))
-    return rc;
-  for (hipEvent_t& e : g.ch_ev)
-    if (!e && (rc = c->hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event"))) return rc;
-  if ((rc = c->hip_check(hipEventRecord(g.ch_ev[0], s2), "event record"))) return rc;
-  (void)hipStreamWaitEvent(s5, g.ch_ev[0], 0);
-  (void)hipStreamWaitEvent(s6, g.ch_ev[0], 0);
-  // J2's constants: GA's N_i^2 rows (the KD = 144 class; a 32-lane GA set up KD = 160)
-  const uint32_t* cons_nn = g.cons;
-  if (g.wide) {
-    uint32_t* cw = nullptr;
-    StreamScope scope(c, s2);
-    if ((rc = setup_moduli(c, nn, g.nn_rows, g.n, &cw, "collect_ch_nn"))) return rc;
-    cons_nn = cw;
-  }
-  (void)hipStreamWaitEvent(s2, g.ga_setup, 0);
-  (void)hipStreamWaitEvent(s5, g.fb_setup, 0);   // N~_i constants (the table prestart's setup)
-  // FSDKR_CHAL_DEFER=1 (A/B): the two wide launches (J2, J5: ~2 900 waves) wait for the
-  // comb tables, whose short level launches otherwise find every wave slot taken
-  const bool defer = getenv("FSDKR_CHAL_DEFER") && atoi(getenv("FSDKR_CHAL_DEFER")) == 1;
-  if (defer) {
-    hipEvent_t after = g.comb_done ? g.comb_done : g.fb_done;
-    (void)hipStreamWaitEvent(s2, after, 0);
-    (void)hipStreamWaitEvent(s5, after, 0);
-  }
-  // the lanes launch() gives them: J2 at 16 lanes (one instance per wave for <= 1024
-  // chains), J5 at 8 lanes (collect_launch.cpp)
-  const uint32_t j2_group = j2_lanes(J2.size(), nn);
-  if ((rc = launch_modexp_desc(c, nn, (uint32_t)J2.size(), J2.exp_bits, dev + o_dJ2, cons_nn,
-                               reinterpret_cast<uint32_t*>(dev + x_J2), s2, "mxt_J2pre", 0, j2_group)) ||
-      (rc = launch_modexp_desc(c, nl, (uint32_t)J5.size(), J5.exp_bits, dev + o_dJ5, g.fb_cons,
-                               reinterpret_cast<uint32_t*>(dev + x_J5), s5, "mxt_J5pre", 1, 8)))
-    return rc;
-  auto U64 = [&](size_t off) { return reinterpret_cast<const uint64_t*>(dev + off); };
-  auto U32 = [&](size_t off) { return reinterpret_cast<uint32_t*>(dev + off); };
-  InverseArgs inn{U64(o_iynn), U64(o_imnn), U32(x_invc), U32(x_unn), nullptr, n_inv_nn};
-  InverseArgs inl1{U64(o_iynl), U64(o_imnl), U32(x_invz), U32(x_uzA), nullptr, P};
-  InverseArgs inl2{U64(o_iynl) + P, U64(o_imnl) + P, nullptr, U32(x_uzp), nullptr, P};
-  if ((rc = c->hip_check(launch_inverse(nn, inn, s2), "prestart inverse nn")) ||
-      (rc = c->hip_check(launch_inverse(nl, inl1, s5), "prestart inverse nl")) ||
-      (rc = c->hip_check(launch_inverse(nl, inl2, s5), "prestart inverse nl 2")))
-    return rc;
-  PdlU1Args u{U32(R.ps1), U32(o_ep), U32(R.Q), U32(R.pu1), s1l, dev + x_pdlv, P};
-  FeldmanArgs f{U32(R.vss), U32(R.Q), reinterpret_cast<const FeldmanInfo*>(dev + o_fi), dev + x_fel, P, 3};
-  if ((rc = c->hip_check(launch_pdl_u1(u, s6), "prestart pdl_u1")) ||
-      (rc = c->hip_check(launch_feldman(f, s6), "prestart feldman")))
-    return rc;
-  if ((rc = c->hip_check(hipEventRecord(g.ch_ev[0], s2), "event record")) ||
-      (rc = c->hip_check(hipEventRecord(g.ch_ev[1], s5), "event record")) ||
-      (rc = c->hip_check(hipEventRecord(g.ch_ev[2], s6), "event record")))
-    return rc;
-  g.ch_host = img;
-  g.ch_P = P;
-  g.ch_V = V;
-  g.ch_el = el;
-  g.ch_s1l = s1l;
-  g.ch_n_inv_nn = n_inv_nn;
-  g.ch_J2 = U32(x_J2);
-  g.ch_J5 = U32(x_J5);
-  g.ch_invc = U32(x_invc);
-  g.ch_invz = U32(x_invz);
-  g.ch_unn = U32(x_unn);
-  g.ch_uzA = U32(x_uzA);
-  g.ch_uzp = U32(x_uzp);
-  g.ch_pdlv = dev + x_pdlv;
-  g.ch_fel = dev + x_fel;
-  g.ch_valid = true;
-  return FSDKR_OK;
-}
-
-// do the prestarted challenge jobs belong to these sessions (every row they read equal)?
-bool chal_pre_matches(const Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
-  const GaPre* g = reinterpret_cast<const GaPre*>(c->ga_pre);
-  if (!g || !g->ch_valid || !g->ch_host || g->sess.size() != count) return false;
-  const uint32_t nl = g->nl, nn = 2 * nl, el = g->ch_el, s1l = g->ch_s1l;
-  const GaPre::ChRows& R = g->ch_off;
-  auto at = [&](size_t off) { return reinterpret_cast<const uint32_t*>(g->ch_host + off); };
-  const uint32_t* vlen = at(R.vlen);
-  size_t voff = 0, q = count;
-  for (uint32_t k = 0; k < count; ++k) {
-    const fsdkr_collect_batch* b = bs + k;
-    const GaPre::Sess& x = g->sess[k];
-    const uint32_t ns = b->n_recv ? b->n_recv : b->n_refresh + b->n_join;
-    if (b->nl != nl || b->el != el || b->s1l != s1l || x.n != ns || x.R != b->n_refresh || b->range_lens ||
-        b->recv_avail || !b->enc || !b->pdl_z || !b->pdl_u1 || !b->pdl_u2 || !b->pdl_u3 || !b->commit || !b->rp_z ||
-        !b->rp_e || !b->pdl_s1 || !b->rp_s1 || !b->vss || vlen[k] != (b->vss_len ? 1u : 0u) || b->neg_bits)
-      return false;   // (negative z: prepare's J5 takes residue rows)
-    uint32_t vk = 0;
-    for (uint32_t m = 0; m < x.R; ++m, ++q) {
-      if (vlen[q] != ncoef_of(b, m)) return false;
-      vk += vlen[q];
-    }
-    const size_t pb = x.pbase, cnt = (size_t)x.R * x.n;
-    if (!words_equal(at(R.enc) + pb * nn, b->enc, cnt * nn) || !words_equal(at(R.pz) + pb * nl, b->pdl_z, cnt * nl) ||
-        !words_equal(at(R.az) + pb * nl, b->rp_z, cnt * nl) || !words_equal(at(R.ae) + pb * el, b->rp_e, cnt * el) ||
-        !words_equal(at(R.ps1) + pb * s1l, b->pdl_s1, cnt * s1l) || !words_equal(at(R.Q) + pb * 16, b->commit, cnt * 16) ||
-        !words_equal(at(R.pu1) + pb * 16, b->pdl_u1, cnt * 16) || !words_equal(at(R.vss) + voff * 16, b->vss, (size_t)vk * 16) ||
-        !words_equal(at(R.pu2) + pb * nn, b->pdl_u2, cnt * nn) || !words_equal(at(R.pu3) + pb * nl, b->pdl_u3, cnt * nl) ||
-        !words_equal(at(R.as1) + pb * s1l, b->rp_s1, cnt * s1l) ||
-        !words_equal(at(R.rn) + x.rbase * nl, b->recv_n, (size_t)x.n * nl) ||
-        !words_equal(at(R.rt) + x.rbase * nl, b->recv_ntilde, (size_t)x.n * nl))
-      return false;
-    voff += vk;
-  }
-  return true;
-}
-
-
 // GA prestart of `count` sessions (one: fsdkr_collect_prestart; many:
 // fsdkr_collect_prestart_multi), in prepare's global order: session s's
 // receivers and pairs after session s-1's, every row at the widest nl.
@@ -831,16 +309,13 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // an earlier prestart's work that no prepare consumed (a changed batch) may still
   // run and read the buffers this one overwrites: wait for it (a consumed prestart
   // finished before the pipeline that waited on it)
-  for (hipEvent_t e : {g.done, g.fb_done, g.comb_done, g.ck_done, g.tz_done, g.ch_ev[0], g.ch_ev[1], g.ch_ev[2], g.fx_done})
+  for (hipEvent_t e : {g.done, g.fb_done, g.comb_done, g.ck_done, g.tz_done})
     if (e) (void)hipEventSynchronize(e);
   g.valid = false;
   g.fb_valid = false;
   g.comb_pre.clear();
   g.ck_valid = false;
   g.tz_valid = false;
-  g.ch_valid = false;
-  g.fx_valid = false;
-  g.nn_rows = g.nt_rows = nullptr;
   *n_out = *P_out = 0;
   const CollectPlan* running = reinterpret_cast<const CollectPlan*>(c->plan);
   if (running && running->launched) {
@@ -850,8 +325,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // a prepared plan that consumed the previous prestart reads its s^N rows and
   // fixed-base tables in place: this prestart overwrites (or reallocates) those
   // buffers, so the plan is dropped (a later launch reports "no prepared batch")
-  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit || running->ch_hit ||
-                  running->fx_hit))
+  if (running && (running->ga_hit || running->fb_hit || running->ck_hit || running->tz_hit))
     free_collect_plan(c);
   if (!bs || count == 0) {
     c->fail("fsdkr_collect_prestart: no batch");
@@ -1004,7 +478,6 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
     return rc;
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
   g.cons = cons;
-  g.nn_rows = reinterpret_cast<const uint32_t*>(dev + o_NN);
   g.wide = group == kWideGroup;
   if (!g.ga_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_setup, hipEventDisableTiming), "event")))
     return rc;
@@ -1056,34 +529,31 @@ int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count)
   }
   GaPre& g = *gp;
   if (!g.fb_valid && (rc = prestart_fb_tables(c, bs, count, g, n, P))) return rc;
-  // FSDKR_FBX=1: also start the fixed-base exponents behind the tables (off by default:
-  // no gain at n = 64, interleaved A/B profiles/r05/r05c_ab_*; read per call)
-  const char* fbx_env = getenv("FSDKR_FBX");
-  if (!g.fx_valid && fbx_env && atoi(fbx_env) == 1 && (rc = prestart_fbx(c, bs, count, g))) return rc;
-  if (!g.ck_valid && (rc = prestart_ck(c, bs, count, g))) return rc;
-  return g.ch_valid ? FSDKR_OK : prestart_chal(c, bs, count, g);
+  return g.ck_valid ? FSDKR_OK : prestart_ck(c, bs, count, g);
 }
 
-uint64_t rows_digest(const uint32_t* p, size_t rows, uint32_t w, uint64_t row0) {
-  const size_t chunks = std::max<size_t>(1, std::min<size_t>(host_threads(), rows / 4096 + 1));
-  std::vector<uint64_t> part(chunks, 0);
-  parallel_for(chunks, 1, [&](size_t c0, size_t c1) {
-    for (size_t ch = c0; ch < c1; ++ch) {
-      uint64_t acc = 0;
-      for (size_t r = rows * ch / chunks; r < rows * (ch + 1) / chunks; ++r) {
-        const uint32_t* x = p + r * w;
-        int top = (int)w - 1;
-        while (top >= 0 && x[top] == 0) --top;
-        uint64_t h = 0x9E3779B97F4A7C15ull ^ (row0 + r);
-        for (int k = 0; k <= top; ++k) h = (h ^ x[k]) * 0x100000001B3ull + (h >> 29);
-        acc += h * (2 * (row0 + r) + 1);
+std::vector<RowsSha> rows_sha256(size_t rows, const std::function<std::pair<const uint32_t*, uint32_t>(size_t)>& row) {
+  const size_t blocks = (rows + kShaRows - 1) / kShaRows;
+  std::vector<RowsSha> out(blocks);
+  std::atomic<bool> ok{true};
+  parallel_for(blocks, 1, [&](size_t b0, size_t b1) {
+    EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+    for (size_t bl = b0; bl < b1 && ctx; ++bl) {
+      bool good = EVP_DigestInit_ex(ctx, sha256_md(), nullptr) == 1;
+      for (size_t r = bl * kShaRows; r < std::min(rows, (bl + 1) * kShaRows) && good; ++r) {
+        const std::pair<const uint32_t*, uint32_t> x = row(r);
+        uint32_t top = x.second;
+        while (top && x.first[top - 1] == 0) --top;
+        good = EVP_DigestUpdate(ctx, &top, 4) == 1 && (!top || EVP_DigestUpdate(ctx, x.first, (size_t)top * 4) == 1);
       }
-      part[ch] = acc;
+      unsigned int len = 0;
+      if (!good || EVP_DigestFinal_ex(ctx, out[bl].data(), &len) != 1 || len != 32) ok = false;
     }
+    if (!ctx) ok = false;
+    EVP_MD_CTX_free(ctx);
   });
-  uint64_t d = 0;
-  for (uint64_t v : part) d += v;
-  return d;
+  if (!ok) out.clear();   // no digest: never equal to a prestart's (callers recompute)
+  return out;
 }
 
 // fsdkr_collect_prestart_rp: every message's ring-Pedersen T^Z_k (ring_pedersen_proof.rs:144)
@@ -1133,8 +603,8 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
   // w squarings: P_m = entry m pstep) takes ~30 % fewer products than BGMW
   // (3072-bit: ~400 instead of ~575 per exponent, comb.hip)
   CombParams cp;
-  if (comb_mode() != 0)
-    cp = comb_choose(g.bits_z, g.fb_w, TZ.b_h[n], comb_mode() == 2 ? 1e9 : (double)M, Mt,
+  if (comb_mode(c) != 0)
+    cp = comb_choose(g.bits_z, g.fb_w, TZ.b_h[n], comb_mode(c) == 2 ? 1e9 : (double)M, Mt,
                      (size_t)shape_digits(nl) * 4, comb_mem_cap(c));
   CombJob CJ;
   if (cp.h) CJ.init(cp, nl, Mt, (uint32_t)rows);
@@ -1194,8 +664,10 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
   hipStream_t zs = c->side_stream(10);
   StreamScope scope(c, zs);
   int rc;
-  // Z rows: H2D per session (contiguous when the sessions' rows are), then the digest
-  uint64_t digest = 0;
+  // Z rows: H2D per session (contiguous when the sessions' rows are); prepare reuses
+  // the results only for rows equal to these (SHA-256 per block of rows, below)
+  std::vector<std::pair<const uint32_t*, uint32_t>> zsess(count);
+  std::vector<size_t> zrow0(count + 1, 0);
   size_t row = 0;
   for (uint32_t k = 0; k < count; ++k) {
     const fsdkr_collect_batch* b = bs + k;
@@ -1216,8 +688,9 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
           (rc = c->hip_check(hipStreamSynchronize(zs), "prestart rp Z sync")))
         return rc;
     }
-    digest += rows_digest(b->ped_Z, r, b->zl, row);
+    zsess[k] = {b->ped_Z, b->zl};
     row += r;
+    zrow0[k + 1] = row;
   }
   if (!fits) return c->hip_check(hipStreamSynchronize(zs), "prestart rp sync");   // prepare sizes its own tables
   if ((rc = c->hip_check(hipMemcpyAsync(dev + o_desc, desc.data(), desc.size(), hipMemcpyHostToDevice, zs),
@@ -1251,8 +724,11 @@ int collect_prestart_rp_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t cou
   g.tz_zl = zl;
   g.tz_Mt = Mt;
   g.tz_M = M;
-  g.tz_digest = digest;
-  g.tz_valid = true;
+  g.tz_sha = rows_sha256(row, [&](size_t r) {
+    const size_t k = (size_t)(std::upper_bound(zrow0.begin(), zrow0.end(), r) - zrow0.begin()) - 1;
+    return std::make_pair(zsess[k].first + (r - zrow0[k]) * zsess[k].second, zsess[k].second);
+  });
+  g.tz_valid = !g.tz_sha.empty();
   return FSDKR_OK;
 }
 

@@ -236,22 +236,11 @@ hipError_t launch_comb_exp(uint32_t k32, CombExpArgs& a, int group, hipStream_t 
   if (a.ngroups == 0 || a.ngroups > (uint32_t)kCombGroups) return hipErrorInvalidValue;
   for (uint32_t k = 0; k < a.ngroups; ++k)
     if (!a.g[k].steps) return hipErrorInvalidValue;
-  // quotient-scaled rows by default (no v_mul_lo_u32 per row); FSDKR_COMB_QS=0: plain (A/B)
-  static int qs_env = -1;
-  if (qs_env < 0) {
-    const char* e = getenv("FSDKR_COMB_QS");
-    qs_env = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (qs_env) {
-    switch (k32) {
-      case 64: return group == 8 ? exp_launch<72, 8, 64, true>(a, st) : exp_launch<72, 4, 64, true>(a, st);
-      case 96: return exp_launch<108, 4, 96, true>(a, st);
-      default: return hipErrorInvalidValue;
-    }
-  }
+  // quotient-scaled rows (no v_mul_lo_u32 per row: -0.9 % kernel time against the
+  // plain rows, profiles/r05/r05cqs_ab/)
   switch (k32) {
-    case 64: return group == 8 ? exp_launch<72, 8, 64, false>(a, st) : exp_launch<72, 4, 64, false>(a, st);
-    case 96: return exp_launch<108, 4, 96, false>(a, st);
+    case 64: return group == 8 ? exp_launch<72, 8, 64, true>(a, st) : exp_launch<72, 4, 64, true>(a, st);
+    case 96: return exp_launch<108, 4, 96, true>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

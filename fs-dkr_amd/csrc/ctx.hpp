@@ -30,6 +30,7 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool timing = false;
+  uint32_t flags = 0;   // fsdkr_cfg flags (FSDKR_CFG_*)
   std::string err;
   std::map<std::string, DevBuf> bufs;
   std::map<std::string, TimeAcc> times;

@@ -78,7 +78,7 @@ struct FbJob {
   // plan the comb groups (reorders the instances by group); false: BGMW.  pre:
   // tables built ahead for these bases (a group with the same bases and
   // parameters takes them)
-  bool plan_comb(size_t cap, const std::vector<CombPre>* pre = nullptr);
+  bool plan_comb(int mode, size_t cap, const std::vector<CombPre>* pre = nullptr);
 
   uint32_t add_base(uint64_t ptr, uint32_t len, uint32_t mod) {
     b_ptr.push_back(ptr);
@@ -219,9 +219,11 @@ int comb_build_launch(Ctx* c, const CombJob& j, const CombDev& d, const uint32_t
                       hipStream_t st);
 // device bytes the comb tables may take (a fraction of the free memory)
 size_t comb_mem_cap(Ctx* c);
-// FSDKR_FB_COMB: 0 = BGMW only, 2 = the comb whenever it is possible, else
-// (default, 1) the comb where comb_choose finds it cheaper
-int comb_mode();
+// the context's fixed-base engine: 0 = BGMW only (FSDKR_CFG_FB_BGMW), 2 = the comb
+// whenever it is possible (FSDKR_CFG_FB_COMB), else (default, 1) the comb where
+// comb_choose finds it cheaper
+struct Ctx;
+int comb_mode(const Ctx* c);
 // upload + launch + wait (stand-alone callers)
 int fb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag);
 

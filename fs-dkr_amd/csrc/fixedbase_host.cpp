@@ -215,10 +215,9 @@ static int comb_path(Ctx* c, const FbJob& j, const FbDev& d, const uint32_t* con
   return comb_exp_launch(c, jobs.data(), devs.data(), (uint32_t)ng, consts, st, tag);
 }
 
-bool FbJob::plan_comb(size_t cap, const std::vector<CombPre>* pre) {
+bool FbJob::plan_comb(int mode, size_t cap, const std::vector<CombPre>* pre) {
   cgroups.clear();
   comb_scratch = 0;
-  const int mode = comb_mode();
   if (mode == 0 || (k32 != 64 && k32 != 96) || count() == 0) return false;
   // groups: runs of consecutive bases with one exponent bound (hence one chain height)
   std::vector<uint32_t> gid(bases());
@@ -282,15 +281,16 @@ bool FbJob::plan_comb(size_t cap, const std::vector<CombPre>* pre) {
   return true;
 }
 
-int comb_mode() {
-  const char* e = getenv("FSDKR_FB_COMB");
-  return e ? atoi(e) : 1;
+int comb_mode(const Ctx* c) {
+  return (c->flags & FSDKR_CFG_FB_BGMW) ? 0 : (c->flags & FSDKR_CFG_FB_COMB) ? 2 : 1;
 }
+
+bool batch_inv_on(const Ctx* c) { return !(c->flags & FSDKR_CFG_INV_EACH); }
 
 // Stand-alone fixed-base job as a comb: the chains P_m = b^(2^(m b)) (fb_table
 // with window b, h v entries per base), then comb_launch.  false: not taken.
 static bool comb_run(Ctx* c, FbJob& j, const uint32_t* consts, const char* tag, int* rc_out) {
-  const int mode = comb_mode();
+  const int mode = comb_mode(c);
   if (mode == 0 || (j.k32 != 64 && j.k32 != 96)) return false;
   uint32_t bits = 1;
   for (uint32_t b : j.b_bits) bits = std::max(bits, b);

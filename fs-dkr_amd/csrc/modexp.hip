@@ -773,14 +773,8 @@ hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_
 // G = 4 (L = 18: no in-cycle normalisation, profiles/r01_modexp_group_sweep_*),
 // 4096-bit G = 4 (L = 36; with squaring rows it edges out L = 18 by 4%,
 // profiles/r02h_modexp_sqr.jsonl).  G = 2 (2048-bit) only when forced.
-// ModexpArgs.group or FSDKR_MODEXP_G=<G> force a group size (tuning, tests).
-static int pick_group(uint32_t count, int forced_arg, std::initializer_list<int> allowed, int min_auto) {
-  static int forced_env = -1;
-  if (forced_env < 0) {
-    const char* e = getenv("FSDKR_MODEXP_G");
-    forced_env = e ? atoi(e) : 0;
-  }
-  const int forced = forced_arg ? forced_arg : forced_env;
+// ModexpArgs.group (fsdkr_ctx_set_modexp_group) forces a group size (tuning, tests).
+static int pick_group(uint32_t count, int forced, std::initializer_list<int> allowed, int min_auto) {
   for (int g : allowed)
     if (g == forced) return g;
   constexpr uint64_t kLaneCapacity = 256ull * 4 * 3 * 64;   // CUs x SIMDs x resident waves x lanes
@@ -802,45 +796,32 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
       default: return hipErrorInvalidValue;
     }
   }
-  // the short-lane group shapes (8-32 lanes) run quotient-scaled chains
-  // (modexp_kernel QS); FSDKR_QS=0 selects the plain rows (A/B)
-  static int qs_env = -1;
-  if (qs_env < 0) {
-    const char* e = getenv("FSDKR_QS");
-    qs_env = (e && e[0] == '0') ? 0 : 1;
-  }
-  const bool qs = qs_env == 1;
-  // the 4-lane throughput shapes run quotient-scaled rows too (no v_mul_lo_u32
-  // per row: metric 2 -1.5 % keyed, -0.9 % per-instance exponents, interleaved,
-  // profiles/r05/r05qs4_*); FSDKR_QS4=0 keeps them plain (A/B)
-  static int qs4_env = -1;
-  if (qs4_env < 0) {
-    const char* e = getenv("FSDKR_QS4");
-    qs4_env = (e && e[0] == '0') ? 0 : 1;
-  }
-  const bool qs4 = qs && qs4_env == 1;
+  // public exponents run quotient-scaled chains (modexp_kernel QS: no quotient
+  // multiply per row) at every group shape: 8-32 lanes since round 4, the 4-lane
+  // throughput shapes since round 5 (metric 2 -1.5 % keyed, -0.9 % per-instance
+  // exponents, interleaved, profiles/r05/r05qs4_*)
   if (a.slide) {   // shared exponent per wave: the 4096-bit shapes of GA
     if (k32 != 128 || a.ct || a.group == kWaveGroup) return hipErrorInvalidValue;
     if (a.group == kWideGroup) {   // 32 lanes (KD = 160 constants, the caller's): small launches
       if (a.lo_bit && a.tail)
-        return qs ? launch_modexp_tail<160, 32, 128, true>(a, st) : launch_modexp_tail<160, 32, 128, false>(a, st);
-      return qs ? launch_modexp_slide<160, 32, 128, true>(a, st) : launch_modexp_slide<160, 32, 128, false>(a, st);
+        return launch_modexp_tail<160, 32, 128, true>(a, st);
+      return launch_modexp_slide<160, 32, 128, true>(a, st);
     }
     if (a.lo_bit) {   // split chains: head and tail at the caller's lanes, QS as the full chain's
       switch (a.group) {
-        case 16: return a.tail ? (qs ? launch_modexp_tail<144, 16, 128, true>(a, st) : launch_modexp_tail<144, 16, 128, false>(a, st))
-                               : (qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st));
-        case 8: return a.tail ? (qs ? launch_modexp_tail<144, 8, 128, true>(a, st) : launch_modexp_tail<144, 8, 128, false>(a, st))
-                              : (qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st));
-        case 4: return a.tail ? (qs4 ? launch_modexp_tail<144, 4, 128, true>(a, st) : launch_modexp_tail<144, 4, 128, false>(a, st))
-                              : (qs4 ? launch_modexp_slide<144, 4, 128, true>(a, st) : launch_modexp_slide<144, 4, 128, false>(a, st));
+        case 16: return a.tail ? launch_modexp_tail<144, 16, 128, true>(a, st)
+                               : launch_modexp_slide<144, 16, 128, true>(a, st);
+        case 8: return a.tail ? launch_modexp_tail<144, 8, 128, true>(a, st)
+                              : launch_modexp_slide<144, 8, 128, true>(a, st);
+        case 4: return a.tail ? launch_modexp_tail<144, 4, 128, true>(a, st)
+                              : launch_modexp_slide<144, 4, 128, true>(a, st);
         default: return hipErrorInvalidValue;
       }
     }
     switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
-      case 16: return qs ? launch_modexp_slide<144, 16, 128, true>(a, st) : launch_modexp_slide<144, 16, 128, false>(a, st);
-      case 8: return qs ? launch_modexp_slide<144, 8, 128, true>(a, st) : launch_modexp_slide<144, 8, 128, false>(a, st);
-      default: return qs4 ? launch_modexp_slide<144, 4, 128, true>(a, st) : launch_modexp_slide<144, 4, 128, false>(a, st);
+      case 16: return launch_modexp_slide<144, 16, 128, true>(a, st);
+      case 8: return launch_modexp_slide<144, 8, 128, true>(a, st);
+      default: return launch_modexp_slide<144, 4, 128, true>(a, st);
     }
   }
   switch (k32) {
@@ -849,27 +830,27 @@ hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st) {
                                                               : launch_modexp<36, 4, 32>(a, st);
     case 64:
       switch (pick_group(a.count, (int)a.group, {2, 4, 8}, 4)) {
-        case 8: return qs ? launch_modexp<72, 8, 64, false, true>(a, st) : launch_modexp<72, 8, 64>(a, st);
-        case 4: return qs4 ? launch_modexp<72, 4, 64, false, true>(a, st) : launch_modexp<72, 4, 64>(a, st);
+        case 8: return launch_modexp<72, 8, 64, false, true>(a, st);
+        case 4: return launch_modexp<72, 4, 64, false, true>(a, st);
         default: return launch_modexp<72, 2, 64>(a, st);
       }
-    case 96: return qs4 ? launch_modexp<108, 4, 96, false, true>(a, st) : launch_modexp<108, 4, 96>(a, st);
+    case 96: return launch_modexp<108, 4, 96, false, true>(a, st);
     case 128:
       // 32 lanes only on explicit request: it needs KD = 160 constants (mod_setup_g)
       if (a.group == kWideGroup)
-        return qs ? launch_modexp<160, 32, 128, false, true>(a, st) : launch_modexp<160, 32, 128>(a, st);
+        return launch_modexp<160, 32, 128, false, true>(a, st);
       if (a.group == kWaveGroup) return launch_modexp_wave<144, 3, 128>(a, st);
       // a launch past the resident-lane capacity: 4 lanes (L = 36, squaring rows
       // with 19 + 36 MACs per row) beat 8 (L = 18) by 4% (profiles/r02h_modexp_sqr.jsonl)
       switch (pick_group(a.count, (int)a.group, {4, 8, 16}, 4)) {
-        case 16: return qs ? launch_modexp<144, 16, 128, false, true>(a, st) : launch_modexp<144, 16, 128>(a, st);
-        case 8: return qs ? launch_modexp<144, 8, 128, false, true>(a, st) : launch_modexp<144, 8, 128>(a, st);
-        default: return qs4 ? launch_modexp<144, 4, 128, false, true>(a, st) : launch_modexp<144, 4, 128>(a, st);
+        case 16: return launch_modexp<144, 16, 128, false, true>(a, st);
+        case 8: return launch_modexp<144, 8, 128, false, true>(a, st);
+        default: return launch_modexp<144, 4, 128, false, true>(a, st);
       }
     case 192:
       if (pick_group(a.count, (int)a.group, {4, 8}, 4) == 8)
-        return qs ? launch_modexp<216, 8, 192, false, true>(a, st) : launch_modexp<216, 8, 192>(a, st);
-      return qs4 ? launch_modexp<216, 4, 192, false, true>(a, st) : launch_modexp<216, 4, 192>(a, st);
+        return launch_modexp<216, 8, 192, false, true>(a, st);
+      return launch_modexp<216, 4, 192, false, true>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

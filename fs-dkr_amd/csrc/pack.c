@@ -314,12 +314,8 @@ static void run_work(Work* w, int threads) {
   if (threads > 64) threads = 64;
   /* a worker per >= 4 chunks of 512 values (thread start ~ tens of us): n = 64
    * whole call 45.9 -> 44.5 ms against one per 16 chunks, interleaved A/B
-   * (profiles/r05/r05q_ab_pack_chunks); FSDKR_PACK_CHUNKS overrides the 4 */
-  static int per = 0;
-  if (!per) {
-    const char* e = getenv("FSDKR_PACK_CHUNKS");
-    per = (e && atoi(e) > 0) ? atoi(e) : 4;
-  }
+   * (profiles/r05/r05q_ab_pack_chunks) */
+  const int per = 4;
   if ((size_t)threads > w->n / ((size_t)per * CHUNK) + 1) threads = (int)(w->n / ((size_t)per * CHUNK) + 1);
   pthread_t tid[64];
   int started = 0;

@@ -154,12 +154,10 @@ hipError_t launch_inverse(uint32_t k32, const InverseArgs& a, hipStream_t st);
 hipError_t launch_inverse_coop(uint32_t k32, const InverseArgs& a, hipStream_t st);
 hipError_t launch_inverse_batch(uint32_t k32, const BatchInverseArgs& a, hipStream_t st);
 // Montgomery's simultaneous inversion where instances share a modulus (one
-// binary-GCD inverse per modulus instead of one per instance); FSDKR_BATCH_INV=0:
-// one inverse each (A/B).  Read per call.
-inline bool batch_inv_on() {
-  const char* e = getenv("FSDKR_BATCH_INV");
-  return !(e && atoi(e) == 0);
-}
+// binary-GCD inverse per modulus instead of one per instance); FSDKR_CFG_INV_EACH:
+// one inverse each (tests, A/B)
+struct Ctx;
+bool batch_inv_on(const Ctx* c);
 size_t inverse_batch_scratch_words(uint32_t k32);
 hipError_t launch_eq_check(uint32_t k32, const EqCheckArgs& a, hipStream_t st);
 hipError_t launch_prod3(uint32_t k32, const Prod3Args& a, hipStream_t st);

@@ -17,6 +17,10 @@ FSDKR_E_HIP = -2
 FSDKR_E_OOM = -3
 FSDKR_E_UNSUPPORTED = -4
 FSDKR_CFG_TIMING = 1
+# algorithm switches (parity tests, A/B runs; results identical under each)
+FSDKR_CFG_FB_BGMW = 2    # fixed-base exponentiations by BGMW windows only
+FSDKR_CFG_FB_COMB = 4    # a Lim-Lee comb wherever one fits
+FSDKR_CFG_INV_EACH = 8   # one inverse per element (no simultaneous inversion)
 
 u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -181,6 +185,8 @@ def lib():
     L.fsdkr_ctx_set_cu_split.argtypes = [vp, ctypes.c_uint32]
     L.fsdkr_ctx_set_cu_split.restype = ctypes.c_int
     L.fsdkr_ctx_set_timing.restype = ctypes.c_int
+    L.fsdkr_ctx_set_flags.argtypes = [vp, ctypes.c_uint32]
+    L.fsdkr_ctx_set_flags.restype = ctypes.c_int
     L.fsdkr_mod_inverse.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p, u32p]
     L.fsdkr_mod_inverse.restype = ctypes.c_int
     L.fsdkr_miller_rabin.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u32p]
@@ -234,6 +240,7 @@ class Context:
             raise FsdkrError(rc, "fsdkr_ctx_create failed (no HIP device?)")
         self._h = h
         self._lib = L
+        self._flags = cfg.flags
 
     @property
     def handle(self):
@@ -326,6 +333,18 @@ class Context:
     def set_timing(self, on):
         """Per-kernel HIP-event timing on/off (kernel_time needs it on)."""
         self.check(self._lib.fsdkr_ctx_set_timing(self._h, 1 if on else 0))
+        self._flags = (self._flags | FSDKR_CFG_TIMING) if on else (self._flags & ~FSDKR_CFG_TIMING)
+
+    def set_flags(self, flags):
+        """Replace the fsdkr_cfg flags (FSDKR_CFG_*); returns the previous ones."""
+        old = self._flags
+        self.check(self._lib.fsdkr_ctx_set_flags(self._h, flags))
+        self._flags = flags
+        return old
+
+    @property
+    def flags(self):
+        return self._flags
 
     def mod_inverse(self, ys, ms, mod_limbs):
         """[(y^-1 mod m or None)] on the GPU (None where gcd(y, m) != 1)."""
@@ -402,7 +421,7 @@ class Context:
         device work -> the pipeline's last kernel), -1 before any."""
         return float(self._lib.fsdkr_collect_last_span_ms(self._h))
 
-    REUSE = {"ga": 1, "tables": 2, "ck": 4, "tz": 8, "chal": 16, "fx": 32}
+    REUSE = {"ga": 1, "tables": 2, "ck": 4, "tz": 8}
 
     def collect_reuse(self):
         """Names of the prestarted parts the last prepare reused (fsdkr_collect_reuse_mask)."""

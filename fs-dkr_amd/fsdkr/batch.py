@@ -366,7 +366,7 @@ class CollectBatch:
         M = m_security
         G = _Gather()
         k = self._k
-        self._ga, self._pending, self._stage1b, self._stage1c = None, None, None, False
+        self._ga, self._pending, self._stage1b = None, None, None
         self.negs = _Negatives()
         if self.header_only:
             f_ckn = G.field([m.ek.n for m in all_m] or [0])
@@ -424,7 +424,6 @@ class CollectBatch:
             # whole call 0.5-1.2 ms shorter, profiles/r04/r04g_*, r04h_*)
             names = ("recv_n", "pdl_s2", "rp_s") + (() if split_stage1 else _STAGE1B)
             self._stage1b = _STAGE1B if split_stage1 else None
-            self._stage1c = split_stage1
             ga = {name: Gs.slot(F[name], _STAGE1_WIDTH.get(name, lambda c_: nl_ga)(c)) for name in names}
             # the correct-key job (sigma^n mod n) reads only ek.n and sigma: stage 1
             # packs them at the width complete() gives them, so the prestart runs
@@ -553,8 +552,7 @@ class CollectBatch:
         if st["ck_short"]:
             c.ck_lens = k(np.array([len(x) for x in st["sig"]], dtype=np.uint32))
         G.run()
-        if "commit" not in ga_arrs:   # (stage1c packed the points already)
-            self._points(st)
+        self._points(st)
         if self.negs:
             self.negs.decide(msgs, joins, n, st["avail"], st["pdl"], st["rng"], st["sts"])
             for arr, attr in ((self.negs.s3, "pdl_s3_neg"), (self.negs.z, "neg_bits"), (self.negs.a, "ped_a_neg")):
@@ -566,7 +564,7 @@ class CollectBatch:
 
     def _late(self, st):
         """The gathers of the challenge jobs' fields (PDL transcript, Alice c / z / e,
-        DLog proofs): from stage1c() or complete(), once."""
+        DLog proofs): from complete(), once."""
         if st.get("late"):
             return
         st["late"] = True
@@ -595,47 +593,6 @@ class CollectBatch:
         if any(len(x) != st["t"] + 1 for x in com):   # Horner over each message's own vector
             c.vss_len = k(np.array([len(x) for x in com], dtype=np.uint32))
         c.vss = k(pack_points([p for x in com for p in x] or [None]))
-
-    def stage1c(self):
-        """After stage1b(): the fields of the jobs that read no exponent table -- the
-        PDL transcript (c, z, u1, u2, u3, Q), Alice c / z / e, the Feldman
-        commitments, ek.n with sigma_vec and the joins' DLog proofs -- at the width
-        complete() gives them, for a third fsdkr_collect_prestart call: the PDL
-        challenges are hashed on the host and c^e, z^e (their inverses and unit
-        flags), pdl_u1, Feldman, the correct-key and DLog exponentiations start
-        beside GA instead of after prepare.  True when it packed them (False: a
-        field is wider than stage 1's width, or stage 1 was not split)."""
-        if not self._stage1c or self._pending is None or self._ga is None or self._stage1b is not None or \
-                os.environ.get("FSDKR_STAGE1C") != "1":   # opt-in: no gain at n = 64 (profiles/r05/r05c_ab_*)
-            return False
-        self._stage1c = False
-        st = self._pending
-        self._rest()
-        self._late(st)
-        F, c = st["F"], self.c
-        nl_ga, ga = self._ga
-        one = max(F[x][1] for x in ("pdl_z", "pdl_u3", "rp_z"))
-        two = max(F[x][1] for x in ("enc", "pdl_u2"))
-        dl = max([1] + [F[x][1] for x in ("dlog_N", "dlog_g", "dlog_ni", "dlog_x1", "dlog_x2") if x in F])
-        if max(one, dl) > 32 * nl_ga or two > 64 * nl_ga or st["ck_short"]:
-            return False   # complete() picks the batch width; the prestart is skipped
-        c.el = _limbs_for(max(F["rp_e"][1], 1))
-        if "dlog_y1" in F:
-            c.yl = _limbs_for(max(F["dlog_y1"][1], F["dlog_y2"][1], 1))
-        width = {"enc": 2 * nl_ga, "pdl_u2": 2 * nl_ga, "rp_e": c.el, "dlog_y1": c.yl, "dlog_y2": c.yl}
-        names = [x for x in _STAGE1C if x in F]
-        Gs = _Gather()
-        for name in names:
-            ga[name] = Gs.slot(F[name], width.get(name, nl_ga))
-        c.ckl = max(st["ckl"], nl_ga)
-        ga["ck_n"] = Gs.slot(st["f_ckn"], c.ckl)
-        ga["ck_sigma"] = Gs.slot(st["f_sig"], c.ckl)
-        Gs.run()
-        for name in names + ["ck_n", "ck_sigma"]:
-            setattr(c, name, self._k(ga[name]))
-        self._points(st)
-        ga["commit"] = None   # marker: complete() keeps the packed points
-        return True
 
     def stage1b(self):
         """The rest of stage 1 (the fixed-base tables' bases and the exponents
@@ -685,10 +642,6 @@ class CollectBatch:
 # stage-1 fields after GA's own (recv_n, pdl_s2, rp_s): the fixed-base tables'
 # bases and the exponents that size them
 _STAGE1B = ("recv_ntilde", "recv_h1", "recv_h2", "ped_T", "ped_N", "pdl_s1", "rp_s1", "pdl_s3", "rp_s2", "ped_Z")
-
-# stage 1c (after 1b): the challenge jobs' limb fields (+ the points, ek.n and sigma_vec)
-_STAGE1C = ("enc", "pdl_z", "pdl_u2", "pdl_u3", "rp_z", "rp_e", "dlog_N", "dlog_g", "dlog_ni", "dlog_x1", "dlog_x2",
-            "dlog_y1", "dlog_y2")
 
 # stage-1 fields whose slot width does not depend on nl
 _STAGE1_WIDTH = {"pdl_s1": lambda c: c.s1l, "rp_s1": lambda c: c.s1l, "pdl_s3": lambda c: c.s3l,

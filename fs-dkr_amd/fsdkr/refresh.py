@@ -232,16 +232,12 @@ def prestart(ctx, batch):
     """The staged starts of a CollectBatch(..., staged=True) before complete():
     stage 1 (GA's fields) -> fsdkr_collect_prestart starts GA; stage 1b (the
     tables' bases and exponents) -> the table chains and comb tables start beside
-    it; stage 1c (the PDL transcripts, Alice c / z / e, Feldman, correct-key and
-    DLog inputs) -> the challenge jobs start.  Each call finds GA running and
-    starts what the newly packed fields allow."""
+    it.  Each call finds GA running and starts what the newly packed fields allow."""
     if not batch.ga_ready or not hasattr(ctx, "collect_prestart"):
         return
     ctx.collect_prestart(batch)
     if batch.stage1b():
         ctx.collect_prestart(batch)
-        if batch.stage1c():
-            ctx.collect_prestart(batch)
 
 
 def collect(refresh_messages, local_key, new_dk, join_messages, ctx=None, m_security=256, key_bits=2048,

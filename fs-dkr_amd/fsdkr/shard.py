@@ -28,7 +28,7 @@ from .batch import CollectBatch, Verdicts
 
 
 # GA split of a small slice (measured: profiles/r02zd_ga_lanes_cus_ab.jsonl, r02zn_ga_split_size_ab.jsonl)
-GA_SPLIT_CUS = int(os.environ.get("FSDKR_SHARD_GA_CUS", "160"))   # env: tuning runs only
+GA_SPLIT_CUS = 160
 GA_SPLIT_MAX_CHAINS = 1024
 
 

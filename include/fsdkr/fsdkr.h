@@ -37,10 +37,19 @@ typedef struct fsdkr_ctx fsdkr_ctx;
 
 typedef struct fsdkr_cfg {
   int32_t device;  /* HIP device ordinal (-1: current device)                 */
-  uint32_t flags;  /* FSDKR_CFG_TIMING: record HIP events around every kernel */
+  uint32_t flags;  /* FSDKR_CFG_* below                                        */
 } fsdkr_cfg;
 
+/* record HIP events around every kernel (fsdkr_kernel_timing) */
 #define FSDKR_CFG_TIMING 1u
+/* Algorithm switches for parity tests and A/B runs.  Results are identical
+ * under every setting; the default (0) is the fastest measured.
+ *   FB_BGMW   fixed-base exponentiations by BGMW windows only (no Lim-Lee comb)
+ *   FB_COMB   a Lim-Lee comb wherever one fits, even where it saves nothing
+ *   INV_EACH  one binary-GCD inverse per element (no simultaneous inversion) */
+#define FSDKR_CFG_FB_BGMW 2u
+#define FSDKR_CFG_FB_COMB 4u
+#define FSDKR_CFG_INV_EACH 8u
 
 /* Context: owns the HIP stream, device buffers and per-modulus constant
  * tables.  Replaces nothing in the reference (which holds no state between
@@ -57,6 +66,9 @@ int fsdkr_ctx_set_modexp_group(fsdkr_ctx* ctx, uint32_t lanes);
  * creation.  The events cost ~9 ms per n = 64 collect (eight streams, one
  * event pair per launch), so timed benchmark regions run with it off. */
 int fsdkr_ctx_set_timing(fsdkr_ctx* ctx, int on);
+/* Replace the context's fsdkr_cfg flags (FSDKR_CFG_*) after creation.  Waits
+ * for outstanding work first. */
+int fsdkr_ctx_set_flags(fsdkr_ctx* ctx, uint32_t flags);
 
 /* Multi-GPU shards: run the s^N mod N^2 chains (GA, the longest dependent
  * chains of collect()) on `ga_cus` CUs spread over the 8 XCDs and every other
@@ -291,7 +303,7 @@ int fsdkr_modexp_joint_batch(fsdkr_ctx* ctx, uint32_t count, const uint32_t* bas
 
 /* Which prestarted parts the last fsdkr_collect_prepare[_multi] reused (bit
  * mask): 1 GA chains, 2 fixed-base tables, 4 correct-key job, 8 ring-Pedersen
- * T^Z exponents (multi-session), 16 challenge jobs, 32 fixed-base exponents.  0 before any prepare.  Diagnostic (tests
+ * T^Z exponents (multi-session).  0 before any prepare.  Diagnostic (tests
  * check that a changed batch is recomputed); the reference has no counterpart. */
 uint32_t fsdkr_collect_reuse_mask(const fsdkr_ctx* ctx);
 
@@ -371,7 +383,7 @@ int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verd
  * evaluates every exponent with Brickell-Gordon-McCurley-Wilson windowing, or,
  * when many exponents share a base, with a Lim-Lee comb over the chain (tables
  * of 2^h products per base: b - 1 squarings and v b products per exponent;
- * FSDKR_FB_COMB=0 forces BGMW); results are identical to fsdkr_modexp_batch.  This is the engine behind the bases the
+ * the context flag FSDKR_CFG_FB_BGMW forces BGMW); results are identical to fsdkr_modexp_batch.  This is the engine behind the bases the
  * reference exponentiates many times with curv BigInt::mod_pow: h1, h2 of a
  * receiver's DLogStatement (zk_pdl_with_slack.rs:144-157, range_proofs.rs:129-137)
  * and ring-Pedersen T (ring_pedersen_proof.rs:144).  mod_limbs in {64, 96}. */

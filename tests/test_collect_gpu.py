@@ -357,77 +357,3 @@ def _vt(v):
     return tuple(bytes(getattr(v, f)) for f in ("feldman", "pdl", "range", "ped", "ck", "dlog"))
 
 
-def _change(msgs, field):
-    """one field of pair (message 1, receiver 2) changed: a field the prestarted
-    challenge jobs read (or hash)"""
-    bad = copy.deepcopy(msgs)
-    m = bad[1]
-    if field in ("u1", "u2", "u3", "z", "s1", "s3"):
-        p = m.pdl_proof_vec[2]
-        val = ec.add(p.u1, ec.G) if field == "u1" else getattr(p, field) + 1
-        m.pdl_proof_vec[2] = dataclasses.replace(p, **{field: val})
-    elif field in ("alice_z", "alice_e"):
-        a = m.range_proofs[2]
-        f = field.split("_")[1]
-        m.range_proofs[2] = dataclasses.replace(a, **{f: getattr(a, f) ^ 1})
-    elif field == "c":
-        m.points_encrypted_vec = list(m.points_encrypted_vec)
-        m.points_encrypted_vec[2] += 1
-    elif field == "Q":
-        m.points_committed_vec = list(m.points_committed_vec)
-        m.points_committed_vec[2] = ec.add(m.points_committed_vec[2], ec.G)
-    elif field == "rp_Z":
-        pf = m.ring_pedersen_proof
-        m.ring_pedersen_proof = dataclasses.replace(pf, Z=tuple(z + (j == 5) for j, z in enumerate(pf.Z)))
-    elif field == "vss":
-        com = m.coefficients_committed_vec
-        pts = list(com.commitments)
-        pts[0] = ec.add(pts[0], ec.G)
-        m.coefficients_committed_vec = type(com)(**{**com.__dict__, "commitments": pts})
-    return bad
-
-
-_FX_FIELDS = ("s1", "s3", "rp_Z")   # read by the prestarted fixed-base exponents (stage 1b)
-
-
-@pytest.mark.parametrize("field", ["u1", "u2", "u3", "z", "s1", "s3", "alice_z", "alice_e", "c", "Q", "vss", "rp_Z"])
-def test_prestart_challenge_jobs_hit_and_miss(gpu_ctx, field, monkeypatch):
-    """Stages 1b / 1c: the second fsdkr_collect_prestart also starts every
-    fixed-base exponent (h1^s1, h2^s3, T^Z behind the tables), the third the
-    challenge jobs -- PDL challenges hashed on the host, c^e mod N^2 and z^e mod
-    N~ with their inverses, pdl_u1, Feldman -- from the packed fields.  A prepare
-    of the same batch reuses them (fsdkr_collect_reuse_mask) and its verdicts equal
-    an un-prestarted run's.  A prepare of a batch with one field changed after the
-    prestart must recompute the parts that read it: its verdicts equal that
-    batch's own un-prestarted run, which rejects the changed proof."""
-    from fsdkr.batch import CollectBatch
-    from fsdkr.refresh import prestart
-    monkeypatch.setenv("FSDKR_STAGE1C", "1")   # both stages are opt-in (profiles/r05/r05c_ab_*)
-    monkeypatch.setenv("FSDKR_FBX", "1")
-    # the challenge jobs include the c^e chains (J2), which GA's joint tail replaces
-    # on the sliding-window shapes: this test runs the separate-J2 path
-    monkeypatch.setenv("FSDKR_JOINT", "0")
-    keys, msgs, dks, _ = _dkr(1, 3, "prestart-chal")
-    lk = keys[0]
-    a = CollectBatch(msgs, lk, [], 256, KB, staged=True)
-    prestart(gpu_ctx, a)
-    a.complete()
-    gpu_ctx.collect_prepare(a)
-    assert {"ga", "chal", "fx"} <= gpu_ctx.collect_reuse()
-    v = gpu_ctx.collect_run(a)
-    ref = gpu_ctx.verify_collect(CollectBatch(msgs, lk, [], 256, KB))
-    assert _vt(v) == _vt(ref)
-    assert (v.pdl & 7 == 7).all() and (v.range & 1).all() and (v.feldman & 1).all()
-    bad = _change(msgs, field)
-    prestart(gpu_ctx, CollectBatch(msgs, lk, [], 256, KB, staged=True))
-    b = CollectBatch(bad, lk, [], 256, KB)
-    gpu_ctx.collect_prepare(b)
-    reused = gpu_ctx.collect_reuse()
-    if field in _FX_FIELDS:
-        assert "fx" not in reused
-    if field not in ("s3", "rp_Z"):   # (the challenge jobs read neither)
-        assert "chal" not in reused
-    vb = gpu_ctx.collect_run(b)
-    want = gpu_ctx.verify_collect(CollectBatch(bad, lk, [], 256, KB))
-    assert _vt(vb) == _vt(want)
-    assert _vt(want) != _vt(ref)

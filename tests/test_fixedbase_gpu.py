@@ -81,24 +81,23 @@ def test_fixed_base_window_widths(gpu_ctx, top_bits):
 
 
 @pytest.fixture
-def comb_mode():
-    """FSDKR_FB_COMB for the duration of a test (read by the library per call)."""
-    import os
-    old = os.environ.get("FSDKR_FB_COMB")
+def comb_mode(gpu_ctx):
+    """The fixed-base engine for the duration of a test: 0 BGMW only
+    (FSDKR_CFG_FB_BGMW), 2 a comb wherever one fits (FSDKR_CFG_FB_COMB), 1 chosen."""
+    from fsdkr._native import FSDKR_CFG_FB_BGMW, FSDKR_CFG_FB_COMB
+    old = gpu_ctx.flags
 
     def set_mode(m):
-        os.environ["FSDKR_FB_COMB"] = str(m)
+        base = old & ~(FSDKR_CFG_FB_BGMW | FSDKR_CFG_FB_COMB)
+        gpu_ctx.set_flags(base | {0: FSDKR_CFG_FB_BGMW, 1: 0, 2: FSDKR_CFG_FB_COMB}[m])
     yield set_mode
-    if old is None:
-        os.environ.pop("FSDKR_FB_COMB", None)
-    else:
-        os.environ["FSDKR_FB_COMB"] = old
+    gpu_ctx.set_flags(old)
 
 
 @pytest.mark.parametrize("limbs", [64, 96])
 @pytest.mark.parametrize("mode", [0, 2])
 def test_comb_matches_pow(gpu_ctx, comb_mode, limbs, mode):
-    """Lim-Lee comb (comb.hip, forced by FSDKR_FB_COMB=2) and BGMW (=0) on the
+    """Lim-Lee comb (comb.hip, forced by FSDKR_CFG_FB_COMB) and BGMW (FSDKR_CFG_FB_BGMW) on the
     mixed case: zero / one / unreduced bases, half-width modulus, exponents of
     0 .. 2816 bits including all-ones rows and columns of the bit array."""
     comb_mode(mode)

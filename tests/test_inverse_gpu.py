@@ -54,13 +54,14 @@ def test_inverse_matches_python(gpu_ctx, limbs):
 
 @pytest.mark.parametrize("limbs", [64, 128])
 @pytest.mark.parametrize("kind", ["units", "one_non_unit", "zero", "singletons"])
-def test_simultaneous_inverse_groups(gpu_ctx, limbs, kind, monkeypatch):
+def test_simultaneous_inverse_groups(gpu_ctx, limbs, kind):
     """Instances sharing a modulus are inverted together (Montgomery's trick,
     inverse_batch_kernel: prefix products, ONE binary-GCD inverse, a backward
     pass): exact inverses and unit flags equal pow(y, -1, m), including a group
     whose product is not a unit (every element of it then inverted on its own),
-    y = 0 and groups of one.  FSDKR_BATCH_INV=0 (one inverse each) gives the
+    y = 0 and groups of one.  FSDKR_CFG_INV_EACH (one inverse each) gives the
     same results."""
+    from fsdkr._native import FSDKR_CFG_INV_EACH
     rnd = random.Random(1000 * limbs + len(kind))
     bits = 32 * limbs
     mods = [_case(rnd, bits, "rsa2" if limbs == 128 else "odd") for _ in range(5)]
@@ -76,8 +77,11 @@ def test_simultaneous_inverse_groups(gpu_ctx, limbs, kind, monkeypatch):
     if kind == "zero":
         ys[3] = 0
     got = gpu_ctx.mod_inverse(ys, ms, limbs)
-    monkeypatch.setenv("FSDKR_BATCH_INV", "0")
-    ref = gpu_ctx.mod_inverse(ys, ms, limbs)
+    old = gpu_ctx.set_flags(gpu_ctx.flags | FSDKR_CFG_INV_EACH)
+    try:
+        ref = gpu_ctx.mod_inverse(ys, ms, limbs)
+    finally:
+        gpu_ctx.set_flags(old)
     for k, (y, m, g) in enumerate(zip(ys, ms, got)):
         try:
             want = pow(y, -1, m)

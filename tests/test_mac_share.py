@@ -39,7 +39,7 @@ def _rows(KD, G, sq):
 
 @pytest.mark.parametrize("kernel,KD,G", [("modexp_slide_kernel<144, 16, 128, true>", 144, 16),
                                           ("modexp_kernel<72, 8, 64, false, true>", 72, 8),
-                                          ("modexp_kernel<144, 4, 128, false, false>", 144, 4)])
+                                          ("modexp_kernel<144, 4, 128, false, true>", 144, 4)])
 def test_cycle_loops_match_row_structure(shares, kernel, KD, G):
     s, how, cyc = shares[kernel]
     assert how == "min over cycle loops"

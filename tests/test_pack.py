@@ -138,25 +138,18 @@ def _dump(b, M):
 
 @pytest.mark.parametrize("big_ped", [False, True])
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("stage1c", [False, True])
-def test_staged_batch_equals_one_shot(big_ped, split, stage1c, monkeypatch):
+def test_staged_batch_equals_one_shot(big_ped, split):
     """CollectBatch(staged=True) + complete() packs exactly what the one-shot
     constructor packs, also when stage 1's width is superseded (a 3000-bit PDL z,
-    a stage-2 field, moves the batch to 3072-bit slots), when stage 1 is split
-    (GA's fields, then stage1b()), and with stage1c() (the challenge jobs' fields:
-    refused when a field is wider than stage 1's width)."""
+    a stage-2 field, moves the batch to 3072-bit slots) and when stage 1 is split
+    (GA's fields, then stage1b())."""
     from fsdkr.batch import CollectBatch
-    monkeypatch.setenv("FSDKR_STAGE1C", "1")   # (opt-in stage)
     M = 8
     msgs, joins, lk = _fake_collect(M=M, big_ped=big_ped)
     one = CollectBatch(msgs, lk, joins, M, 2048)
     st = CollectBatch(msgs, lk, joins, M, 2048, staged=True, split_stage1=split)
     assert st.ga_ready and st.c.nl == 64
-    assert not st.stage1c()   # only after stage1b()
     assert st.stage1b() == split and not st.stage1b()
-    if stage1c:
-        assert st.stage1c() == (split and not big_ped)
-        assert not st.stage1c()
     st.complete()
     one._msgs = st._msgs = msgs
     a, b = _dump(one, M), _dump(st, M)

@@ -36,7 +36,6 @@ def main():
     tc, nc = ctx.kernel_time("comb_exp")
     print(json.dumps({"bases": a.bases, "per_base": a.per_base, "bits": a.bits, "fb_table_ms": tt / max(nt, 1),
                       "fb_exp_ms": te / max(ne, 1), "comb_exp_ms": tc / max(nc, 1), "comb_launches": nc,
-                      "comb_qs": os.environ.get("FSDKR_COMB_QS", "1"),
                       "table_us_per_square": tt / max(nt, 1) * 1e3 / a.bits}))
 
 
