@@ -512,10 +512,7 @@ int run_modexp_keyed(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_bas
             exp_limbs, exp_bits, idx[i]);
   }
   job.exp_bits = exp_bits;
-  // lanes per instance as the generic 4096-bit launch picks them (modexp.hip
-  // pick_group): the widest shape whose lanes fit the resident-wave capacity
-  constexpr uint64_t kLaneCapacity = 256ull * 4 * 3 * 64;
-  const uint32_t G = (uint64_t)count * 16 <= kLaneCapacity ? 16u : (uint64_t)count * 8 <= kLaneCapacity ? 8u : 4u;
+  const uint32_t G = keyed_lanes(count);
   uint32_t flags = 0;   // the regrouped job carries out_idx (the caller's rows)
   if (k32 == 128 && !c->ct && group_by_exponent(job, 64 / G, kPadSelf)) flags = kDescOutIdx | kDescSlide;
   return launch_modexp_job(c, job, d_consts, d_out, "keyed", (flags & kDescSlide) ? G : 0u, flags);

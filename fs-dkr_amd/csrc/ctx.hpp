@@ -189,6 +189,12 @@ constexpr uint32_t kDescOutIdx = 1, kDescSlide = 2;
 // pad_row == kPadSelf: a pad copy writes its chain's own row (the same value
 // twice, no scratch row needed)
 constexpr uint32_t kNoPad = 0xffffffffu, kPadSelf = 0xfffffffeu;
+// lanes per instance of a keyed 4096-bit launch, as the generic launch picks them
+// (modexp.hip pick_group): the widest shape whose lanes fit the resident-wave capacity
+inline uint32_t keyed_lanes(size_t count) {
+  constexpr uint64_t kLaneCapacity = 256ull * 4 * 3 * 64;
+  return (uint64_t)count * 16 <= kLaneCapacity ? 16u : (uint64_t)count * 8 <= kLaneCapacity ? 8u : 4u;
+}
 inline bool group_by_exponent(ModexpJob& J, uint32_t per_wave, uint32_t pad_row) {
   const size_t cnt = J.size();
   // stable order by exponent address: a counting sort over the few distinct

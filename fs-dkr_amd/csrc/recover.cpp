@@ -177,14 +177,34 @@ int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const ui
   }
   for (uint32_t k = 0; k < count; ++k)
     if (n_idx[k] >= n_keys) return FSDKR_E_ARG;
-  // device image: ns | NNs | m | r | one | outputs
+  // device image: ns | NNs | m | r | one | outputs | descriptors
   const size_t b_ns = 0, b_nns = b_ns + (size_t)n_keys * nl * 4, b_m = b_nns + NNs.size() * 4;
   const size_t b_r = b_m + (size_t)count * ml * 4, b_one = b_r + (size_t)count * nl * 4;
   const size_t b_gm = b_one + (size_t)nn * 4, b_rn = b_gm + (size_t)count * nn * 4;
   const size_t b_out = b_rn + (size_t)count * nn * 4, b_desc = b_out + (size_t)count * nn * 4;
-  const size_t total = b_desc + (size_t)count * (16 + 32 + sizeof(Prod3Operand) + 4) + 8 * 256 + 4096;
+  // r^N mod N^2: every share under key k has exponent N_k.  At 4096 bits the job is
+  // regrouped by key so every wave shares its exponent and runs sliding windows
+  // (modexp_slide_kernel, as fsdkr_modexp_keyed_device: metric 2); pads rewrite
+  // their own chain's row.  Other widths keep fixed windows.  The base r and the
+  // exponent schedule's memory accesses depend on N only (public).
+  ModexpJob job;
+  job.k32 = nn;
+  auto A0 = [](size_t off) { return (uint64_t)off; };   // offsets until the buffer exists
+  for (uint32_t k = 0; k < count; ++k)
+    job.add(A0(b_r + (size_t)k * nl * 4), nl, A0(b_ns + (size_t)n_idx[k] * nl * 4), nl, 32 * nl, n_idx[k]);
+  uint32_t G = 0, flags = 0;
+  if (nn == 128 && !cx->ct) {
+    G = keyed_lanes(count);
+    if (group_by_exponent(job, 64 / G, kPadSelf)) flags = kDescOutIdx | kDescSlide;
+    else G = 0;
+  }
+  const size_t total = b_desc + job.desc_bytes() + (size_t)count * (16 + sizeof(Prod3Operand) + 4) + 8 * 256 + 4096;
   uint8_t* d = (uint8_t*)cx->buf("enc", total);
   if (!d) return FSDKR_E_OOM;
+  for (size_t i = 0; i < job.size(); ++i) {   // offsets -> device addresses
+    job.base_ptr[i] += (uint64_t)(uintptr_t)d;
+    job.exp_ptr[i] += (uint64_t)(uintptr_t)d;
+  }
   std::vector<uint8_t> img(b_desc, 0);
   memcpy(img.data() + b_ns, ns, (size_t)n_keys * nl * 4);
   memcpy(img.data() + b_nns, NNs.data(), NNs.size() * 4);
@@ -194,14 +214,11 @@ int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const ui
   auto A = [&](size_t off) { return (uint64_t)(uintptr_t)(d + off); };
   // binom: gm = 1 + m*N  (m < N for a share; reduced mod N^2 by prod3 anyway)
   std::vector<uint64_t> s_ptr(count), n_ptr(count);
-  ModexpJob job;
-  job.k32 = nn;
   std::vector<Prod3Operand> ops(count);
   std::vector<uint32_t> midx(count);
   for (uint32_t k = 0; k < count; ++k) {
     s_ptr[k] = A(b_m + (size_t)k * ml * 4);
     n_ptr[k] = A(b_ns + (size_t)n_idx[k] * nl * 4);
-    job.add(A(b_r + (size_t)k * nl * 4), nl, A(b_ns + (size_t)n_idx[k] * nl * 4), nl, 32 * nl, n_idx[k]);
     ops[k] = {A(b_gm + (size_t)k * nn * 4), A(b_rn + (size_t)k * nn * 4), A(b_one), nn, nn, nn, 0};
     midx[k] = n_idx[k];
   }
@@ -223,7 +240,9 @@ int fsdkr_paillier_encrypt(fsdkr_ctx* ctx, uint32_t nl, uint32_t count, const ui
   if ((rc = setup_moduli(cx, nn, (const uint32_t*)(d + b_nns), n_keys, &consts, "enc"))) return rc;
   BinomArgs ba{(const uint64_t*)(d + o_s), (const uint64_t*)(d + o_n), ml, nl, nn, (uint32_t*)(d + b_gm), count};
   if ((rc = cx->hip_check(launch_binom(ba, cx->stream), "binom"))) return rc;
-  if ((rc = launch_modexp_desc(cx, nn, count, 32 * nl, d + o_job, consts, (uint32_t*)(d + b_rn)))) return rc;
+  if ((rc = launch_modexp_desc(cx, nn, (uint32_t)job.size(), 32 * nl, d + o_job, consts, (uint32_t*)(d + b_rn),
+                                nullptr, "mxtable", cx->prio, G, flags)))
+    return rc;
   Prod3Args pa{(const Prod3Operand*)(d + o_ops), (const uint32_t*)(d + o_midx), consts, (uint32_t*)(d + b_out), count};
   // prod3 computes a*b*c mod N^2 exactly: (1+mN) * r^N * 1
   if ((rc = cx->hip_check(launch_prod3(nn, pa, cx->stream), "prod3"))) return rc;

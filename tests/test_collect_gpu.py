@@ -214,6 +214,26 @@ def test_paillier_encrypt_job1(gpu_ctx):
     assert got == want
 
 
+@pytest.mark.parametrize("bits", [2048, 3072])
+def test_paillier_encrypt_ragged_keys(gpu_ctx, bits):
+    """Job 1 with the shares of many keys in shuffled order and ragged counts per
+    key (one key with a single share, one with 70, one unused): at 2048 bits the
+    r^N chains are regrouped by key into sliding-window waves (pads rewrite their
+    own row), at 3072 bits fixed windows; every ciphertext equals
+    encrypt_with_chosen_randomness in the caller's order."""
+    import random
+    rng = Rng(f"job1-ragged-{bits}")
+    keys = [paillier.keypair_with_modulus_size(bits, rng)[0] for _ in range(5)]
+    idx = [0] * 1 + [1] * 70 + [2] * 9 + [4] * 33   # key 3 unused
+    random.Random(bits).shuffle(idx)
+    ms = [rng.sample_below(ec.Q) for _ in idx]
+    rs = [rng.sample_below(keys[i].n) for i in idx]
+    rs[5] = 1                                        # r = 1: c = 1 + mN
+    got = gpu_ctx.paillier_encrypt(ms, rs, [k.n for k in keys], idx, bits // 32)
+    want = [paillier.encrypt_with_chosen_randomness(keys[i], m, r) for m, r, i in zip(ms, rs, idx)]
+    assert got == want
+
+
 def test_prestart_hit_and_miss(gpu_ctx):
     """fsdkr_collect_prestart: a prepare of the batch it was started for reuses
     the s^N mod N^2 rows (every proof verifies); a prepare of a DIFFERENT batch
