@@ -341,17 +341,23 @@ def modexp_roofline(ctx, count, reps, seed=1234, keyed=True):
 
 
 def pmc_traffic(count, pattern="r*_pmc_modexp4096_keyed.json"):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    """Bytes past L2 per launch of the roofline kernel from the committed rocprofv3
     --pmc passes (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 per the
     gfx950 correction + WRITE_SIZE, one pass each), scaled to `count`
-    instances.  PMC cannot be collected inside the timed run."""
+    instances, and the pass's L2 hit rate.  FETCH_SIZE / WRITE_SIZE count the
+    L2's fabric requests, Infinity-Cache (MALL) hits included
+    (MI355X_MICROARCH.md, HBM section), so this bounds HBM traffic from above.
+    The newest round's file wins.  PMC cannot be collected inside the timed run."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "**", pattern), recursive=True))
+    import re
+    files = glob.glob(os.path.join(REPO, "profiles", "**", pattern), recursive=True)
     if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    inst = d.get("instances", 65536)
-    return d["hbm_traffic_bytes"] * count / inst, os.path.relpath(files[-1], REPO)
+        return None, None, None
+    rnd = lambda f: int(re.search(r"r(\d+)", os.path.basename(f)).group(1))   # noqa: E731
+    f = max(files, key=lambda f: (rnd(f), os.path.basename(f)))
+    d = json.load(open(f))
+    inst = d.get("instances", 65536)   # tools/pmc.sh's --count (files before round 6 did not record it)
+    return d["hbm_traffic_bytes"] * count / inst, os.path.relpath(f, REPO), d.get("l2_hit_rate")
 
 
 def _phases_once(ctx, msgs, lk, joins, key_bits):
@@ -644,7 +650,7 @@ def main():
     s4 = sessions_bench(ctx, a.sessions, a.session_steps, a.seed + 4) if a.sessions and world == 1 else None
     kg = keygen_bench(ctx) if world == 1 else None
     W_collect = collect_work(R, J, n)
-    traffic, traffic_src = pmc_traffic(roof["count"])
+    traffic, traffic_src, l2_hit = pmc_traffic(roof["count"])
     out = {
         "metric": METRIC, "value": value, "unit": "proofs/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
@@ -666,14 +672,19 @@ def main():
             "what": "fsdkr_modexp_batch_device: a per-instance exponent row, fixed 5-bit windows (modexp_kernel)"},
         "roofline": {"bound": "valu-int", "achieved": roof["achieved_mac_per_s"] / 1e12, "peak": PEAK_MAC / 1e12,
                      "unit": "T u32-MAC/s", "frac": roof["achieved_mac_per_s"] / PEAK_MAC, "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (PMC)", "traffic_source": traffic_src,
+                     "traffic_unit": "bytes past L2 per launch (PMC FETCH_SIZE x2 + WRITE_SIZE; Infinity-Cache "
+                                     "hits included, so an upper bound on HBM bytes)",
+                     "traffic_source": traffic_src, "l2_hit_rate": l2_hit,
                      "algorithmic_bytes": roof["count"] * (512 + 256 + 512),
                      "kernel": "modexp_slide_kernel (4096-bit modulus N^2, 2048-bit exponent N shared per key: "
                                "fsdkr_modexp_keyed_device, 16 keys x 4096 instances, sliding windows w = 7)",
                      "per_launch": f"{roof['count']} instances x {w_modexp(128, 2048) / 1e6:.2f} M MACs in "
                                    f"{roof['kernel_ms']:.2f} ms (HIP events)",
-                     "accounting": "achieved = SURVEY §8d MACs (32-bit limbs, 2k^2+k per modmul); issued = the "
-                                   "kernel's own v_mad_u64_u32 lane-ops (29-bit digits, squaring rows)",
+                     "accounting": "achieved / frac = SURVEY §8d MACs (32-bit limbs, 2k^2+k per modmul, fixed "
+                                   "5-bit windows): an algorithmic-equivalent rate; the kernel runs w = 7 sliding "
+                                   "windows and issues fewer products.  issued / issued_frac = the kernel's own "
+                                   "v_mad_u64_u32 lane-ops (29-bit digits, squaring rows): the fraction of the "
+                                   "int-MAC peak it actually uses",
                      "issued": roof["issued_mac_per_s"] / 1e12, "issued_frac": roof["issued_mac_per_s"] / PEAK_MAC,
                      "lanes_per_instance": roof["group"]},
         "collect_efficiency": efficiency(W_collect, collect_issued(R, J, n), ms_per_step * 1e-3, world,

@@ -208,7 +208,15 @@ class _Negatives:
     - composite DLog (zk-paillier, joins :417-424): y < 0 panics in g^y once the
       N > 2^128 and gcd checks pass (else false); proof 2 runs only if proof 1
       holds; x < 0 (hashed as |x|) never equals mod_mul(g^y, ni^e) >= 0: that
-      proof is false unless its y panics first."""
+      proof is false unless its y panics first.
+
+    Provenance and parity: the sign rules of curv-kzen 0.10 (Cargo.toml:33;
+    BigInt::mod_pow / mod_mul / to_bytes over rust-gmp, Cargo.toml:43) and the
+    DLog verification order of zk-paillier 0.4.4 (Cargo.toml:32,
+    CompositeDLogProof::verify) are restated from those published crates, which
+    /root/reference does not vendor.  The GPU outcomes for negative operands are
+    checked against the local oracle (oracle/), which encodes the same
+    restatement, not against reference-produced fixtures: parity unpinned."""
 
     def __init__(self):
         self.rows = {}     # field -> rows packed with a stand-in

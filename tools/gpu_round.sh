@@ -19,6 +19,7 @@
 #                    tools/mac_share.py's per-kernel MAC shares of this build: pmc_mac_per_call)
 #   pmcmx            PMC passes over the metric-2 modexp launch (tools/pmc.sh)
 #   shard256         bench.py --emulate-shard 2 / 4 / 8 at n = 256 -> shard_n256.jsonl
+#   trace256s8       kernel trace of the emulated rank 0 of an 8-way n = 256 shard -> trace256s8_summary.txt
 #   shard64          the same at n = 64                            -> shard_n64.jsonl
 #   anything else    run as a shell command                       -> extra.log
 # Interleaved A/B runs: tools/ab_env.sh (environment variants of one build) and
@@ -79,6 +80,11 @@ for step in "$@"; do
                 || fail trace256 $? $OUT/trace256.log
               f=$(find $OUT/trace256 -name "*kernel_trace.csv" | head -1)
               python $R/tools/prof_summary.py "$f" --gap 10 --step -1 > $OUT/trace256_summary.txt || exit 1 ;;
+    trace256s8) (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace256s8 -o tr \
+                  -- python3 $R/bench.py --n 256 --t 128 --joins 0 --steps 3 --warmup 1 --emulate-shard 8 --gap-ms 60 \
+                  > $OUT/trace256s8.log 2>&1) || fail trace256s8 $? $OUT/trace256s8.log
+                f=$(find $OUT/trace256s8 -name "*kernel_trace.csv" | head -1)
+                python $R/tools/prof_summary.py "$f" --gap 40 --step -1 > $OUT/trace256s8_summary.txt || exit 1 ;;
     pmc64) pmc_step n64 --n 64 --joins 4 --t 32 ;;
     pmc256) pmc_step n256 --n 256 --joins 0 --t 128 ;;
     pmc4) pmc_step c4 --sessions 1024 --seed 2028 ;;

@@ -43,7 +43,7 @@ def main():
             names |= nm
     fetch_raw = per.get("FETCH_SIZE", 0.0) * 1024
     write = per.get("WRITE_SIZE", 0.0) * 1024
-    out = {"kernel": sorted(names), "per_launch": per,
+    out = {"kernel": sorted(names), "instances": a.instances, "per_launch": per,
            "hbm_fetch_bytes_raw": fetch_raw, "hbm_fetch_bytes_corrected_x2": 2 * fetch_raw,
            "hbm_write_bytes": write, "hbm_traffic_bytes": 2 * fetch_raw + write}
     if "SQ_INSTS_VALU" in per:
