@@ -340,12 +340,27 @@ struct Mont29 {
   // the read's latency hides behind this row's MACs instead of stalling the
   // next row (one wave per SIMD in latency-bound launches has no other wave
   // to cover it).  arow[L] past the last cycle reads a harmless in-range word.
+  // Short lanes (latency shapes) carry the next cycle's first NXT digits in
+  // registers from the top of the cycle (product(), cycle_c)
+  static constexpr int NXT = L <= 12 ? 1 : 0;
   template <int R, bool SQ, bool QS>
   __device__ __forceinline__ void row_pf(uint64_t* acc, const uint32_t* b, const uint32_t* b2, const uint32_t* n,
                                          const uint32_t* arow, uint32_t& cur, uint32_t next_off) const {
     const uint32_t ai = cur;
     cur = (R + 1 < L) ? arow[R + 1] : arow[next_off];
     row<R, SQ, QS>(acc, b, b2, n, ai);
+  }
+  // row R of a carried-digit cycle: its digit is carried (R < NXT) or read here
+  template <int R, bool SQ, bool QS>
+  __device__ __forceinline__ void row_c(uint64_t* acc, const uint32_t* b, const uint32_t* b2, const uint32_t* n,
+                                        const uint32_t* arow, const uint32_t* carried) const {
+    row<R, SQ, QS>(acc, b, b2, n, R < NXT ? carried[R < NXT ? R : 0] : arow[R]);
+  }
+  template <bool SQ, bool QS, int... Rs>
+  __device__ __forceinline__ void cycle_c(uint64_t* acc, const uint32_t* b, const uint32_t* b2, const uint32_t* n,
+                                          const uint32_t* arow, const uint32_t* carried,
+                                          std::integer_sequence<int, Rs...>) const {
+    (row_c<Rs, SQ, QS>(acc, b, b2, n, arow, carried), ...);
   }
 
   template <bool SQ, bool QS, int... Rs>
@@ -376,6 +391,33 @@ struct Mont29 {
     if constexpr (SQ && USE_B2) {
 #pragma unroll
       for (int j = 0; j < L; ++j) b2[j] = b[j] << 1;   // digits <= 2^29 + 127: fits
+    }
+    if constexpr (NXT) {
+      // the next cycle's first NXT digits are read at the top of this cycle and
+      // held in registers to its end (left to itself the compiler issued every
+      // cycle's reads at its top and waited there for the first one: one LDS
+      // round trip per cycle, 16 per 16-lane product); the later rows' reads are
+      // then done before those rows
+      uint32_t car[NXT];
+#pragma unroll
+      for (int k = 0; k < NXT; ++k) car[k] = a_lds[k];
+#pragma unroll 1
+      for (int cyc = 0; cyc < G; ++cyc) {
+        uint32_t nx[NXT];
+#pragma unroll
+        for (int k = 0; k < NXT; ++k) nx[k] = a_lds[(cyc + 1 < G ? cyc + 1 : 0) * L + k];
+        opaque<L>(b);
+        if constexpr (!(SQ && USE_B2)) opaque<L>(n);
+        if constexpr (SQ && USE_B2) opaque<L>(b2);
+        cycle_c<SQ, QS>(acc, b, b2, n, a_lds + cyc * L, car, std::make_integer_sequence<int, L>{});
+#pragma unroll
+        for (int k = 0; k < NXT; ++k) {
+          asm volatile("" : "+v"(nx[k]));
+          car[k] = nx[k];
+        }
+      }
+      finish(out, acc);
+      return;
     }
     uint32_t cur = a_lds[0];
 #pragma unroll 1

@@ -398,61 +398,5 @@ EC_D void scalar_reduce(uint32_t* k) {
   }
 }
 
-// r = k*P (P affine, not infinity), k < 2^256 (caller reduces mod q)
-EC_D void scalar_mul_aff(Jac& r, const uint32_t* k, const Fe& x, const Fe& y) {
-  Jac acc;
-  jac_set_inf(acc);
-  for (int i = 7; i >= 0; --i) {
-    const uint32_t w = k[i];
-    for (int b = 31; b >= 0; --b) {
-      jac_dbl(acc, acc);
-      if ((w >> b) & 1u) jac_add_aff(acc, acc, x, y);
-    }
-  }
-  r = acc;
-}
-
-// r = k1*P1 + k2*P2 (P1, P2 affine; an infinite P2 is passed as inf2 = true),
-// k1, k2 < 2^256: Shamir's trick with 4-bit fixed windows -- 256 shared
-// doublings and at most 2 x 64 table additions instead of two separate
-// double-and-add ladders (512 doublings + ~256 additions).  The 15-entry
-// Jacobian tables live in private (scratch) memory.
-EC_D void shamir_mul2_aff(Jac& r, const uint32_t* k1, const Fe& x1, const Fe& y1, const uint32_t* k2, const Fe& x2,
-                          const Fe& y2, bool inf2) {
-  Jac T1[16], T2[16];
-  jac_set_inf(T1[0]);
-  jac_set_inf(T2[0]);
-  T1[1].X = x1;
-  T1[1].Y = y1;
-  fe_set_u32(T1[1].Z, 1);
-  if (inf2) {
-    jac_set_inf(T2[1]);
-  } else {
-    T2[1].X = x2;
-    T2[1].Y = y2;
-    fe_set_u32(T2[1].Z, 1);
-  }
-  for (int d = 2; d < 16; ++d) {
-    if (inf2) jac_set_inf(T2[d]);
-    else jac_add_aff(T2[d], T2[d - 1], x2, y2);
-    jac_add_aff(T1[d], T1[d - 1], x1, y1);
-  }
-  Jac acc;
-  jac_set_inf(acc);
-  for (int nib = 63; nib >= 0; --nib) {
-    if (nib != 63) {
-      jac_dbl(acc, acc);
-      jac_dbl(acc, acc);
-      jac_dbl(acc, acc);
-      jac_dbl(acc, acc);
-    }
-    const uint32_t d1 = (k1[nib >> 3] >> (4 * (nib & 7))) & 15u;
-    const uint32_t d2 = (k2[nib >> 3] >> (4 * (nib & 7))) & 15u;
-    if (d1) jac_add(acc, acc, T1[d1]);
-    if (d2) jac_add(acc, acc, T2[d2]);
-  }
-  r = acc;
-}
-
 }  // namespace ec
 }  // namespace fsdkr

@@ -1,6 +1,7 @@
 // Stand-alone verification entry points of the C ABI (include/fsdkr/fsdkr.h):
 //   fsdkr_feldman_check          validate_collect's Feldman loop (refresh_message.rs:177-188)
 //   fsdkr_ring_pedersen_verify   RingPedersenProof::verify (ring_pedersen_proof.rs:126-157)
+//   fsdkr_pdl_u1_check           PDLwSlackProof::verify's u1 equation (zk_pdl_with_slack.rs:124-127,158)
 // JoinMessage::collect (add_party_message.rs:136-175) needs exactly these two
 // checks and none of the pair proofs, so it calls them instead of the whole
 // fsdkr_verify_collect pipeline.  Both run on the context stream; the ring-
@@ -68,6 +69,43 @@ int fsdkr_feldman_check(fsdkr_ctx* ctx, uint32_t n_msgs, uint32_t n, uint32_t t,
   c->mark("ec", false);
   if (rc) return rc;
   if ((rc = c->hip_check(hipMemcpyAsync(verdict, d_out, P, hipMemcpyDeviceToHost, c->stream), "D2H feldman")))
+    return rc;
+  return c->sync();
+}
+
+int fsdkr_pdl_u1_check(fsdkr_ctx* ctx, uint32_t count, const uint32_t* s1, uint32_t s1_len, const uint32_t* e,
+                       const uint32_t* Q, const uint32_t* u1, uint8_t* verdict) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (!c) return FSDKR_E_ARG;
+  if (count == 0) return FSDKR_OK;
+  if (!s1 || !e || !Q || !u1 || !verdict || s1_len == 0) {
+    c->fail("fsdkr_pdl_u1_check: bad argument");
+    return FSDKR_E_ARG;
+  }
+  const size_t sb = (size_t)count * s1_len * 4, eb = (size_t)count * 32, pb = (size_t)count * 64;
+  uint8_t* d = (uint8_t*)c->buf("u1_io", al256(sb) + al256(eb) + 2 * al256(pb) + count);
+  if (!d) {
+    c->fail("fsdkr_pdl_u1_check: device allocation failed");
+    return FSDKR_E_OOM;
+  }
+  uint32_t* d_s1 = (uint32_t*)d;
+  uint32_t* d_e = (uint32_t*)(d + al256(sb));
+  uint32_t* d_q = (uint32_t*)(d + al256(sb) + al256(eb));
+  uint32_t* d_u = (uint32_t*)(d + al256(sb) + al256(eb) + al256(pb));
+  uint8_t* d_out = d + al256(sb) + al256(eb) + 2 * al256(pb);
+  int rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(d_s1, s1, sb, hipMemcpyHostToDevice, c->stream), "H2D s1")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_e, e, eb, hipMemcpyHostToDevice, c->stream), "H2D e")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_q, Q, pb, hipMemcpyHostToDevice, c->stream), "H2D Q")) ||
+      (rc = c->hip_check(hipMemcpyAsync(d_u, u1, pb, hipMemcpyHostToDevice, c->stream), "H2D u1")) ||
+      (rc = c->hip_check(hipMemsetAsync(d_out, 0, count, c->stream), "memset u1")))
+    return rc;
+  PdlU1Args u{d_s1, d_e, d_q, d_u, s1_len, d_out, count};
+  c->mark("ec", true);
+  rc = c->hip_check(launch_pdl_u1(u, c->stream), "pdl_u1");
+  c->mark("ec", false);
+  if (rc) return rc;
+  if ((rc = c->hip_check(hipMemcpyAsync(verdict, d_out, count, hipMemcpyDeviceToHost, c->stream), "D2H u1")))
     return rc;
   return c->sync();
 }

@@ -198,6 +198,8 @@ def lib():
     L.fsdkr_fixed_base_modexp.restype = ctypes.c_int
     L.fsdkr_feldman_check.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, u8p]
     L.fsdkr_feldman_check.restype = ctypes.c_int
+    L.fsdkr_pdl_u1_check.argtypes = [vp, ctypes.c_uint32, u32p, ctypes.c_uint32, u32p, u32p, u32p, u8p]
+    L.fsdkr_pdl_u1_check.restype = ctypes.c_int
     L.fsdkr_ring_pedersen_verify.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                              u32p, u32p, u32p, u32p, u32p, u8p]
     L.fsdkr_ring_pedersen_verify.restype = ctypes.c_int
@@ -511,6 +513,18 @@ class Context:
         self.check(self._lib.fsdkr_paillier_encrypt(self._h, nl, len(ms), _ptr(Mm), ml, _ptr(Rr), _ptr(I), _ptr(Nn),
                                                     len(ns), _ptr(O)))
         return limbs_to_ints(O)
+
+    def pdl_u1_check(self, s1s, es, Qs, u1s):
+        """[G*(s1 mod q) + Q*(q - e mod q) == u1] per pair (uint8 0/1)."""
+        from .batch import pack_points
+        sl = max(1, (max(s.bit_length() for s in s1s) + 31) // 32)
+        S = ints_to_limbs(s1s, sl)
+        E = ints_to_limbs(es, 8)
+        Qp, Up = pack_points(Qs), pack_points(u1s)
+        out = np.zeros(len(s1s), dtype=np.uint8)
+        self.check(self._lib.fsdkr_pdl_u1_check(self._h, len(s1s), _ptr(S), sl, _ptr(E), _ptr(Qp), _ptr(Up),
+                                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out
 
     def feldman_check(self, vss, commit, n, t):
         """vss: [n_msgs][t+1] points, commit: [n_msgs*n] points -> uint8 verdicts [n_msgs*n]."""

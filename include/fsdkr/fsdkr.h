@@ -396,6 +396,13 @@ int fsdkr_fixed_base_modexp(fsdkr_ctx* ctx, uint32_t mod_limbs, uint32_t n_bases
  * VerifiableSS::validate_share_public): verdict[k*n + i] = 1 iff
  * commit[k*n + i] == sum_j vss[k][j] * (i+1)^j.  vss: [n_msgs][t+1][16],
  * commit: [n_msgs*n][16] affine points ((0,0) = infinity). */
+/* PDLwSlackProof::verify's u1 equation (zk_pdl_with_slack.rs:124-127, :158):
+ * verdict[p] = 1 iff G*(s1[p] mod q) + Q[p]*(q - e[p] mod q) == u1[p].  s1:
+ * [count][s1_len] limbs (any width), e: [count][8], Q / u1: [count][16] affine
+ * points ((0,0) = infinity).  The collect() pipeline runs the same kernel
+ * (pdl_u1_kernel: four lanes per pair over the GLV split of both scalars). */
+int fsdkr_pdl_u1_check(fsdkr_ctx* ctx, uint32_t count, const uint32_t* s1, uint32_t s1_len, const uint32_t* e,
+                       const uint32_t* Q, const uint32_t* u1, uint8_t* verdict);
 int fsdkr_feldman_check(fsdkr_ctx* ctx, uint32_t n_msgs, uint32_t n, uint32_t t, const uint32_t* vss,
                         const uint32_t* commit, uint8_t* verdict);
 /* RingPedersenProof::verify (ring_pedersen_proof.rs:126-157) for `count`
