@@ -433,7 +433,7 @@ int launch_modexp_job(Ctx* c, const ModexpJob& job, const uint32_t* d_consts, ui
 }
 
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
-                 uint32_t group) {
+                 uint32_t group, bool wave) {
   const int KD = shape_digits_g(k32, group);
   if (!KD) {
     c->fail("unsupported modulus width %u limbs", k32);
@@ -446,7 +446,9 @@ int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, u
     return FSDKR_E_OOM;
   }
   c->mark("mod_setup", true);
-  int rc = c->hip_check(mod_setup_g(k32, group, d_mods, n_mod, *d_consts, c->stream), "mod_setup launch");
+  int rc = c->hip_check(wave && !group ? mod_setup_wave(k32, d_mods, n_mod, *d_consts, c->stream)
+                                       : mod_setup_g(k32, group, d_mods, n_mod, *d_consts, c->stream),
+                        "mod_setup launch");
   c->mark("mod_setup", false);
   return rc;
 }

@@ -169,7 +169,10 @@ static int prestart_fb_tables(Ctx* c, const fsdkr_collect_batch* bs, uint32_t co
       (rc = c->hip_check(hipStreamSynchronize(ts), "prestart fb H2D sync")))
     return rc;
   uint32_t* cons = nullptr;
-  if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl")))
+  // the table chains are the head of the fixed-base chain (tables -> comb levels -> comb
+  // exponents): their setup runs one wave per modulus so it starts beside GA's waves
+  if ((rc = setup_moduli(c, nl, reinterpret_cast<const uint32_t*>(dev + o_mod), nmod, &cons, "collect_fbpre_nl", 0,
+                         true)))
     return rc;
   if (!g.fb_setup && (rc = c->hip_check(hipEventCreateWithFlags(&g.fb_setup, hipEventDisableTiming), "event")))
     return rc;

@@ -270,9 +270,11 @@ int launch_modexp_desc(Ctx* c, uint32_t k32, uint32_t count, uint32_t exp_bits, 
                        const uint32_t* d_consts, uint32_t* d_out, hipStream_t st = nullptr,
                        const char* table_tag = "mxtable", uint32_t prio = 0, uint32_t group = 0,
                        uint32_t desc_flags = 0, const SplitArgs* split = nullptr);
-// group: kWideGroup prepares the KD = 160 constants of the 32-lane 4096-bit shape
+// group: kWideGroup prepares the KD = 160 constants of the 32-lane 4096-bit shape;
+// wave: the same constants from one wave per modulus where the width has that shape
+// (mod_setup_wave: few VGPRs, so it is dispatched beside long-running waves)
 int setup_moduli(Ctx* c, uint32_t k32, const uint32_t* d_mods, uint32_t n_mod, uint32_t** d_consts, const char* tag,
-                 uint32_t group = 0);
+                 uint32_t group = 0, bool wave = false);
 int run_modexp_device(Ctx* c, uint32_t k32, uint32_t count, const uint32_t* d_base, const uint32_t* d_exp,
                       uint32_t exp_limbs, uint32_t exp_bits, const uint32_t* d_mod_idx, const uint32_t* d_mods,
                       uint32_t n_mod, uint32_t* d_out);

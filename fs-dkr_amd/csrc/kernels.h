@@ -65,6 +65,7 @@ constexpr uint32_t kWaveGroup = 64;
 int shape_digits_g(uint32_t k32, uint32_t group);   // digits of the Montgomery constants
 int table_digits(uint32_t k32, uint32_t group);     // words per window-table entry
 hipError_t mod_setup(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st);
+hipError_t mod_setup_wave(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st);
 hipError_t mod_setup_g(uint32_t k32, uint32_t group, const uint32_t* mods, uint32_t n_mod, uint32_t* consts,
                        hipStream_t st);
 hipError_t modexp(uint32_t k32, const ModexpArgs& a, hipStream_t st);

@@ -92,6 +92,72 @@ __global__ __launch_bounds__(BLOCK) void mod_setup_kernel(const uint32_t* __rest
   if (g == 0) out[3 * KD] = M.ninv;
 }
 
+// mod_setup_kernel's constants from one wave per modulus (Mont29<64 L, 64, KR>:
+// L digits per lane, KR = the class's digits), so the setup takes ~20 VGPRs and
+// little time: it is dispatched beside long-running throughput waves instead of
+// waiting for a whole free slot.  (The 4-lane 3072-bit group setup took 196
+// VGPRs and waited ~90 ms beside configs[4]'s GA at 2 waves/SIMD of 228 VGPRs,
+// profiles/r05/r05j_config4_trace_head.txt.)  R^2 mod N by an addition chain on
+// the exponent: x_a = 2^a R mod N, x_2a = mont(x_a, x_a), x_(a+1) = 2 x_a, from
+// a = 1 to a = 29 KR (12 squarings and a few doublings instead of 29 KR / 4
+// doublings).  Every value is exact, so the constants equal mod_setup_kernel's.
+template <int KR, int L, int K32>
+__global__ __launch_bounds__(64) void mod_setup_wave_kernel(const uint32_t* __restrict__ mods, uint32_t n_mod,
+                                                            uint32_t* __restrict__ consts) {
+  constexpr int KD = 64 * L;
+  using MT = Mont29<KD, 64, KR>;
+  constexpr bool SC = scaled_ok(KR, K32);
+  const uint32_t mi = blockIdx.x;
+  if (mi >= (SC ? 2 * n_mod : n_mod)) return;
+  const bool scaled = SC && mi >= n_mod;
+  const uint32_t m = scaled ? mi - n_mod : mi;
+  __builtin_amdgcn_s_setprio(3);
+  const int g = threadIdx.x;
+  const bool live = g * L < KR;
+  const uint32_t* N = mods + (size_t)m * K32;
+  MT M;
+  M.init_lane(g);
+#pragma unroll
+  for (int j = 0; j < L; ++j) M.n[j] = live ? digit_of(N, K32, g * L + j) : 0u;
+  const uint32_t n0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)N[0]);
+  uint32_t inv = n0;
+#pragma unroll
+  for (int it = 0; it < 5; ++it) inv *= 2u - n0 * inv;
+  M.ninv = (0u - inv) & M29;
+  if (scaled) M.scale_modulus();   // n <- N', ninv <- 1
+  int hb = -1;
+#pragma unroll
+  for (int j = 0; j < L; ++j)
+    if (M.n[j]) hb = (g * L + j) * 29 + 31 - __builtin_clz(M.n[j]);
+  hb = group_max<64>(hb);
+  uint32_t y[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) y[j] = ((g * L + j) == hb / 29) ? (1u << (hb % 29)) : 0u;   // 2^(bitlen-1) < N
+  for (int k = 0; k < 29 * KR - hb; ++k) M.dbl(y);                                     // R mod N (exact)
+  uint32_t* out = consts + (size_t)m * cons_stride(KR) + (scaled ? cons_scaled(KR) : 0);
+  if (live) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) out[KR + g * L + j] = y[j];
+  }
+  constexpr int E = 29 * KR;
+  constexpr int TOP = 31 - __builtin_clz(E);
+  M.dbl(y);   // x_1
+  for (int b = TOP - 1; b >= 0; --b) {
+    M.sqr_w(y, y);   // x_2a (almost Montgomery, < 2N)
+    M.carry_exact(y);
+    M.sub_if_ge(y);
+    if ((E >> b) & 1) M.dbl(y);   // x_(a+1)
+  }
+  if (live) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      out[g * L + j] = M.n[j];
+      out[2 * KR + g * L + j] = y[j];
+    }
+  }
+  if (g == 0) out[3 * KR] = M.ninv;
+}
+
 // dst = this lane's digits of table row d, read by scanning every row and keeping
 // row d through a mask: the addresses and the instruction stream do not depend
 // on d (a secret exponent's window digit).
@@ -673,6 +739,13 @@ __global__ __launch_bounds__(64) void modexp_wave_kernel(const ModexpArgs a) {
 }
 
 // ---- host-side launchers -------------------------------------------------------
+template <int KR, int L, int K32>
+static hipError_t launch_setup_wave(const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
+  const uint32_t waves = scaled_ok(KR, K32) ? 2 * n_mod : n_mod;
+  if (waves == 0) return hipSuccess;
+  hipLaunchKernelGGL((mod_setup_wave_kernel<KR, L, K32>), dim3(waves), dim3(64), 0, st, mods, n_mod, consts);
+  return hipGetLastError();
+}
 template <int KD, int G, int K32>
 static hipError_t launch_setup(const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
   constexpr int IPB = BLOCK / G;
@@ -723,6 +796,14 @@ static hipError_t launch_modexp_wave(const ModexpArgs& a, hipStream_t st) {
   if (a.count == 0) return hipSuccess;
   hipLaunchKernelGGL((modexp_wave_kernel<KR, L, K32>), dim3(a.count), dim3(64), 0, st, a);
   return hipGetLastError();
+}
+
+// The same constants from one wave per modulus (mod_setup_wave_kernel) where a
+// width has that shape: 3072-bit moduli.  Used for the multi-session prestart's
+// table chains, whose setup otherwise waits for a whole free slot beside GA.
+hipError_t mod_setup_wave(uint32_t k32, const uint32_t* mods, uint32_t n_mod, uint32_t* consts, hipStream_t st) {
+  if (k32 == 96) return launch_setup_wave<108, 2, 96>(mods, n_mod, consts, st);
+  return mod_setup(k32, mods, n_mod, consts, st);
 }
 
 int shape_digits(uint32_t k32) {
