@@ -265,7 +265,7 @@ __global__ void pdl_u1_kernel(const PdlU1Args a) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t p = tid >> 2, j = tid & 3u;
   if (p >= a.count) return;   // whole quads (count pairs x 4 lanes)
-  __builtin_amdgcn_s_setprio(1);   // a long serial EC chain per lane
+  __builtin_amdgcn_s_setprio(3);   // a long serial EC chain per lane on few waves: wins issue arbitration
   uint32_t k[8];
   if (j < 2) {
     bigint_mod_q(k, a.s1 + (size_t)p * a.s1_len, a.s1_len);
