@@ -144,10 +144,18 @@ struct Mont29 {
   static_assert(KD % G == 0, "KD must split evenly over the group");
   static_assert(KR == KD || (G == 64 && KR % L == 0 && KR < KD), "spare slots only in the wave shape");
   // A column spends exactly L rows in a lane and leaves it as a 29-bit digit
-  // (row(): the retired column's carry stays behind), gaining < 2^59.01 per row
-  // (< 2^59.6 in squaring rows): for L <= 24 it cannot reach 2^64 before it
-  // moves on, so only the final carry passes of mul() are needed.
-  static constexpr bool NORM_IN_CYCLE = L > 24;
+  // (row(): the retired column's carry stays behind).  Each row adds at most one
+  // a*b and one m*n product to it (< 2^58.01 each), so a product cycle adds
+  // < L 2^59.01.  A squaring row may add 2 a_r b_j instead (sq_dbl), but over the
+  // column's L rows the tournament offset d = (j - r) mod L steps by -2 per row:
+  // for odd L it takes every residue once ((L-1)/2 doubled, one raw, (L-1)/2
+  // none), for even L one parity class twice (at most L - 2 doubled units and 4
+  // raw), so the a*b part stays <= (L + 2) 2^58.01 and the column
+  // < (L + 1) 2^59.01 + 2^35 (the carry it receives as the lane's second
+  // column).  For L <= 30 that is < 2^64 (2^63.96): no carries inside the cycle,
+  // only the final carry passes of mul().  (Round 5 folded from L > 24 on the
+  // per-row worst case 2^59.6; profiles/r06/r06n_*.)
+  static constexpr bool NORM_IN_CYCLE = L > 30;
   // Longer lanes fold the column at logical position P_k into P_k + 1 once per
   // row (rolling normalisation, roll_norm), so every column is folded once per
   // fold point during its L-row stay and accumulates at most 18 rows between
@@ -239,8 +247,8 @@ struct Mont29 {
   // (L odd) or L/2 + 1 (L even) MACs per row instead of L.  A pair {r, p} is
   // issued in a row <= r + p, so the column a row retires holds the same value
   // as in the plain product: identical m digits, bit-identical results.  A
-  // column now gains < 2^59.6 per row (2 a_r < 2^30.01), so L <= 21 rows fit a
-  // 64-bit accumulator between normalisations (NSTEP <= 18, L <= 18 here).
+  // column gains < 2^59.6 in one row (2 a_r < 2^30.01), but < (L + 1) 2^59.01
+  // over its L-row stay in a lane (NORM_IN_CYCLE), as in the plain product.
   static constexpr bool sq_raw(int d) { return d == 0 || (L % 2 == 0 && d == L / 2); }
   static constexpr bool sq_dbl(int d) { return d > 0 && (L % 2 == 1 ? d <= L / 2 : d < L / 2); }
   // Short-lane group shapes (8-32 lanes) keep the doubled digits 2 b_j of a
@@ -382,7 +390,7 @@ struct Mont29 {
 
   template <bool SQ, bool QS>
   __device__ __forceinline__ void product(uint32_t* out, uint32_t* b, const uint32_t* a_lds) {
-    static_assert(!SQ || NORM_IN_CYCLE || L <= 21, "squaring rows: column bound");
+    static_assert(NORM_IN_CYCLE || L <= 30, "column bound of a product cycle (NORM_IN_CYCLE)");
     static_assert(G != 64, "the wave shape streams from registers: product_w");
     uint64_t acc[L];
 #pragma unroll
