@@ -488,6 +488,12 @@ inline uint32_t j2_lanes(size_t count, uint32_t nn) {
   return nn == 128 ? (count <= 1024 ? kWaveGroup : count <= 16384 ? 16 : 8) : 8;
 }
 
+// GA's chains per wave when they are padded to whole waves per receiver: only the
+// 4096-bit shapes have a sliding-window kernel that pads buy; the other widths
+// (configs[4]'s 6144-bit GA, 6 chains per receiver) run fixed windows, where a
+// pad is a whole duplicate chain (+33 % GA work at 8 per wave, profiles/r06/r06o_*)
+inline uint32_t ga_per_wave(uint32_t group, uint32_t nn) { return (nn == 128 && group <= 64) ? 64 / group : 0u; }
+
 // the descriptor flags of a regrouped GA job launched with `group` lanes
 inline uint32_t ga_desc_flags(bool aligned_for, uint32_t group) {
   const bool slide_shape = group == 4 || group == 8 || group == 16 || group == kWideGroup;

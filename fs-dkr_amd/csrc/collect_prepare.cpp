@@ -777,7 +777,7 @@ int collect_prepare_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) 
   // joint: J1 alone (padded, pads write row 3P), J9 its own launch in job slot 2
   const uint32_t ga_group = ga_lanes((uint32_t)(J1.size() + (pl.joint ? 0 : J9.size())), nn);
   // (pads write the first J9 row, unused when J9 is empty)
-  const uint32_t ga_pw = ga_group <= 64 ? 64 / ga_group : 0;
+  const uint32_t ga_pw = ga_per_wave(ga_group, nn);
   const uint32_t pad_row = pl.joint ? (uint32_t)(3 * P) : J9.size() ? kNoPad : (uint32_t)(2 * P);
   const bool ga_aligned = J1.size() && group_by_exponent(J1, ga_pw, pad_row) && (pl.joint || J9.size() == 0);
   ModexpJob GA = J1, GD = J7;

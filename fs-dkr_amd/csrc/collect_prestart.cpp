@@ -390,7 +390,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
                o_s = o_s2 + al((size_t)P * nl * 4), o_desc = o_s + al((size_t)P * nl * 4);
   // the lanes launch() would give GA: 32 lanes (KD = 160 constants) for the small
   // batches of a multi-GPU shard, where GA's chain latency is the critical path
-  const uint32_t group = ga_lanes(2 * P, nn), per_wave = group <= 64 ? 64 / group : 0;
+  const uint32_t group = ga_lanes(2 * P, nn), per_wave = ga_per_wave(group, nn);
   // descriptors with out_idx, for 2P chains + at most per_wave - 1 pads per receiver
   const size_t desc_bytes = ((size_t)2 * P + (size_t)n * (per_wave ? per_wave - 1 : 0)) * 36,
                o_out = o_desc + al(desc_bytes);
