@@ -23,6 +23,7 @@ void free_ga_pre(Ctx* c) {
   GaPre* g = reinterpret_cast<GaPre*>(c->ga_pre);
   if (g && g->done) (void)hipEventDestroy(g->done);
   if (g && g->ga_setup) (void)hipEventDestroy(g->ga_setup);
+  if (g && g->ga_rows_up) (void)hipEventDestroy(g->ga_rows_up);
   if (g && g->fb_done) (void)hipEventDestroy(g->fb_done);
   if (g && g->fb_setup) (void)hipEventDestroy(g->fb_setup);
   if (g && g->ck_done) (void)hipEventDestroy(g->ck_done);

@@ -380,6 +380,7 @@ struct GaPre {
   const uint8_t* ga_desc = nullptr;
   std::vector<uint32_t> ga_rows;
   hipEvent_t ga_setup = nullptr;   // GA's Montgomery constants ready (before its chains)
+  hipEvent_t ga_rows_up = nullptr;  // the pair rows and descriptors copied up (beside the moduli setup)
   const uint32_t* cons = nullptr;   // those constants (KD 160 when `wide`, else the width's KD)
   bool wide = false;
   // the fixed-base tables of h1_i, h2_i (bases 2i, 2i+1 of prepare's FbJob), built

@@ -352,38 +352,6 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
     P += R * ns;
   }
   const uint32_t nn = 2 * nl;
-  // the inputs, at each session's own width, for the match in prepare (copied in
-  // parallel chunks: 67 MB at n = 256, on the path before GA starts)
-  size_t words_n = 0, words_p = 0;
-  for (const GaPre::Sess& x : ss) {
-    words_n += (size_t)x.n * x.nl;
-    words_p += (size_t)x.R * x.n * x.nl;
-  }
-  g.recv_n.resize(words_n);
-  g.s2.resize(words_p);
-  g.s.resize(words_p);
-  {
-    struct Cp { uint32_t* dst; const uint32_t* src; size_t words; };
-    std::vector<Cp> cps;
-    size_t on = 0, op = 0;
-    constexpr size_t kChunk = 1u << 18;   // 1 MB pieces
-    auto add = [&](uint32_t* dst, const uint32_t* src, size_t words) {
-      for (size_t o = 0; o < words; o += kChunk) cps.push_back(Cp{dst + o, src + o, std::min(kChunk, words - o)});
-    };
-    for (uint32_t k = 0; k < count; ++k) {
-      const fsdkr_collect_batch* b = bs + k;
-      const GaPre::Sess& x = ss[k];
-      const size_t wn = (size_t)x.n * x.nl, wp = (size_t)x.R * x.n * x.nl;
-      add(g.recv_n.data() + on, b->recv_n, wn);
-      add(g.s2.data() + op, b->pdl_s2, wp);
-      add(g.s.data() + op, b->rp_s, wp);
-      on += wn;
-      op += wp;
-    }
-    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
-      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].words * 4);
-    });
-  }
   // image: [N^2 | N | s2 | s | descriptors], outputs after it
   auto al = Img::al;
   const size_t o_NN = 0, o_rn = al((size_t)n * nn * 4), o_s2 = o_rn + al((size_t)n * nl * 4),
@@ -432,6 +400,26 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   });
   uint32_t recvn_max = 1;
   for (uint32_t r = 0; r < n; ++r) recvn_max = std::max(recvn_max, rbits[r]);
+  // the moduli go up first and their setup starts at once; the pair rows and the
+  // descriptors are laid out and copied on another stream meanwhile, so the setup
+  // kernel is off the path to GA's first chain (round 5: one H2D, a host sync, then
+  // the setup)
+  hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
+  hipStream_t us = c->side_stream(10);  // the bulk copy (the ring-Pedersen prestart's copy stream)
+  StreamScope scope(c, gs);
+  int rc;
+  auto fail_sync = [&](int r) {   // the arena is reused by prepare: no copy may still read it
+    (void)hipStreamSynchronize(gs);
+    (void)hipStreamSynchronize(us);
+    return r;
+  };
+  if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_s2, hipMemcpyHostToDevice, gs), "prestart H2D moduli")))
+    return fail_sync(rc);
+  if ((rc = c->span_begin(gs))) return fail_sync(rc);   // the call's first device work
+  uint32_t* cons = nullptr;
+  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
+                         group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
+    return fail_sync(rc);
   for (uint32_t k = 0; k < count; ++k) {   // pair rows, zero-extended to nl
     const GaPre::Sess& x = ss[k];
     const size_t cnt = (size_t)x.R * x.n;
@@ -464,21 +452,17 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   J1.pack(desc);
   if (desc.size() > desc_bytes) {
     c->fail("fsdkr_collect_prestart: GA descriptors %zu > %zu bytes", desc.size(), desc_bytes);
-    return FSDKR_E_ARG;
+    return fail_sync(FSDKR_E_ARG);
   }
   memcpy(img + o_desc, desc.data(), desc.size());
   memset(img + o_desc + desc.size(), 0, o_out - o_desc - desc.size());
-  hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
-  StreamScope scope(c, gs);
-  int rc;
-  if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_out, hipMemcpyHostToDevice, gs), "prestart H2D")) ||
-      (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")))   // the arena is reused by prepare
-    return rc;
-  if ((rc = c->span_begin(gs))) return rc;   // the call's first device work
-  uint32_t* cons = nullptr;
-  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
-                         group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
-    return rc;
+  if (!g.ga_rows_up && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_rows_up, hipEventDisableTiming), "event")))
+    return fail_sync(rc);
+  if ((rc = c->hip_check(hipMemcpyAsync(dev + o_s2, img + o_s2, o_out - o_s2, hipMemcpyHostToDevice, us),
+                         "prestart H2D rows")) ||
+      (rc = c->hip_check(hipEventRecord(g.ga_rows_up, us), "event record")) ||
+      (rc = c->hip_check(hipStreamWaitEvent(gs, g.ga_rows_up, 0), "stream wait")))
+    return fail_sync(rc);
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
   g.cons = cons;
   g.wide = group == kWideGroup;
@@ -496,7 +480,41 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   head.lo_bit = kGaSplit;
   if ((rc = launch_modexp_desc(c, nn, (uint32_t)J1.size(), recvn_max, dev + o_desc, cons, g.out, gs, "mxt_GApre", gprio, group,
                                flags, g.split ? &head : nullptr)))
-    return rc;
+    return fail_sync(rc);
+  // the arena is reused by prepare: the copies complete before the call returns
+  if ((rc = c->hip_check(hipStreamSynchronize(us), "prestart H2D sync"))) return fail_sync(rc);
+  // the inputs, at each session's own width, for the match in prepare (copied in
+  // parallel chunks: 67 MB at n = 256; after GA's launch, off its path)
+  size_t words_n = 0, words_p = 0;
+  for (const GaPre::Sess& x : ss) {
+    words_n += (size_t)x.n * x.nl;
+    words_p += (size_t)x.R * x.n * x.nl;
+  }
+  g.recv_n.resize(words_n);
+  g.s2.resize(words_p);
+  g.s.resize(words_p);
+  {
+    struct Cp { uint32_t* dst; const uint32_t* src; size_t words; };
+    std::vector<Cp> cps;
+    size_t on = 0, op = 0;
+    constexpr size_t kChunk = 1u << 18;   // 1 MB pieces
+    auto add = [&](uint32_t* dst, const uint32_t* src, size_t words) {
+      for (size_t o = 0; o < words; o += kChunk) cps.push_back(Cp{dst + o, src + o, std::min(kChunk, words - o)});
+    };
+    for (uint32_t k = 0; k < count; ++k) {
+      const fsdkr_collect_batch* b = bs + k;
+      const GaPre::Sess& x = ss[k];
+      const size_t wn = (size_t)x.n * x.nl, wp = (size_t)x.R * x.n * x.nl;
+      add(g.recv_n.data() + on, b->recv_n, wn);
+      add(g.s2.data() + op, b->pdl_s2, wp);
+      add(g.s.data() + op, b->rp_s, wp);
+      on += wn;
+      op += wp;
+    }
+    parallel_for(cps.size(), 1, [&](size_t c0, size_t c1) {
+      for (size_t q = c0; q < c1; ++q) memcpy(cps[q].dst, cps[q].src, cps[q].words * 4);
+    });
+  }
   g.ga_group = group;
   g.ga_flags = flags;
   g.ga_count = (uint32_t)J1.size();
