@@ -388,7 +388,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   std::vector<uint32_t> rbits(n);
   std::vector<uint32_t> sess_of_recv(n);
   for (uint32_t k = 0; k < count; ++k) std::fill(sess_of_recv.begin() + ss[k].rbase, sess_of_recv.begin() + ss[k].rbase + ss[k].n, k);
-  parallel_for(n, 64, [&](size_t r0, size_t r1) {
+  parallel_for(n, 4, [&](size_t r0, size_t r1) {   // N^2 per receiver: 64 products of 2048-bit N at n = 64, ~5 us each
     for (size_t r = r0; r < r1; ++r) {
       const GaPre::Sess& x = ss[sess_of_recv[r]];
       const uint32_t* Np = bs[sess_of_recv[r]].recv_n + (r - x.rbase) * x.nl;

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace fsdkr {
@@ -198,13 +199,28 @@ inline uint32_t keyed_lanes(size_t count) {
 inline bool group_by_exponent(ModexpJob& J, uint32_t per_wave, uint32_t pad_row) {
   const size_t cnt = J.size();
   // stable order by exponent address: a counting sort over the few distinct
-  // addresses (a comparison sort of 131k instances cost ~10 ms at n = 256)
-  std::vector<uint64_t> keys(J.exp_ptr);
-  std::sort(keys.begin(), keys.end());
-  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-  std::vector<uint32_t> kid(cnt), start(keys.size() + 1, 0), ord(cnt);
+  // addresses (a comparison sort of 131k instances cost ~10 ms at n = 256).  The
+  // distinct addresses are found by hashing (first-seen ids), then only they are
+  // sorted: O(instances) on the path before GA's launch
+  std::unordered_map<uint64_t, uint32_t> seen;
+  seen.reserve(512);
+  std::vector<uint64_t> keys;
+  std::vector<uint32_t> kid(cnt), ord(cnt);
   for (size_t k = 0; k < cnt; ++k) {
-    kid[k] = (uint32_t)(std::lower_bound(keys.begin(), keys.end(), J.exp_ptr[k]) - keys.begin());
+    const auto it = seen.emplace(J.exp_ptr[k], (uint32_t)keys.size());
+    if (it.second) keys.push_back(J.exp_ptr[k]);
+    kid[k] = it.first->second;
+  }
+  std::vector<uint32_t> rank(keys.size());
+  {
+    std::vector<uint32_t> by(keys.size());
+    for (uint32_t q = 0; q < (uint32_t)by.size(); ++q) by[q] = q;
+    std::sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return keys[x] < keys[y]; });
+    for (uint32_t q = 0; q < (uint32_t)by.size(); ++q) rank[by[q]] = q;
+  }
+  std::vector<uint32_t> start(keys.size() + 1, 0);
+  for (size_t k = 0; k < cnt; ++k) {
+    kid[k] = rank[kid[k]];
     ++start[kid[k] + 1];
   }
   for (size_t q = 1; q < start.size(); ++q) start[q] += start[q - 1];
