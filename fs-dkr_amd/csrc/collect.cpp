@@ -264,4 +264,14 @@ int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verd
   return fsdkr::first_error_impl(batch, verdicts, out);
 }
 
+int fsdkr_collect_first_error_multi(const fsdkr_collect_batch* batches, const fsdkr_verdicts* verdicts, uint32_t count,
+                                    fsdkr_error* out) {
+  if (count && (!batches || !verdicts || !out)) return FSDKR_E_ARG;
+  for (uint32_t s = 0; s < count; ++s) {
+    const int rc = fsdkr::first_error_impl(batches + s, verdicts + s, out + s);
+    if (rc) return rc;
+  }
+  return FSDKR_OK;
+}
+
 }  // extern "C"

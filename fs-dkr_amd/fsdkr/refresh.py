@@ -310,9 +310,10 @@ def collect_many(sessions, ctx=None, m_security=256, key_bits=2048, recovery="sp
             for i, r in zip(live, rs or ()):
                 specs[i] = r
     errs = []
+    fe = sset.first_errors(verdicts) if sset.row else {}
     for i, (msgs, lk, dk, joins) in enumerate(sess):
-        if i in sset.row:
-            e = sset.first_error(i, verdicts)
+        if i in fe:
+            e = fe[i]
             errs.append((_error_of(e), e.keys_applied))
         else:
             errs.append(_mapped(ctx, sset.batches[i], msgs, None))

@@ -377,6 +377,13 @@ typedef struct fsdkr_error {
  * per join message index, correct-key, DLog, modulus size.  `verdicts` may be
  * NULL when the threshold or size check already fails.  Pure host logic. */
 int fsdkr_collect_first_error(const fsdkr_collect_batch* batch, const fsdkr_verdicts* verdicts, fsdkr_error* out);
+/* fsdkr_collect_first_error for `count` sessions of a multi-session batch
+ * (fsdkr_collect_prepare_multi / fsdkr_verify_collect_multi): out[s] from
+ * batches[s] and verdicts[s], in one call (each session's collect() outcome is
+ * its own, refresh_message.rs:321-467 per session).  Stops at the first session
+ * whose mapping fails and returns that code.  Pure host logic. */
+int fsdkr_collect_first_error_multi(const fsdkr_collect_batch* batches, const fsdkr_verdicts* verdicts, uint32_t count,
+                                    fsdkr_error* out);
 
 /* Fixed-base batch: out[i] = bases[base_idx[i]] ^ exp[i] mod mods[base_mod_idx[base_idx[i]]]
  * (exact).  The GPU builds one squaring chain of base^(2^(w j)) per base and

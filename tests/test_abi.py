@@ -64,3 +64,10 @@ def test_limb_roundtrip():
     lim = ints_to_limbs(vals, 64)
     assert lim.shape == (len(vals), 64) and lim.dtype == np.uint32
     assert limbs_to_ints(lim) == vals
+
+
+def test_integration_binding_matches_header():
+    """INTEGRATION.md's Rust extern block binds exactly the entry points the header declares."""
+    src = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    bound = sorted(set(re.findall(r"pub fn (fsdkr_\w+)\(", src)))
+    assert bound == _declared()
