@@ -17,6 +17,7 @@
 #                    configs[4] collect_many() calls (tools/pmc_step.py) -> pmc_step_n64.json /
 #                    pmc_step_n256.json / pmc_step_c4.json (per-call counter totals; with
 #                    tools/mac_share.py's per-kernel MAC shares of this build: pmc_mac_per_call)
+#   pmc256s8         the same over rank 0 of an emulated 8-way n = 256 shard -> pmc_step_n256s8.json
 #   pmcmx            PMC passes over the metric-2 modexp launch (tools/pmc.sh)
 #   shard256         bench.py --emulate-shard 2 / 4 / 8 at n = 256 -> shard_n256.jsonl
 #   trace256s8       kernel trace of the emulated rank 0 of an 8-way n = 256 shard -> trace256s8_summary.txt
@@ -88,6 +89,7 @@ for step in "$@"; do
                 python $R/tools/prof_summary.py "$f" --gap 40 --step -1 > $OUT/trace256s8_summary.txt || exit 1 ;;
     pmc64) pmc_step n64 --n 64 --joins 4 --t 32 ;;
     pmc256) pmc_step n256 --n 256 --joins 0 --t 128 ;;
+    pmc256s8) pmc_step n256s8 --n 256 --joins 0 --t 128 --shard 8 ;;
     pmc4) pmc_step c4 --sessions 1024 --seed 2028 ;;
     pmcmx) bash $R/tools/pmc.sh $TAG/pmcmx || exit 1 ;;
     shard256|shard64)

@@ -14,7 +14,7 @@ SMALLEST loop share is taken, a lower bound for any mix of them.  The INT64
 work outside the cycle loops (finish(), window steps) is < 1 % of a product's
 (GA's slide kernel: 18 of 2338 INT64 instructions per 4096-bit squaring), and
 is not credited; neither are the long-lane shapes' rolling-normalisation folds
-(L > 24: one v_mad_u64_u32 by 8 per fold point and row, folds_per_cycle).
+(L > 30: one v_mad_u64_u32 by 8 per fold point and row, folds_per_cycle).
 Kernels with no cycle loop (inverses, secp256k1, hashing) get their
 whole-body share of v_mad_u64_u32 among INT64 instructions.
 
@@ -86,13 +86,13 @@ GROUP_KERNELS = ("modexp_kernel", "modexp_slide_kernel", "modexp_tail_kernel", "
 
 def folds_per_cycle(name):
     """v_mad_u64_u32 of a cycle loop that are NOT products: the rolling
-    normalisation of long lanes (mont29.hpp roll_fold: L > 24, NROLL folds per
+    normalisation of long lanes (mont29.hpp NORM_IN_CYCLE: L > 30, NROLL folds per
     row, a multiply by 8 that moves a column's high word) -- L rows per cycle"""
     m = re.match(r"(\w+)<(\d+), (\d+)", name)
     if not m or m.group(1) not in GROUP_KERNELS:
         return 0
     L = int(m.group(2)) // int(m.group(3))
-    return L * ((L + 17) // 18 - 1) if L > 24 else 0
+    return L * ((L + 17) // 18 - 1) if L > 30 else 0
 
 
 def share(ins, name=""):

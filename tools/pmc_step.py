@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--sessions", type=int, default=0)
+    ap.add_argument("--shard", type=int, default=0,
+                    help="W: rank 0's shard.collect() of a W-way shard (the all-reduce replaced by the other "
+                         "ranks' all-valid verdicts, as bench.py --emulate-shard)")
     ap.add_argument("--cache", required=True)
     ap.add_argument("--gen-only", action="store_true")
     a = ap.parse_args()
@@ -54,6 +57,31 @@ def main():
         return
     msgs, joins, lk = data
     keys = [copy.deepcopy(lk) for _ in range(a.steps + 1)]
+    if a.shard:
+        from fsdkr import shard
+        R, J, n = len(msgs), len(joins), a.n
+
+        class Rank0:   # bench.py --emulate-shard's stand-in for the process group
+            class ReduceOp:
+                MAX = None
+
+            def get_world_size(self):
+                return a.shard
+
+            def get_rank(self):
+                return 0
+
+            def all_reduce(self, t, op=None):
+                P, M = R * n, R + J
+                for lo, hi, ok in ((0, P, 1), (P, 2 * P, 7), (2 * P, 3 * P, 1), (3 * P, 3 * P + 2 * M, 1),
+                                   (3 * P + 2 * M, 3 * P + 2 * M + J, 3)):
+                    t[lo:hi] = ok
+        for k in range(a.steps + 1):
+            t0 = time.perf_counter()
+            shard.collect(Rank0(), msgs, keys[k], lk.paillier_dk, joins, ctx)
+            print(f"shard collect {k} {(time.perf_counter() - t0) * 1e3:.1f} ms", flush=True)
+        print(f"calls {a.steps + 1}", flush=True)
+        return
     for k in range(a.steps + 1):
         t0 = time.perf_counter()
         refresh.collect(msgs, keys[k], lk.paillier_dk, joins, ctx=ctx)
