@@ -23,6 +23,7 @@
 #   trace256s8       kernel trace of the emulated rank 0 of an 8-way n = 256 shard -> trace256s8_summary.txt
 #   shard64          the same at n = 64                            -> shard_n64.jsonl
 #   rehearse2        bench.py --gpus 2 under torch.distributed.run, both ranks on GPU 0 (gloo) -> rehearse2.json
+#   rehearse4        the same with 4 ranks                          -> rehearse4.json
 #   anything else    run as a shell command                       -> extra.log
 # Interleaved A/B runs: tools/ab_env.sh (environment variants of one build) and
 # tools/ab_lib.sh (two builds of libfsdkr.so).
@@ -102,6 +103,10 @@ for step in "$@"; do
       FSDKR_BENCH_REHEARSE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
         --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline \
         --sessions 0 --config3-steps 1 > $OUT/rehearse2.json 2> $OUT/rehearse2.err || fail rehearse2 $? $OUT/rehearse2.err ;;
+    rehearse4)   # the same with four ranks (shard_range over 4, max over 4 ranks)
+      FSDKR_BENCH_REHEARSE=1 timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+        --master-addr 127.0.0.1 --master-port 29519 $R/bench.py --gpus 4 --steps 3 --warmup 1 --no-cpu-baseline \
+        --sessions 0 --config3-steps 1 > $OUT/rehearse4.json 2> $OUT/rehearse4.err || fail rehearse4 $? $OUT/rehearse4.err ;;
     *) timeout -k 10 600 bash -c "$step" > $OUT/extra.log 2>&1 || fail "$step" $? $OUT/extra.log ;;
   esac
   echo "step $step ok"
