@@ -21,6 +21,8 @@
 #   pmcmx            PMC passes over the metric-2 modexp launch (tools/pmc.sh)
 #   shard256         bench.py --emulate-shard 2 / 4 / 8 at n = 256 -> shard_n256.jsonl
 #   trace256s8       kernel trace of the emulated rank 0 of an 8-way n = 256 shard -> trace256s8_summary.txt
+#   trace64s8        the same for rank 0 of an 8-way n = 64 shard       -> trace64s8_summary.txt
+#   rt64s8           that rank with HIP runtime and memory-copy traces too -> rt64s8/
 #   shard64          the same at n = 64                            -> shard_n64.jsonl
 #   rehearse2        bench.py --gpus 2 under torch.distributed.run, both ranks on GPU 0 (gloo) -> rehearse2.json
 #   rehearse4        the same with 4 ranks                          -> rehearse4.json
@@ -88,6 +90,14 @@ for step in "$@"; do
                   > $OUT/trace256s8.log 2>&1) || fail trace256s8 $? $OUT/trace256s8.log
                 f=$(find $OUT/trace256s8 -name "*kernel_trace.csv" | head -1)
                 python $R/tools/prof_summary.py "$f" --gap 40 --step -1 > $OUT/trace256s8_summary.txt || exit 1 ;;
+    trace64s8) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace64s8 -o tr \
+                 -- python3 $R/bench.py --steps 4 --warmup 1 --emulate-shard 8 --gap-ms 30 --sessions 0 --config3-steps 0 \
+                 > $OUT/trace64s8.log 2>&1) || fail trace64s8 $? $OUT/trace64s8.log
+               f=$(find $OUT/trace64s8 -name "*kernel_trace.csv" | head -1)
+               python $R/tools/prof_summary.py "$f" --gap 20 --step -1 > $OUT/trace64s8_summary.txt || exit 1 ;;
+    rt64s8) (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --output-format csv \
+              -d $OUT/rt64s8 -o tr -- python3 $R/bench.py --steps 3 --warmup 1 --emulate-shard 8 --gap-ms 30 --sessions 0 \
+              --config3-steps 0 > $OUT/rt64s8.log 2>&1) || fail rt64s8 $? $OUT/rt64s8.log ;;
     pmc64) pmc_step n64 --n 64 --joins 4 --t 32 ;;
     pmc256) pmc_step n256 --n 256 --joins 0 --t 128 ;;
     pmc256s8) pmc_step n256s8 --n 256 --joins 0 --t 128 --shard 8 ;;
