@@ -404,22 +404,33 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   // descriptors are laid out and copied on another stream meanwhile, so the setup
   // kernel is off the path to GA's first chain (round 5: one H2D, a host sync, then
   // the setup)
-  hipStream_t gs = c->side_stream(0);   // GA's stream in launch()
-  hipStream_t us = c->side_stream(10);  // the bulk copy (the ring-Pedersen prestart's copy stream)
+  // the smallest batches (an 8-way n = 64 rank's 960 chains) keep round 5's order:
+  // one H2D of the whole image, then the setup; the emulated 8-way n = 64 rank
+  // 25.8 -> 21.7 ms with it, while the 4- and 2-way ranks (1 920 / 3 840 chains)
+  // ran 2-4 % faster with the split copies (profiles/r06/r06zl_*, r06zm_*)
+  const bool overlap = 2 * (size_t)P > 1024;
+  hipStream_t gs = c->side_stream(0);                          // GA's stream in launch()
+  hipStream_t us = overlap ? c->side_stream(10) : nullptr;   // the bulk copy (the ring-Pedersen prestart's copy stream)
   StreamScope scope(c, gs);
   int rc;
   auto fail_sync = [&](int r) {   // the arena is reused by prepare: no copy may still read it
     (void)hipStreamSynchronize(gs);
-    (void)hipStreamSynchronize(us);
+    if (us) (void)hipStreamSynchronize(us);
     return r;
   };
-  if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_s2, hipMemcpyHostToDevice, gs), "prestart H2D moduli")))
-    return fail_sync(rc);
-  if ((rc = c->span_begin(gs))) return fail_sync(rc);   // the call's first device work
   uint32_t* cons = nullptr;
-  if ((rc = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
-                         group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u)))
-    return fail_sync(rc);
+  auto setup = [&]() -> int {
+    int r = c->span_begin(gs);   // the call's first device work
+    if (!r)
+      r = setup_moduli(c, nn, reinterpret_cast<const uint32_t*>(dev + o_NN), n, &cons,
+                       group == kWideGroup ? "collect_ga_nn_w" : "collect_ga_nn", group == kWideGroup ? kWideGroup : 0u);
+    return r;
+  };
+  if (overlap) {
+    if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_s2, hipMemcpyHostToDevice, gs), "prestart H2D moduli")) ||
+        (rc = setup()))
+      return fail_sync(rc);
+  }
   for (uint32_t k = 0; k < count; ++k) {   // pair rows, zero-extended to nl
     const GaPre::Sess& x = ss[k];
     const size_t cnt = (size_t)x.R * x.n;
@@ -456,13 +467,19 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
   }
   memcpy(img + o_desc, desc.data(), desc.size());
   memset(img + o_desc + desc.size(), 0, o_out - o_desc - desc.size());
-  if (!g.ga_rows_up && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_rows_up, hipEventDisableTiming), "event")))
-    return fail_sync(rc);
-  if ((rc = c->hip_check(hipMemcpyAsync(dev + o_s2, img + o_s2, o_out - o_s2, hipMemcpyHostToDevice, us),
-                         "prestart H2D rows")) ||
-      (rc = c->hip_check(hipEventRecord(g.ga_rows_up, us), "event record")) ||
-      (rc = c->hip_check(hipStreamWaitEvent(gs, g.ga_rows_up, 0), "stream wait")))
-    return fail_sync(rc);
+  if (!overlap) {
+    if ((rc = c->hip_check(hipMemcpyAsync(dev, img, o_out, hipMemcpyHostToDevice, gs), "prestart H2D")) ||
+        (rc = c->hip_check(hipStreamSynchronize(gs), "prestart H2D sync")) || (rc = setup()))
+      return fail_sync(rc);
+  } else {
+    if (!g.ga_rows_up && (rc = c->hip_check(hipEventCreateWithFlags(&g.ga_rows_up, hipEventDisableTiming), "event")))
+      return fail_sync(rc);
+    if ((rc = c->hip_check(hipMemcpyAsync(dev + o_s2, img + o_s2, o_out - o_s2, hipMemcpyHostToDevice, us),
+                           "prestart H2D rows")) ||
+        (rc = c->hip_check(hipEventRecord(g.ga_rows_up, us), "event record")) ||
+        (rc = c->hip_check(hipStreamWaitEvent(gs, g.ga_rows_up, 0), "stream wait")))
+      return fail_sync(rc);
+  }
   g.out = reinterpret_cast<uint32_t*>(dev + o_out);
   g.cons = cons;
   g.wide = group == kWideGroup;
@@ -482,7 +499,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
                                flags, g.split ? &head : nullptr)))
     return fail_sync(rc);
   // the arena is reused by prepare: the copies complete before the call returns
-  if ((rc = c->hip_check(hipStreamSynchronize(us), "prestart H2D sync"))) return fail_sync(rc);
+  if (overlap && (rc = c->hip_check(hipStreamSynchronize(us), "prestart H2D sync"))) return fail_sync(rc);
   // the inputs, at each session's own width, for the match in prepare (copied in
   // parallel chunks: 67 MB at n = 256; after GA's launch, off its path)
   size_t words_n = 0, words_p = 0;
