@@ -282,6 +282,10 @@ int Ctx::sync() {
     (void)hipEventDestroy(p.e0);
   }
   pending.swap(keep);
+  // the launch checks read hipGetLastError: the best-effort timing queries above
+  // (not-ready events, pairs split over streams) must not surface as the next
+  // launch's failure
+  (void)hipGetLastError();
   return rc;
 }
 

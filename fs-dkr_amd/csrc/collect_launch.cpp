@@ -364,7 +364,10 @@ int collect_finish_impl(Ctx* c, fsdkr_verdicts* out, uint32_t count) {
   if ((rc = c->sync())) return rc;
   if (c->span_armed) {
     c->span_armed = false;
-    if (hipEventElapsedTime(&c->span_ms, c->span_beg, c->span_end) != hipSuccess) c->span_ms = -1.0f;
+    if (hipEventElapsedTime(&c->span_ms, c->span_beg, c->span_end) != hipSuccess) {
+      c->span_ms = -1.0f;
+      (void)hipGetLastError();   // best effort: not reported by the next launch check
+    }
   }
   // PDL unit test of c: c^eA witnesses it unless eA == 0 / the Alice proof was rejected early
   // (joint: unn is c's own unit flag)

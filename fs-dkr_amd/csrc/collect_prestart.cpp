@@ -551,6 +551,7 @@ int prestart_ga(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count, uint32_t*
 }
 
 int collect_prestart_impl(Ctx* c, const fsdkr_collect_batch* bs, uint32_t count) {
+  (void)hipGetLastError();   // launch checks read it: start from a clean slate
   uint32_t n = 0, P = 0;
   int rc;
   GaPre* gp = reinterpret_cast<GaPre*>(c->ga_pre);
